@@ -1,0 +1,388 @@
+// q3t_synth — writes synthetic Qwen3-TTS GGUF files (talker+code-predictor and tokenizer decoder)
+// with the exact tensor names / shapes / dtypes the reference converters emit
+// (scripts/convert_tts_to_gguf.py:42-125,289-297; scripts/convert_tokenizer_to_gguf.py:42-163,265-296).
+//
+// This is TEST/BENCH DATA tooling, not product code. No checkpoint exists in this environment
+// (SURVEY.md §8(d)), so every weight is generated from a portable counter-based hash:
+//   h   = mix(mix(seed ^ fnv1a64(name)) + index)         (mix = splitmix64 finaliser)
+//   s   = sum of four 10-bit fields of h  - 2046           (integer in [-2046, 2046], ~normal)
+//   val = center + s * 2^-e                                 (e chosen so std ~= the target sigma)
+// Every value has <= 11 significant bits, so it is EXACT in f16 and f32: the GGUF bytes are identical
+// no matter which language regenerates them.
+//
+// usage: q3t_synth <config: full|tiny> <out_dir> [seed]
+//   writes <out_dir>/qwen3-tts-0.6b-f16.gguf and <out_dir>/qwen3-tts-tokenizer-f16.gguf
+//   (the fixed file names the reference loads, src/qwen3_tts.cpp:117-118).
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+
+#define GGML_F32 0
+#define GGML_F16 1
+enum { GV_U32 = 4, GV_F32 = 6, GV_STR = 8, GV_ARR = 9 };
+
+static uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static uint64_t fnv1a64(const char *s) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (; *s; ++s) { h ^= (uint8_t)*s; h *= 0x100000001b3ull; }
+    return h;
+}
+
+typedef struct {
+    const char *name;
+    int text_vocab, text_dim, hidden, n_layers, n_heads, n_kv, head_dim, inter, codec_vocab, n_codebooks;
+    int cp_layers, cp_vocab;
+    float eps, rope_theta;
+    int tts_bos, tts_eos, tts_pad;
+    int cb_size, cb_dim, voc_hidden, voc_latent, voc_layers, voc_heads, voc_ffn, dec_dim;
+    int up_ratio, convnext_mult;
+    int rates[4];
+} cfg_t;
+
+static const cfg_t CFG_FULL = {
+    "full", 151936, 2048, 1024, 28, 16, 8, 128, 3072, 3072, 16,
+    5, 2048, 1e-6f, 1000000.0f, 151672, 151673, 151671,
+    2048, 256, 512, 1024, 8, 16, 1024, 1536, 2, 4, {8, 5, 4, 3}};
+static const cfg_t CFG_TINY = {
+    "tiny", 1024, 128, 256, 5, 4, 2, 64, 512, 3072, 16,
+    5, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
+    2048, 32, 64, 128, 2, 2, 128, 96, 2, 4, {8, 5, 4, 3}};
+
+// ---------------------------------------------------------------- tensor catalogue
+typedef struct {
+    char name[96];
+    int ndims;
+    int64_t ne[4];
+    int type;
+    float center;
+    int e;  // value = center + s * 2^-e
+    uint64_t off;
+} tens_t;
+
+static tens_t *g_t = NULL;
+static int g_nt = 0, g_cap = 0;
+
+static int exp_for_sigma(double sigma) {
+    // std of s (sum of 4 uniform 10-bit ints) = sqrt(4 * (1024^2-1)/12) = 591.3
+    int e = (int)lround(log2(591.3 / sigma));
+    if (e < 0) e = 0;
+    if (e > 24) e = 24;
+    return e;
+}
+
+static void add_t(const char *name, int ndims, int64_t n0, int64_t n1, int64_t n2, double center, double sigma) {
+    if (g_nt == g_cap) { g_cap = g_cap ? g_cap * 2 : 256; g_t = realloc(g_t, sizeof(tens_t) * g_cap); }
+    tens_t *t = &g_t[g_nt++];
+    memset(t, 0, sizeof(*t));
+    snprintf(t->name, sizeof(t->name), "%s", name);
+    t->ndims = ndims;
+    t->ne[0] = n0; t->ne[1] = n1; t->ne[2] = n2; t->ne[3] = 1;
+    // dtype policy of the converters: 1-D -> F32, >=2-D -> F16
+    t->type = ndims <= 1 ? GGML_F32 : GGML_F16;
+    t->center = (float)center;
+    t->e = exp_for_sigma(sigma);
+}
+static void add1(const char *n, int64_t a, double c, double s) { add_t(n, 1, a, 1, 1, c, s); }
+// 2-D linear weight PyTorch [out, in] -> ggml ne [in, out]
+static void addw(const char *n, int64_t out, int64_t in, double gain) { add_t(n, 2, in, out, 1, 0.0, gain / sqrt((double)in)); }
+// conv1d weight PyTorch [oc, ic, k] -> ne [k, ic, oc]
+static void addconv(const char *n, int64_t oc, int64_t ic, int64_t k, double gain) {
+    add_t(n, 3, k, ic, oc, 0.0, gain / sqrt((double)(ic * k)));
+}
+
+static void build_talker(const cfg_t *c) {
+    char b[96];
+    const int H = c->hidden, Dq = c->n_heads * c->head_dim, Dkv = c->n_kv * c->head_dim;
+    addw("talker.text_embd.weight", c->text_vocab, c->text_dim, 0.02 * sqrt((double)c->text_dim));
+    addw("talker.text_proj.fc1.weight", c->text_dim, c->text_dim, 1.0);
+    add1("talker.text_proj.fc1.bias", c->text_dim, 0.0, 0.02);
+    addw("talker.text_proj.fc2.weight", H, c->text_dim, 1.0);
+    add1("talker.text_proj.fc2.bias", H, 0.0, 0.02);
+    addw("talker.codec_embd.weight", c->codec_vocab, H, 0.02 * sqrt((double)H) * 8.0);
+    addw("talker.codec_head.weight", c->codec_vocab, H, 4.0);
+    add1("talker.output_norm.weight", H, 1.0, 0.1);
+    for (int L = 0; L < 2; ++L) {
+        const int nl = L == 0 ? c->n_layers : c->cp_layers;
+        const char *p = L == 0 ? "talker" : "code_pred";
+        for (int i = 0; i < nl; ++i) {
+#define NM(suf) (snprintf(b, sizeof b, "%s.blk.%d.%s", p, i, suf), b)
+            add1(NM("attn_norm.weight"), H, 1.0, 0.1);
+            addw(NM("attn_q.weight"), Dq, H, 1.0);
+            addw(NM("attn_k.weight"), Dkv, H, 1.0);
+            addw(NM("attn_v.weight"), Dkv, H, 1.0);
+            addw(NM("attn_output.weight"), H, Dq, 0.5);
+            add1(NM("attn_q_norm.weight"), c->head_dim, 1.0, 0.1);
+            add1(NM("attn_k_norm.weight"), c->head_dim, 1.0, 0.1);
+            add1(NM("ffn_norm.weight"), H, 1.0, 0.1);
+            addw(NM("ffn_gate.weight"), c->inter, H, 1.0);
+            addw(NM("ffn_up.weight"), c->inter, H, 1.0);
+            addw(NM("ffn_down.weight"), H, c->inter, 0.5);
+#undef NM
+        }
+    }
+    add1("code_pred.output_norm.weight", H, 1.0, 0.1);
+    for (int i = 0; i < c->n_codebooks - 1; ++i) {
+        snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
+        addw(b, c->cp_vocab, H, 0.02 * sqrt((double)H) * 8.0);
+        snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
+        addw(b, c->cp_vocab, H, 4.0);
+    }
+}
+
+static void build_tokenizer(const cfg_t *c) {
+    char b[128];
+    const int CD = c->cb_dim, VH = c->voc_hidden, LAT = c->voc_latent;
+    add_t("tok_dec.vq_first.0.codebook", 2, CD, c->cb_size, 1, 0.0, 1.0);
+    add_t("tok_dec.vq_first.input_proj.weight", 3, 1, VH, CD, 0.0, 1.0 / sqrt((double)VH));
+    add_t("tok_dec.vq_first.output_proj.weight", 3, 1, CD, VH, 0.0, 1.0 / sqrt((double)CD));
+    for (int i = 0; i < c->n_codebooks - 1; ++i) {
+        snprintf(b, sizeof b, "tok_dec.vq_rest.%d.codebook", i);
+        add_t(b, 2, CD, c->cb_size, 1, 0.0, 1.0);
+    }
+    add_t("tok_dec.vq_rest.input_proj.weight", 3, 1, VH, CD, 0.0, 1.0 / sqrt((double)VH));
+    add_t("tok_dec.vq_rest.output_proj.weight", 3, 1, CD, VH, 0.0, 0.25 / sqrt((double)CD));
+    addconv("tok_dec.pre_conv.weight", LAT, VH, 3, 1.0);
+    add1("tok_dec.pre_conv.bias", LAT, 0.0, 0.02);
+    addw("tok_dec.pre_tfm.input_proj.weight", VH, LAT, 1.0);
+    add1("tok_dec.pre_tfm.input_proj.bias", VH, 0.0, 0.02);
+    for (int i = 0; i < c->voc_layers; ++i) {
+#define NM(suf) (snprintf(b, sizeof b, "tok_dec.pre_tfm.blk.%d.%s", i, suf), b)
+        add1(NM("attn_norm.weight"), VH, 1.0, 0.1);
+        addw(NM("attn_q.weight"), LAT, VH, 1.0);
+        addw(NM("attn_k.weight"), LAT, VH, 1.0);
+        addw(NM("attn_v.weight"), LAT, VH, 1.0);
+        addw(NM("attn_output.weight"), VH, LAT, 1.0);
+        add1(NM("attn_scale"), VH, 0.25, 0.05);
+        add1(NM("ffn_norm.weight"), VH, 1.0, 0.1);
+        addw(NM("ffn_gate.weight"), c->voc_ffn, VH, 1.0);
+        addw(NM("ffn_up.weight"), c->voc_ffn, VH, 1.0);
+        addw(NM("ffn_down.weight"), VH, c->voc_ffn, 1.0);
+        add1(NM("ffn_scale"), VH, 0.25, 0.05);
+#undef NM
+    }
+    add1("tok_dec.pre_tfm.norm.weight", VH, 1.0, 0.1);
+    addw("tok_dec.pre_tfm.output_proj.weight", LAT, VH, 1.0);
+    add1("tok_dec.pre_tfm.output_proj.bias", LAT, 0.0, 0.02);
+    for (int u = 0; u < 2; ++u) {
+#define NM(suf) (snprintf(b, sizeof b, "tok_dec.upsample.%d.%s", u, suf), b)
+        // ConvTranspose1d weight PyTorch [ic, oc, k] -> ne [k, oc, ic]
+        add_t(NM("conv.weight"), 3, c->up_ratio, LAT, LAT, 0.0, 1.0 / sqrt((double)LAT));
+        add1(NM("conv.bias"), LAT, 0.0, 0.02);
+        add_t(NM("dwconv.weight"), 3, 7, 1, LAT, 0.0, 1.0 / sqrt(7.0));
+        add1(NM("dwconv.bias"), LAT, 0.0, 0.02);
+        add1(NM("norm.weight"), LAT, 1.0, 0.1);
+        add1(NM("norm.bias"), LAT, 0.0, 0.02);
+        addw(NM("pwconv1.weight"), c->convnext_mult * LAT, LAT, 1.0);
+        add1(NM("pwconv1.bias"), c->convnext_mult * LAT, 0.0, 0.02);
+        addw(NM("pwconv2.weight"), LAT, c->convnext_mult * LAT, 1.0);
+        add1(NM("pwconv2.bias"), LAT, 0.0, 0.02);
+        add1(NM("gamma"), LAT, 0.25, 0.05);
+#undef NM
+    }
+    addconv("tok_dec.dec.0.conv.weight", c->dec_dim, LAT, 7, 1.0);
+    add1("tok_dec.dec.0.conv.bias", c->dec_dim, 0.0, 0.02);
+    int ch = c->dec_dim;
+    for (int d = 1; d <= 4; ++d) {
+        const int r = c->rates[d - 1], oc = ch / 2;
+#define NM(suf) (snprintf(b, sizeof b, "tok_dec.dec.%d.%s", d, suf), b)
+        add1(NM("snake.alpha"), ch, 0.0, 0.1);
+        add1(NM("snake.beta"), ch, 0.0, 0.1);
+        add_t(NM("conv_t.weight"), 3, 2 * r, oc, ch, 0.0, 1.0 / sqrt((double)ch * 2.0));
+        add1(NM("conv_t.bias"), oc, 0.0, 0.02);
+#undef NM
+        for (int ri = 2; ri <= 4; ++ri) {
+#define NM(suf) (snprintf(b, sizeof b, "tok_dec.dec.%d.res.%d.%s", d, ri, suf), b)
+            add1(NM("act1.alpha"), oc, 0.0, 0.1);
+            add1(NM("act1.beta"), oc, 0.0, 0.1);
+            addconv(NM("conv1.weight"), oc, oc, 7, 1.0);
+            add1(NM("conv1.bias"), oc, 0.0, 0.02);
+            add1(NM("act2.alpha"), oc, 0.0, 0.1);
+            add1(NM("act2.beta"), oc, 0.0, 0.1);
+            addconv(NM("conv2.weight"), oc, oc, 1, 0.35);
+            add1(NM("conv2.bias"), oc, 0.0, 0.02);
+#undef NM
+        }
+        ch = oc;
+    }
+    add1("tok_dec.dec.5.snake.alpha", ch, 0.0, 0.1);
+    add1("tok_dec.dec.5.snake.beta", ch, 0.0, 0.1);
+    addconv("tok_dec.dec.6.conv.weight", 1, ch, 7, 0.3);
+    add1("tok_dec.dec.6.conv.bias", 1, 0.0, 0.002);
+}
+
+// ---------------------------------------------------------------- GGUF v3 writer
+static void w_u32(FILE *f, uint32_t v) { fwrite(&v, 4, 1, f); }
+static void w_u64(FILE *f, uint64_t v) { fwrite(&v, 8, 1, f); }
+static void w_str(FILE *f, const char *s) { w_u64(f, strlen(s)); fwrite(s, 1, strlen(s), f); }
+
+typedef struct { const char *key; int type; uint32_t u; float fl; const char *s; int arr_n; const int *arr; } kv_t;
+
+static uint16_t f32_to_f16_rne(float x) {
+    uint32_t u; memcpy(&u, &x, 4);
+    uint32_t sign = (u >> 16) & 0x8000u;
+    int32_t exp = (int32_t)((u >> 23) & 0xff) - 127 + 15;
+    uint32_t mant = u & 0x7fffffu;
+    if (((u >> 23) & 0xff) == 0xff) return (uint16_t)(sign | 0x7c00u | (mant ? 0x200u : 0));
+    if (exp >= 31) return (uint16_t)(sign | 0x7c00u);
+    if (exp <= 0) {
+        if (exp < -10) return (uint16_t)sign;
+        mant |= 0x800000u;
+        int shift = 14 - exp;
+        uint32_t half = 1u << (shift - 1);
+        uint32_t r = mant >> shift, rem = mant & ((1u << shift) - 1);
+        if (rem > half || (rem == half && (r & 1))) r++;
+        return (uint16_t)(sign | r);
+    }
+    uint32_t r = mant >> 13, rem = mant & 0x1fffu;
+    uint32_t h = sign | ((uint32_t)exp << 10) | r;
+    if (rem > 0x1000u || (rem == 0x1000u && (r & 1))) h++;
+    return (uint16_t)h;
+}
+
+static float synth_value(uint64_t base, uint64_t i, float center, int e) {
+    uint64_t h = mix64(base + i);
+    int s = (int)(h & 1023) + (int)((h >> 10) & 1023) + (int)((h >> 20) & 1023) + (int)((h >> 30) & 1023) - 2046;
+    return center + ldexpf((float)s, -e);
+}
+
+static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed) {
+    FILE *f = fopen(path, "wb");
+    if (!f) { perror(path); return 1; }
+    const uint64_t align = 32;
+    uint64_t off = 0;
+    for (int i = 0; i < g_nt; ++i) {
+        tens_t *t = &g_t[i];
+        g_t[i].off = off;
+        uint64_t n = (uint64_t)t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
+        off += n * (t->type == GGML_F16 ? 2 : 4);
+        off = (off + align - 1) / align * align;
+    }
+    fwrite("GGUF", 1, 4, f);
+    w_u32(f, 3);
+    w_u64(f, (uint64_t)g_nt);
+    w_u64(f, (uint64_t)nkv);
+    for (int i = 0; i < nkv; ++i) {
+        w_str(f, kvs[i].key);
+        w_u32(f, (uint32_t)kvs[i].type);
+        if (kvs[i].type == GV_U32) w_u32(f, kvs[i].u);
+        else if (kvs[i].type == GV_F32) fwrite(&kvs[i].fl, 4, 1, f);
+        else if (kvs[i].type == GV_STR) w_str(f, kvs[i].s);
+        else if (kvs[i].type == GV_ARR) {
+            w_u32(f, GV_U32 + 1);  // INT32 array
+            w_u64(f, (uint64_t)kvs[i].arr_n);
+            for (int j = 0; j < kvs[i].arr_n; ++j) w_u32(f, (uint32_t)kvs[i].arr[j]);
+        }
+    }
+    for (int i = 0; i < g_nt; ++i) {
+        tens_t *t = &g_t[i];
+        w_str(f, t->name);
+        w_u32(f, (uint32_t)t->ndims);
+        for (int d = 0; d < t->ndims; ++d) w_u64(f, (uint64_t)t->ne[d]);
+        w_u32(f, (uint32_t)t->type);
+        w_u64(f, t->off);
+    }
+    long pos = ftell(f);
+    long pad = (long)((pos + align - 1) / align * align) - pos;
+    static const char zeros[64] = {0};
+    fwrite(zeros, 1, (size_t)pad, f);
+    const uint64_t data_start = (uint64_t)ftell(f);
+    const size_t CH = 1 << 22;
+    void *buf = malloc(CH * 4);
+    for (int i = 0; i < g_nt; ++i) {
+        tens_t *t = &g_t[i];
+        fseek(f, (long)(data_start + t->off), SEEK_SET);
+        const uint64_t n = (uint64_t)t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
+        const uint64_t base = mix64(seed ^ fnv1a64(t->name));
+        for (uint64_t s0 = 0; s0 < n; s0 += CH) {
+            const uint64_t m = (n - s0) < CH ? (n - s0) : CH;
+            if (t->type == GGML_F16) {
+                uint16_t *o = (uint16_t *)buf;
+#pragma omp parallel for schedule(static)
+                for (int64_t j = 0; j < (int64_t)m; ++j) o[j] = f32_to_f16_rne(synth_value(base, s0 + j, t->center, t->e));
+                fwrite(o, 2, m, f);
+            } else {
+                float *o = (float *)buf;
+#pragma omp parallel for schedule(static)
+                for (int64_t j = 0; j < (int64_t)m; ++j) o[j] = synth_value(base, s0 + j, t->center, t->e);
+                fwrite(o, 4, m, f);
+            }
+        }
+    }
+    // pad file end to alignment
+    fseek(f, 0, SEEK_END);
+    pos = ftell(f);
+    pad = (long)((pos + align - 1) / align * align) - pos;
+    fwrite(zeros, 1, (size_t)pad, f);
+    free(buf);
+    fclose(f);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 3) { fprintf(stderr, "usage: %s full|tiny <out_dir> [seed]\n", argv[0]); return 2; }
+    const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : NULL;
+    if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
+    uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
+    char path[4096];
+
+    build_talker(c);
+    kv_t kt[] = {
+        {"general.architecture", GV_STR, 0, 0, "qwen3-tts", 0, 0},
+        {"general.name", GV_STR, 0, 0, c->name, 0, 0},
+        {"general.file_type", GV_U32, 1, 0, 0, 0, 0},
+        {"qwen3-tts.block_count", GV_U32, (uint32_t)c->n_layers, 0, 0, 0, 0},
+        {"qwen3-tts.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
+        {"qwen3-tts.feed_forward_length", GV_U32, (uint32_t)c->inter, 0, 0, 0, 0},
+        {"qwen3-tts.attention.head_count", GV_U32, (uint32_t)c->n_heads, 0, 0, 0, 0},
+        {"qwen3-tts.attention.head_count_kv", GV_U32, (uint32_t)c->n_kv, 0, 0, 0, 0},
+        {"qwen3-tts.attention.key_length", GV_U32, (uint32_t)c->head_dim, 0, 0, 0, 0},
+        {"qwen3-tts.attention.value_length", GV_U32, (uint32_t)c->head_dim, 0, 0, 0, 0},
+        {"qwen3-tts.rope.freq_base", GV_F32, 0, c->rope_theta, 0, 0, 0},
+        {"qwen3-tts.attention.layer_norm_rms_epsilon", GV_F32, 0, c->eps, 0, 0, 0},
+        {"qwen3-tts.vocab_size", GV_U32, (uint32_t)c->codec_vocab, 0, 0, 0, 0},
+        {"qwen3-tts.text_vocab_size", GV_U32, (uint32_t)c->text_vocab, 0, 0, 0, 0},
+        {"qwen3-tts.text_hidden_size", GV_U32, (uint32_t)c->text_dim, 0, 0, 0, 0},
+        {"qwen3-tts.num_code_groups", GV_U32, (uint32_t)c->n_codebooks, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.layer_count", GV_U32, (uint32_t)c->cp_layers, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.vocab_size", GV_U32, (uint32_t)c->cp_vocab, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.feed_forward_length", GV_U32, (uint32_t)c->inter, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.attention.head_count", GV_U32, (uint32_t)c->n_heads, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.attention.head_count_kv", GV_U32, (uint32_t)c->n_kv, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.attention.key_length", GV_U32, (uint32_t)c->head_dim, 0, 0, 0, 0},
+        {"qwen3-tts.codec.pad_id", GV_U32, 2148, 0, 0, 0, 0},
+        {"qwen3-tts.codec.bos_id", GV_U32, 2149, 0, 0, 0, 0},
+        {"qwen3-tts.codec.eos_id", GV_U32, 2150, 0, 0, 0, 0},
+        {"qwen3-tts.tts_bos_token_id", GV_U32, (uint32_t)c->tts_bos, 0, 0, 0, 0},
+        {"qwen3-tts.tts_eos_token_id", GV_U32, (uint32_t)c->tts_eos, 0, 0, 0, 0},
+        {"qwen3-tts.tts_pad_token_id", GV_U32, (uint32_t)c->tts_pad, 0, 0, 0, 0},
+    };
+    snprintf(path, sizeof path, "%s/qwen3-tts-0.6b-f16.gguf", argv[2]);
+    if (write_gguf(path, kt, (int)(sizeof kt / sizeof kt[0]), seed)) return 1;
+
+    g_nt = 0;
+    build_tokenizer(c);
+    kv_t kk[] = {
+        {"general.architecture", GV_STR, 0, 0, "qwen3-tts-tokenizer", 0, 0},
+        {"general.name", GV_STR, 0, 0, c->name, 0, 0},
+        {"qwen3-tts-tokenizer.num_codebooks", GV_U32, (uint32_t)c->n_codebooks, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.codebook_size", GV_U32, (uint32_t)c->cb_size, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.sample_rate", GV_U32, 24000, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.decoder.hidden_size", GV_U32, (uint32_t)c->voc_hidden, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.decoder.num_layers", GV_U32, (uint32_t)c->voc_layers, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.decoder.num_heads", GV_U32, (uint32_t)c->voc_heads, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.decoder.latent_dim", GV_U32, (uint32_t)c->voc_latent, 0, 0, 0, 0},
+        {"qwen3-tts-tokenizer.upsample_rates", GV_ARR, 0, 0, 0, 4, c->rates},
+    };
+    snprintf(path, sizeof path, "%s/qwen3-tts-tokenizer-f16.gguf", argv[2]);
+    if (write_gguf(path, kk, (int)(sizeof kk / sizeof kk[0]), seed ^ 0x70CE11ull)) return 1;
+    return 0;
+}
