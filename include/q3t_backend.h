@@ -1,0 +1,101 @@
+/* q3t_backend.h — C ABI of the MI355X-native Qwen3-TTS decode path (libq3t.so).
+ *
+ * Plain pointers and sizes only; every call returns Q3T_OK (0) or Q3T_ERR (-1) and leaves a message in the
+ * thread-local q3t_last_error() (the reference's `bool` + get_error() convention, src/tts_transformer.h:244,
+ * src/trt_code_predictor.h:85).  One q3t_ctx per GPU; calls on one context are not thread-safe, contexts on
+ * different devices may be driven by different host threads.  All buffers below are HOST buffers unless the
+ * name says _dev; the hot path keeps everything resident in HBM between calls.
+ *
+ * Interfaces replaced (reference file:line):
+ *   q3t_ctx_create        TTSTransformer::load_model (src/tts_transformer.h:170, .cpp:51) +
+ *                         AudioTokenizerDecoder::load_model (src/audio_tokenizer_decoder.h:165) +
+ *                         TRTCodePredictor::load_engine/upload_* (src/trt_code_predictor.h:31-50)
+ *   q3t_generate          TTSTransformer::generate (src/tts_transformer.h:233-241, .cpp:2342-2574)
+ *   q3t_talker_forward    TTSTransformer::forward_step (src/tts_transformer.h:189-192, .cpp:1952-2028)
+ *   q3t_codepred_frame    TTSTransformer::predict_codes_autoregressive (src/tts_transformer.h:203-207) /
+ *                         TRTCodePredictor::run_greedy_loop / run_sampling_loop (src/trt_code_predictor.h:68-79)
+ *   q3t_cb0_select        CB0 logit processing inside generate (src/tts_transformer.cpp:2417-2499)
+ *   q3t_project_text      TTSTransformer::project_text_tokens (src/tts_transformer.cpp:1026-1091)
+ *   q3t_prefill_embd      TTSTransformer::build_prefill_graph (src/tts_transformer.cpp:1093-1231)
+ *   q3t_vocoder_decode    AudioTokenizerDecoder::decode (src/audio_tokenizer_decoder.h:173-174) [FULL] and
+ *                         TRTVocoderDecoder::decode (src/trt_vocoder.h:33-34) [CHUNK40]
+ *   gpu_*                 the four extern "C" wrappers of src/trt_cuda_kernels.cu:10,60,78,183
+ */
+#ifndef Q3T_BACKEND_H
+#define Q3T_BACKEND_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define Q3T_OK 0
+#define Q3T_ERR (-1)
+#define Q3T_VOCODER_FULL 0    /* whole utterance, GGML decoder semantics */
+#define Q3T_VOCODER_CHUNK40 1 /* independent 40-frame chunks, 1920 samples/frame (TRT streaming) */
+
+typedef struct q3t_ctx q3t_ctx;
+
+typedef struct q3t_config {
+    int32_t hidden, n_layers, n_heads, n_kv_heads, head_dim, intermediate;
+    int32_t codec_vocab, n_codebooks, text_vocab, text_dim, cp_layers, cp_vocab;
+    int32_t codec_eos, has_vocoder, sample_rate, max_slots, max_ctx;
+} q3t_config;
+
+/* tts_params (src/qwen3_tts.h:18-43) + generate() arguments; top_p / n_threads are unused by the reference */
+typedef struct q3t_gen_params {
+    int32_t max_len;            /* max_audio_tokens (frames), default 4096 */
+    int32_t language_id;        /* 2050 (english) as passed by synthesize_internal, qwen3_tts.cpp:459-463 */
+    float repetition_penalty;   /* 1.05 */
+    float temperature;          /* 0.9; <= 0 => greedy */
+    int32_t top_k;              /* 50 */
+    uint64_t seed;              /* counter-based sampler seed (the reference seeds std::mt19937 from random_device) */
+    int32_t force_frames;       /* bench only: EOS masked until this many frames (0 = off) */
+} q3t_gen_params;
+
+const char *q3t_last_error(void);
+void q3t_default_params(q3t_gen_params *p);
+
+int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf /* may be NULL: no vocoder */, int device,
+                   int max_slots, int max_ctx, q3t_ctx **out);
+void q3t_ctx_destroy(q3t_ctx *ctx);
+int q3t_get_config(const q3t_ctx *ctx, q3t_config *out);
+
+/* ---- hot path: prefill + frame loop for n_utt utterances batched in lock-step.
+ * tokens[u] -> n_tokens[u] chat-template ids; speaker[u] -> hidden floats or speaker == NULL (all or none).
+ * codes: [n_utt][p->max_len][16] int32 row-major [frame][codebook]; n_frames[u] = frames produced. */
+int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
+                 const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames);
+/* device time (ms) of the last q3t_generate: prefill and frame loop */
+int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms);
+
+/* ---- vocoder */
+int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);
+int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, int32_t n_frames, int mode,
+                       float *pcm /* [q3t_vocoder_num_samples] */, int64_t *n_samples);
+
+/* ---- stage entry points (used by the parity tests; each syncs the context stream) */
+int q3t_talker_forward(q3t_ctx *ctx, int n_slots, const float *embd /* [n][H] */, const int32_t *pos /* [n] */,
+                       float *hidden /* [n][H] or NULL */, float *logits /* [n][codec_vocab] or NULL */);
+int q3t_codepred_frame(q3t_ctx *ctx, int n_slots, const float *hidden /* [n][H] */, const int32_t *cb0 /* [n] */,
+                       float temperature, int32_t top_k, uint64_t seed, int32_t frame,
+                       int32_t *codes15 /* [n][15] */, float *logits /* [n][15][cp_vocab] or NULL */);
+int q3t_cb0_select(q3t_ctx *ctx, int n_slots, const float *logits /* [n][V] */, const uint8_t *seen /* [n][V] */,
+                   const int32_t *frame, const int32_t *n_tokens, const q3t_gen_params *p, int32_t *tokens);
+int q3t_project_text(q3t_ctx *ctx, int n, const int32_t *tokens, float *out /* [n][H] */);
+int q3t_prefill_embd(q3t_ctx *ctx, const int32_t *tokens, int n, const float *speaker, int language_id,
+                     float *prefill /* [10][H] */, int32_t *prefill_len, float *trailing /* [max(1,n-8)][H] */,
+                     int32_t *trailing_len, float *tts_pad /* [H] */);
+
+/* ---- drop-in replacements of src/trt_cuda_kernels.cu (device pointers, stream = hipStream_t or NULL) */
+void gpu_fp32_to_fp16(const float *in, void *out, int n, void *stream);
+void gpu_argmax_f32(const float *in, int32_t *out, int n, void *stream);
+void gpu_embedding_lookup_by_gpu_id(const int32_t *token_id_ptr, const float *table, float *output, int embd_dim,
+                                    void *stream);
+void gpu_sample_topk_f32(const float *logits, const float *rand_val, int32_t *out, float temperature, int32_t top_k,
+                         int32_t vocab_size, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* Q3T_BACKEND_H */

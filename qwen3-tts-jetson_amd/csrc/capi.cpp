@@ -1,0 +1,180 @@
+// capi.cpp — extern "C" boundary (include/q3t_backend.h).  No exception crosses it.
+#include "../../include/q3t_backend.h"
+
+#include <exception>
+
+#include "engine.h"
+#include "vocoder.h"
+
+struct q3t_ctx {
+    q3t::Engine engine;
+};
+
+namespace {
+q3t::GenParams to_gp(const q3t_gen_params *p) {
+    q3t::GenParams g;
+    if (!p) return g;
+    g.max_len = p->max_len;
+    g.language_id = p->language_id;
+    g.rep_penalty = p->repetition_penalty;
+    g.temperature = p->temperature;
+    g.top_k = p->top_k;
+    g.seed = p->seed;
+    g.force_frames = p->force_frames;
+    return g;
+}
+#define GUARD_BEGIN try {
+#define GUARD_END                                                   \
+    }                                                               \
+    catch (const std::exception &e) {                               \
+        q3t::set_error(std::string("exception: ") + e.what());      \
+        return Q3T_ERR;                                             \
+    }                                                               \
+    catch (...) {                                                   \
+        q3t::set_error("unknown exception");                        \
+        return Q3T_ERR;                                             \
+    }
+#define CHECK_CTX(c) if (!(c)) { q3t::set_error("null context"); return Q3T_ERR; }
+}  // namespace
+
+extern "C" {
+
+const char *q3t_last_error(void) { return q3t::last_error().c_str(); }
+
+void q3t_default_params(q3t_gen_params *p) {
+    if (!p) return;
+    p->max_len = 4096;
+    p->language_id = 2050;
+    p->repetition_penalty = 1.05f;
+    p->temperature = 0.9f;
+    p->top_k = 50;
+    p->seed = 0;
+    p->force_frames = 0;
+}
+
+int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf, int device, int max_slots, int max_ctx, q3t_ctx **out) {
+    GUARD_BEGIN
+    if (!out || !tts_gguf) { q3t::set_error("null argument"); return Q3T_ERR; }
+    *out = nullptr;
+    q3t_ctx *c = new q3t_ctx();
+    if (!c->engine.load(tts_gguf, tokenizer_gguf ? tokenizer_gguf : "", device, max_slots, max_ctx)) {
+        delete c;
+        return Q3T_ERR;
+    }
+    *out = c;
+    return Q3T_OK;
+    GUARD_END
+}
+
+void q3t_ctx_destroy(q3t_ctx *ctx) { delete ctx; }
+
+int q3t_get_config(const q3t_ctx *ctx, q3t_config *o) {
+    CHECK_CTX(ctx);
+    if (!o) { q3t::set_error("null argument"); return Q3T_ERR; }
+    const q3t::Config &c = ctx->engine.cfg();
+    o->hidden = c.hidden; o->n_layers = c.n_layers; o->n_heads = c.n_heads; o->n_kv_heads = c.n_kv;
+    o->head_dim = c.head_dim; o->intermediate = c.inter; o->codec_vocab = c.codec_vocab; o->n_codebooks = c.n_codebooks;
+    o->text_vocab = c.text_vocab; o->text_dim = c.text_dim; o->cp_layers = c.cp_layers; o->cp_vocab = c.cp_vocab;
+    o->codec_eos = c.codec_eos;
+    q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();
+    o->has_vocoder = v && v->loaded() ? 1 : 0;
+    o->sample_rate = 24000;
+    o->max_slots = ctx->engine.max_slots();
+    o->max_ctx = ctx->engine.max_ctx();
+    return Q3T_OK;
+}
+
+int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens, const float *const *speaker,
+                 const q3t_gen_params *p, int32_t *codes, int32_t *n_frames) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.generate(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms) {
+    CHECK_CTX(ctx);
+    if (prefill_ms) *prefill_ms = ctx->engine.last_prefill_ms;
+    if (frames_ms) *frames_ms = ctx->engine.last_frames_ms;
+    return Q3T_OK;
+}
+
+int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode) {
+    if (!ctx) return -1;
+    q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();
+    if (!v || !v->loaded()) return -1;
+    return v->n_samples(n_frames, mode);
+}
+
+int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes, int32_t n_frames, int mode, float *pcm, int64_t *n_samples) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::Vocoder *v = ctx->engine.vocoder();
+    if (!v || !v->loaded()) { q3t::set_error("vocoder not loaded (no tokenizer GGUF given)"); return Q3T_ERR; }
+    if (mode != Q3T_VOCODER_FULL && mode != Q3T_VOCODER_CHUNK40) { q3t::set_error("bad vocoder mode"); return Q3T_ERR; }
+    if (n_frames > 0 && (!codes || !pcm)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return v->decode(codes, n_frames, mode, pcm, n_samples) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_talker_forward(q3t_ctx *ctx, int n, const float *embd, const int32_t *pos, float *hidden, float *logits) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (!embd || !pos) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.talker_forward(n, embd, pos, hidden, logits) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_codepred_frame(q3t_ctx *ctx, int n, const float *hidden, const int32_t *cb0, float temperature, int32_t top_k,
+                       uint64_t seed, int32_t frame, int32_t *codes15, float *logits) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (!hidden || !cb0 || !codes15) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.codepred_frame(n, hidden, cb0, temperature, top_k, seed, frame, codes15, logits) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_cb0_select(q3t_ctx *ctx, int n, const float *logits, const uint8_t *seen, const int32_t *frame,
+                   const int32_t *n_tokens, const q3t_gen_params *p, int32_t *tokens) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (!logits || !seen || !frame || !n_tokens || !tokens) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.cb0_select_host(n, logits, seen, frame, n_tokens, to_gp(p), tokens) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_project_text(q3t_ctx *ctx, int n, const int32_t *tokens, float *out) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (n > 0 && (!tokens || !out)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.project_text(n, tokens, out) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_prefill_embd(q3t_ctx *ctx, const int32_t *tokens, int n, const float *speaker, int language_id, float *prefill,
+                     int32_t *prefill_len, float *trailing, int32_t *trailing_len, float *tts_pad) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (!tokens || !prefill || !prefill_len || !trailing || !trailing_len || !tts_pad) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.prefill_embd(tokens, n, speaker, language_id, prefill, prefill_len, trailing, trailing_len, tts_pad)
+               ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+void gpu_fp32_to_fp16(const float *in, void *out, int n, void *stream) {
+    q3t::launch_f32_to_f16(in, static_cast<uint16_t *>(out), n, static_cast<hipStream_t>(stream));
+}
+void gpu_argmax_f32(const float *in, int32_t *out, int n, void *stream) {
+    q3t::launch_argmax_f32(in, out, n, static_cast<hipStream_t>(stream));
+}
+void gpu_embedding_lookup_by_gpu_id(const int32_t *token_id_ptr, const float *table, float *output, int embd_dim, void *stream) {
+    q3t::launch_embed_lookup(token_id_ptr, table, output, embd_dim, static_cast<hipStream_t>(stream));
+}
+void gpu_sample_topk_f32(const float *logits, const float *rand_val, int32_t *out, float temperature, int32_t top_k,
+                         int32_t vocab_size, void *stream) {
+    if (vocab_size > 4096) { q3t::set_error("gpu_sample_topk_f32: vocab_size > 4096"); return; }
+    q3t::launch_sample_topk_f32(logits, rand_val, out, temperature, top_k, vocab_size, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

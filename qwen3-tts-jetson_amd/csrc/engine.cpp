@@ -1,0 +1,666 @@
+// engine.cpp — see engine.h.
+#include "engine.h"
+
+#include <cmath>
+#include <cstring>
+
+#include "vocoder.h"
+
+namespace q3t {
+
+Engine::Engine() = default;
+
+Engine::~Engine() {
+    if (device_ >= 0) hipSetDevice(device_);
+    for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+    voc_.reset();
+    for (void *p : allocs_) hipFree(p);
+    if (stream_) hipStreamDestroy(stream_);
+}
+
+template <class T>
+T *Engine::dalloc(size_t n) {
+    void *p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T));
+    allocs_.push_back(p);
+    return static_cast<T *>(p);
+}
+
+namespace {
+bool check_shape(const GgufTensor *t, const char *name, int64_t cols, int64_t rows, int type) {
+    if (!t) { set_error(std::string("missing tensor ") + name); return false; }
+    const bool lead_ok = t->ne[0] == cols || (t->n_dims == 3 && t->ne[0] == 1 && t->ne[1] == cols);
+    if (t->type != type || !lead_ok || t->nelements() != cols * rows) {
+        set_error(std::string("tensor ") + name + ": unexpected shape/type");
+        return false;
+    }
+    return true;
+}
+}  // namespace
+
+bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx) {
+    device_ = device;
+    max_slots_ = std::max(1, max_slots);
+    max_ctx_ = std::max(32, max_ctx);
+    Q3T_HIP(hipSetDevice(device));
+    Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    Gguf g;
+    if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
+    // parse_config key aliases / defaults: src/tts_transformer.cpp:288-442
+    c_.text_vocab = (int)g.get_int({"qwen3-tts.text.vocab_size", "qwen3-tts.text_vocab_size"}, 151936);
+    c_.text_dim = (int)g.get_int({"qwen3-tts.text.embedding_dim", "qwen3-tts.text_hidden_size"}, 2048);
+    c_.hidden = (int)g.get_int({"qwen3-tts.talker.embedding_length", "qwen3-tts.embedding_length"}, 1024);
+    c_.n_layers = (int)g.get_int({"qwen3-tts.talker.block_count", "qwen3-tts.block_count"}, 28);
+    c_.n_heads = (int)g.get_int({"qwen3-tts.talker.attention.head_count", "qwen3-tts.attention.head_count"}, 16);
+    c_.n_kv = (int)g.get_int({"qwen3-tts.talker.attention.head_count_kv", "qwen3-tts.attention.head_count_kv"}, 8);
+    c_.inter = (int)g.get_int({"qwen3-tts.talker.feed_forward_length", "qwen3-tts.feed_forward_length"}, 3072);
+    c_.head_dim = (int)g.get_int({"qwen3-tts.talker.attention.key_length", "qwen3-tts.attention.key_length"}, 128);
+    c_.eps = g.get_f32({"qwen3-tts.talker.attention.layer_norm_rms_epsilon", "qwen3-tts.attention.layer_norm_rms_epsilon"}, 1e-6f);
+    c_.rope_theta = g.get_f32({"qwen3-tts.talker.rope.freq_base", "qwen3-tts.rope.freq_base"}, 1000000.0f);
+    c_.codec_vocab = (int)g.get_int({"qwen3-tts.talker.codec_vocab_size", "qwen3-tts.vocab_size"}, 3072);
+    c_.n_codebooks = (int)g.get_int({"qwen3-tts.talker.num_codebooks", "qwen3-tts.num_code_groups"}, 16);
+    c_.cp_layers = (int)g.get_int({"qwen3-tts.code_pred.layer_count", "qwen3-tts.code_predictor.layer_count"}, 5);
+    c_.cp_vocab = (int)g.get_int({"qwen3-tts.code_pred.vocab_size", "qwen3-tts.code_predictor.vocab_size"}, 2048);
+    c_.codec_pad = (int)g.get_int({"qwen3-tts.codec.pad_id"}, 2148);
+    c_.codec_bos = (int)g.get_int({"qwen3-tts.codec.bos_id"}, 2149);
+    c_.codec_eos = (int)g.get_int({"qwen3-tts.codec.eos_id", "qwen3-tts.codec.eos_token_id"}, 2150);
+    c_.tts_bos = (int)g.get_int({"qwen3-tts.tts_bos_token_id", "qwen3-tts.tts.bos_token_id", "qwen3-tts.tts.bos_id"}, 151672);
+    c_.tts_eos = (int)g.get_int({"qwen3-tts.tts_eos_token_id", "qwen3-tts.tts.eos_token_id", "qwen3-tts.tts.eos_id"}, 151673);
+    c_.tts_pad = (int)g.get_int({"qwen3-tts.tts_pad_token_id", "qwen3-tts.tts.pad_token_id", "qwen3-tts.tts.pad_id"}, 151671);
+    c_.think = (int)g.get_int({"qwen3-tts.codec.think_id", "qwen3-tts.codec_think_id"}, 2154);
+    c_.nothink = (int)g.get_int({"qwen3-tts.codec.nothink_id", "qwen3-tts.codec_nothink_id"}, 2155);
+    c_.think_bos = (int)g.get_int({"qwen3-tts.codec.think_bos_id", "qwen3-tts.codec_think_bos_id"}, 2156);
+    c_.think_eos = (int)g.get_int({"qwen3-tts.codec.think_eos_id", "qwen3-tts.codec_think_eos_id"}, 2157);
+    const int cp_hidden = (int)g.get_int({"qwen3-tts.code_predictor.embedding_length"}, c_.hidden);
+    if (cp_hidden != c_.hidden || g.find("code_pred.mtp_proj.weight")) {
+        set_error("code predictor hidden != talker hidden (1.7B mtp_proj) is not supported");
+        return false;
+    }
+    if (c_.n_codebooks != 16) { set_error("n_codebooks must be 16"); return false; }
+    if (!upload_weights(g)) return false;
+    if (!alloc_state()) return false;
+    if (!tok_gguf.empty()) {
+        voc_.reset(new Vocoder());
+        if (!voc_->load(tok_gguf, stream_)) return false;
+    }
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
+bool Engine::upload_weights(const Gguf &g) {
+    const int H = c_.hidden, D = c_.head_dim, Dq = c_.n_heads * D, Dkv = c_.n_kv * D, I = c_.inter;
+    if (I % 16 != 0 || H % 8 != 0) { set_error("unsupported hidden/intermediate size"); return false; }
+    auto up16 = [&](const char *name, int64_t cols, int64_t rows) -> uint16_t * {
+        const GgufTensor *t = g.find(name);
+        if (!check_shape(t, name, cols, rows, GGML_TYPE_F16)) return nullptr;
+        uint16_t *d = dalloc<uint16_t>((size_t)cols * rows);
+        if (!d || hipMemcpy(d, t->data, t->nbytes(), hipMemcpyHostToDevice) != hipSuccess) { set_error(std::string("upload ") + name); return nullptr; }
+        return d;
+    };
+    auto up32 = [&](const char *name, int64_t n) -> float * {
+        const GgufTensor *t = g.find(name);
+        if (!t || t->type != GGML_TYPE_F32 || t->nelements() != n) { set_error(std::string("bad f32 tensor ") + name); return nullptr; }
+        float *d = dalloc<float>((size_t)n);
+        if (!d || hipMemcpy(d, t->data, t->nbytes(), hipMemcpyHostToDevice) != hipSuccess) { set_error(std::string("upload ") + name); return nullptr; }
+        return d;
+    };
+    auto rows16 = [&](const std::string &name, int64_t cols, int64_t rows, std::vector<uint16_t> &dst, size_t at) -> bool {
+        const GgufTensor *t = g.find(name);
+        if (!check_shape(t, name.c_str(), cols, rows, GGML_TYPE_F16)) return false;
+        std::memcpy(dst.data() + at, t->data, t->nbytes());
+        return true;
+    };
+    auto layer = [&](const char *pfx, int i, DevLayer &l) -> bool {
+        char b[160];
+        auto nm = [&](const char *s) { snprintf(b, sizeof b, "%s.blk.%d.%s", pfx, i, s); return std::string(b); };
+        // fused [Wq; Wk; Wv] rows
+        std::vector<uint16_t> qkv((size_t)(Dq + 2 * Dkv) * H);
+        if (!rows16(nm("attn_q.weight"), H, Dq, qkv, 0) || !rows16(nm("attn_k.weight"), H, Dkv, qkv, (size_t)Dq * H) ||
+            !rows16(nm("attn_v.weight"), H, Dkv, qkv, (size_t)(Dq + Dkv) * H))
+            return false;
+        l.qkv = dalloc<uint16_t>(qkv.size());
+        Q3T_HIP(hipMemcpy(l.qkv, qkv.data(), qkv.size() * 2, hipMemcpyHostToDevice));
+        // gate/up interleaved in 16-row blocks (k_gemv ACT_SWIGLU layout)
+        std::vector<uint16_t> gate((size_t)I * H), up((size_t)I * H), gu((size_t)2 * I * H);
+        if (!rows16(nm("ffn_gate.weight"), H, I, gate, 0) || !rows16(nm("ffn_up.weight"), H, I, up, 0)) return false;
+        for (int blk = 0; blk < I / 16; ++blk) {
+            std::memcpy(gu.data() + (size_t)(blk * 32) * H, gate.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
+            std::memcpy(gu.data() + (size_t)(blk * 32 + 16) * H, up.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
+        }
+        l.gu = dalloc<uint16_t>(gu.size());
+        Q3T_HIP(hipMemcpy(l.gu, gu.data(), gu.size() * 2, hipMemcpyHostToDevice));
+        if (!(l.o = up16(nm("attn_output.weight").c_str(), Dq, H))) return false;
+        if (!(l.down = up16(nm("ffn_down.weight").c_str(), I, H))) return false;
+        if (!(l.attn_norm = up32(nm("attn_norm.weight").c_str(), H))) return false;
+        if (!(l.ffn_norm = up32(nm("ffn_norm.weight").c_str(), H))) return false;
+        if (!(l.qn = up32(nm("attn_q_norm.weight").c_str(), D))) return false;
+        if (!(l.kn = up32(nm("attn_k_norm.weight").c_str(), D))) return false;
+        return true;
+    };
+    L_.resize(c_.n_layers);
+    CP_.resize(c_.cp_layers);
+    for (int i = 0; i < c_.n_layers; ++i) if (!layer("talker", i, L_[i])) return false;
+    for (int i = 0; i < c_.cp_layers; ++i) if (!layer("code_pred", i, CP_[i])) return false;
+    if (!(text_embd_ = up16("talker.text_embd.weight", c_.text_dim, c_.text_vocab))) return false;
+    if (!(fc1_ = up16("talker.text_proj.fc1.weight", c_.text_dim, c_.text_dim))) return false;
+    if (!(fc2_ = up16("talker.text_proj.fc2.weight", c_.text_dim, H))) return false;
+    if (!(fc1_b_ = up32("talker.text_proj.fc1.bias", c_.text_dim))) return false;
+    if (!(fc2_b_ = up32("talker.text_proj.fc2.bias", H))) return false;
+    if (!(codec_embd_ = up16("talker.codec_embd.weight", H, c_.codec_vocab))) return false;
+    if (!(codec_head_ = up16("talker.codec_head.weight", H, c_.codec_vocab))) return false;
+    if (!(out_norm_ = up32("talker.output_norm.weight", H))) return false;
+    if (!(cp_out_norm_ = up32("code_pred.output_norm.weight", H))) return false;
+    cp_embd_.resize(15);
+    cp_head_.resize(15);
+    for (int i = 0; i < 15; ++i) {
+        char b[96];
+        snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
+        if (!(cp_embd_[i] = up16(b, H, c_.cp_vocab))) return false;
+        snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
+        if (!(cp_head_[i] = up16(b, H, c_.cp_vocab))) return false;
+    }
+    cp_embd_dev_ = dalloc<uint16_t *>(15);
+    Q3T_HIP(hipMemcpy(cp_embd_dev_, cp_embd_.data(), 15 * sizeof(uint16_t *), hipMemcpyHostToDevice));
+    // RoPE cos/sin table with ggml_rope_cache_init's f32 recurrence (theta *= theta_scale), NEOX pairs
+    rope_len_ = std::max(max_ctx_, 16);
+    std::vector<float> rope((size_t)rope_len_ * D);
+    const float theta_scale = powf(c_.rope_theta, -2.0f / (float)D);
+    for (int p = 0; p < rope_len_; ++p) {
+        float theta = (float)p;
+        for (int i0 = 0; i0 < D; i0 += 2) {
+            rope[(size_t)p * D + i0] = cosf(theta);
+            rope[(size_t)p * D + i0 + 1] = sinf(theta);
+            theta *= theta_scale;
+        }
+    }
+    rope_ = dalloc<float>(rope.size());
+    Q3T_HIP(hipMemcpy(rope_, rope.data(), rope.size() * 4, hipMemcpyHostToDevice));
+    return true;
+}
+
+bool Engine::alloc_state() {
+    const int S = max_slots_, H = c_.hidden, D = c_.head_dim;
+    const int QKV = (c_.n_heads + 2 * c_.n_kv) * D;
+    const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
+    max_trailing_ = 512;
+    x_ = dalloc<float>((size_t)S * H);
+    qkv_ = dalloc<float>((size_t)S * QKV);
+    logits_ = dalloc<float>((size_t)S * c_.codec_vocab);
+    hidden_ = dalloc<float>((size_t)S * H);
+    cpx_ = dalloc<float>((size_t)S * H);
+    cp_in1_ = dalloc<float>((size_t)S * H);
+    cp_logits_ = dalloc<float>((size_t)S * c_.cp_vocab);
+    part_ = dalloc<float>((size_t)S * c_.n_heads * max_splits * (D + 2));
+    attn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
+    hmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
+    const size_t kv_layer = (size_t)S * c_.n_kv * max_ctx_ * D;
+    kc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
+    vc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
+    const size_t cpkv_layer = (size_t)S * c_.n_kv * 16 * D;
+    cpkc_ = dalloc<uint16_t>(cpkv_layer * c_.cp_layers);
+    cpvc_ = dalloc<uint16_t>(cpkv_layer * c_.cp_layers);
+    pos_ = dalloc<int>(S);
+    frame_ = dalloc<int>(S);
+    done_ = dalloc<int>(S);
+    token_ = dalloc<int>(S);
+    tokens_ = dalloc<int>((size_t)S * 16);
+    n_tokens_ = dalloc<int>(S);
+    force_ = dalloc<int>(S);
+    trailing_len_ = dalloc<int>(S);
+    cp_pos_ = dalloc<int>((size_t)16 * S);
+    seen_ = dalloc<uint8_t>((size_t)S * c_.codec_vocab);
+    utt_ = dalloc<uint64_t>(S);
+    trailing_ = dalloc<float>((size_t)S * max_trailing_ * H);
+    tts_pad_ = dalloc<float>((size_t)S * H);
+    prefill_ = dalloc<float>((size_t)S * 10 * H);
+    codes_max_len_ = max_ctx_;
+    codes_ = dalloc<int32_t>((size_t)S * codes_max_len_ * 16);
+    proj_cap_ = S * (max_trailing_ + 16);
+    proj_idx_ = dalloc<int>(proj_cap_);
+    proj_h_ = dalloc<uint16_t>((size_t)proj_cap_ * c_.text_dim);
+    proj_out_ = dalloc<float>((size_t)proj_cap_ * H);
+    recipe_cap_ = S * (max_trailing_ + 16);
+    recipe_ = dalloc<RowRecipe>(recipe_cap_);
+    if (!x_ || !kc_ || !vc_ || !recipe_ || !proj_out_) { set_error("device allocation failed"); return false; }
+    std::vector<int> cpp((size_t)16 * S);
+    for (int p = 0; p < 16; ++p) for (int s = 0; s < S; ++s) cpp[(size_t)p * S + s] = p;
+    Q3T_HIP(hipMemcpy(cp_pos_, cpp.data(), cpp.size() * 4, hipMemcpyHostToDevice));
+    std::vector<uint64_t> utt(S);
+    for (int s = 0; s < S; ++s) utt[s] = (uint64_t)s;
+    Q3T_HIP(hipMemcpy(utt_, utt.data(), S * 8, hipMemcpyHostToDevice));
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ one decoder stack
+// 5 launches per layer: [RMSNorm+QKV GEMV] [head-norm+RoPE+KV-append+attention] [O GEMV + residual]
+// [RMSNorm+gate/up GEMV+SwiGLU] [down GEMV + residual]   (tts_transformer.cpp:1410-1494)
+static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, float *qkv,
+                          uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc, size_t kv_layer, int n_ctx,
+                          int max_splits, const int *pos, const float *rope, float *part, hipStream_t s) {
+    const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
+    for (size_t il = 0; il < layers.size(); ++il) {
+        const DevLayer &l = layers[il];
+        GemvParams g;
+        g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
+        g.pro = PRO_RMS; g.x = x; g.ldx = H; g.nw = l.attn_norm; g.eps = c.eps;
+        g.out_f32 = qkv; g.ldo = QKV;
+        if (!gemv(g, s)) return false;
+        AttnParams a;
+        a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
+        a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
+        a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
+        a.max_splits = max_splits; a.part = part; a.out = attn;
+        if (!attn_decode(a, s)) return false;
+        GemvParams o;
+        o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
+        o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
+        o.resid = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
+        if (!gemv(o, s)) return false;
+        GemvParams gu;
+        gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
+        gu.pro = PRO_RMS; gu.x = x; gu.ldx = H; gu.nw = l.ffn_norm; gu.eps = c.eps;
+        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter;
+        if (!gemv(gu, s)) return false;
+        GemvParams dn;
+        dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;
+        dn.pro = PRO_F16; dn.x = hmlp; dn.ldx = c.inter;
+        dn.resid = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
+        if (!gemv(dn, s)) return false;
+    }
+    return true;
+}
+
+bool Engine::enqueue_talker_step(int S, hipStream_t s) {
+    const int H = c_.hidden;
+    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
+    const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
+    if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_, s))
+        return false;
+    // final RMSNorm (hidden_states, side output) + codec_head -> logits  (:1496-1505)
+    GemvParams h;
+    h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = S;
+    h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_;
+    h.out_f32 = logits_; h.ldo = c_.codec_vocab;
+    return gemv(h, s);
+}
+
+// 16 passes of the 5-layer code predictor, token chosen on device each pass (trt_code_predictor.cpp:484-600)
+bool Engine::enqueue_cp_frame(int S, hipStream_t s) {
+    const int H = c_.hidden;
+    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
+    Q3T_HIP(hipMemcpyAsync(cpx_, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, s));
+    for (int p = 0; p < 16; ++p) {
+        if (p == 1) Q3T_HIP(hipMemcpyAsync(cpx_, cp_in1_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, s));
+        if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_,
+                           rope_, part_, s))
+            return false;
+        if (p == 0) continue;
+        const int step = p - 1;
+        GemvParams h;
+        h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
+        h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
+        h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
+        if (!gemv(h, s)) return false;
+        CpSelParams cs;
+        cs.logits = cp_logits_; cs.V = c_.cp_vocab; cs.S = S; cs.step = step;
+        cs.tokens = tokens_; cs.codes = codes_; cs.frame = frame_; cs.done = done_;
+        cs.max_len = codes_max_len_; cs.ncb = 16;
+        cs.temperature = gp_.temperature; cs.top_k = gp_.top_k; cs.seed = gp_.seed; cs.utt = utt_;
+        cs.next_table = step < 14 ? cp_embd_[step] : nullptr;
+        cs.x_next = cpx_; cs.H = H;
+        if (!cp_select(cs, s)) return false;
+    }
+    return true;
+}
+
+bool Engine::enqueue_frame(int S, hipStream_t s) {
+    Cb0Params cb;
+    cb.logits = logits_; cb.V = c_.codec_vocab; cb.S = S; cb.eos = c_.codec_eos;
+    cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
+    cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
+    cb.rep = gp_.rep_penalty; cb.temperature = gp_.temperature; cb.top_k = gp_.top_k; cb.seed = gp_.seed; cb.utt = utt_;
+    cb.next_table = codec_embd_; cb.x_next = cp_in1_; cb.H = c_.hidden;
+    if (!cb0_select(cb, s)) return false;
+    if (!enqueue_cp_frame(S, s)) return false;
+    StepEmbdParams se;
+    se.tokens = tokens_; se.codec_embd = codec_embd_; se.cp_embd = cp_embd_dev_;
+    se.trailing = trailing_; se.trailing_len = trailing_len_; se.max_trailing = max_trailing_;
+    se.tts_pad = tts_pad_; se.frame = frame_; se.out = x_; se.S = S; se.H = c_.hidden; se.ncb = 16;
+    if (!step_embd(se, s)) return false;
+    if (!enqueue_talker_step(S, s)) return false;
+    return advance(pos_, frame_, S, s);
+}
+
+bool Engine::graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t)) {
+    if (cache.count(S)) return true;
+    hipGraph_t graph = nullptr;
+    Q3T_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    const bool ok = (this->*fn)(S, stream_);
+    hipError_t e = hipStreamEndCapture(stream_, &graph);
+    if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
+    if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
+    hipGraphExec_t exec = nullptr;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    hipGraphDestroy(graph);
+    if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
+    cache[S] = exec;
+    return true;
+}
+
+bool Engine::set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame) {
+    Q3T_HIP(hipMemcpyAsync(pos_, pos.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(frame_, frame.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ prefill pieces
+bool Engine::enqueue_text_projection(int n_rows, hipStream_t s) {
+    // text_embd row gather -> fc1 + b -> SiLU -> fc2 + b   (tts_transformer.cpp:1050-1055)
+    GemvParams a;
+    a.W = fc1_; a.N = c_.text_dim; a.K = c_.text_dim; a.B = n_rows;
+    a.pro = PRO_F16; a.x = text_embd_; a.ldx = c_.text_dim; a.x_idx = proj_idx_;
+    a.bias = fc1_b_; a.act = ACT_SILU; a.out_f16 = proj_h_; a.ldo = c_.text_dim;
+    if (!gemv(a, s)) return false;
+    GemvParams b;
+    b.W = fc2_; b.N = c_.hidden; b.K = c_.text_dim; b.B = n_rows;
+    b.pro = PRO_F16; b.x = proj_h_; b.ldx = c_.text_dim;
+    b.bias = fc2_b_; b.out_f32 = proj_out_; b.ldo = c_.hidden;
+    return gemv(b, s);
+}
+
+bool Engine::project_text(int n, const int32_t *toks, float *out) {
+    if (n <= 0) return true;
+    if (n > proj_cap_) { set_error("too many text rows"); return false; }
+    for (int i = 0; i < n; ++i)
+        if (toks[i] < 0 || toks[i] >= c_.text_vocab) { set_error("text token out of range"); return false; }
+    Q3T_HIP(hipMemcpyAsync(proj_idx_, toks, n * 4, hipMemcpyHostToDevice, stream_));
+    if (!enqueue_text_projection(n, stream_)) return false;
+    Q3T_HIP(hipMemcpyAsync(out, proj_out_, (size_t)n * c_.hidden * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
+namespace {
+struct SlotPlan { int rb, n, plen, tcount; };
+}
+
+// Prefill assembly for slots 0..n_utt-1 on device (build_prefill_graph, tts_transformer.cpp:1093-1231).
+// Projection rows of slot s start at rb: [tts_bos, tts_eos, tts_pad, tok0, tok1, tok2, tok3, tok4 .. tok(n-6)]
+static bool plan_rows(const Config &c, int n_utt, const int32_t *const *tokens, const int *n_tokens, int max_trailing,
+                      std::vector<int> &idx, std::vector<SlotPlan> &plan) {
+    idx.clear();
+    plan.clear();
+    for (int s = 0; s < n_utt; ++s) {
+        const int n = n_tokens[s];
+        if (n < 4) { set_error("Need at least 4 text tokens for generation"); return false; }
+        const int tcount = std::max(0, n - 9);
+        if (tcount + 1 > max_trailing) { set_error("prompt too long for the trailing-text buffer"); return false; }
+        SlotPlan p{(int)idx.size(), n, 0, tcount};
+        idx.push_back(c.tts_bos); idx.push_back(c.tts_eos); idx.push_back(c.tts_pad);
+        for (int i = 0; i < 4; ++i) idx.push_back(tokens[s][i]);
+        for (int i = 0; i < tcount; ++i) idx.push_back(tokens[s][4 + i]);
+        plan.push_back(p);
+    }
+    for (int v : idx)
+        if (v < 0 || v >= c.text_vocab) { set_error("text token out of range"); return false; }
+    return true;
+}
+
+bool Engine::prefill_embd(const int32_t *toks, int n, const float *spk, int language_id, float *prefill, int *prefill_len,
+                          float *trailing, int *trailing_len, float *tts_pad) {
+    // host entry for the parity tests: run the same device assembly as generate() on slot 0
+    const int32_t *tk[1] = {toks};
+    std::vector<int> idx;
+    std::vector<SlotPlan> plan;
+    if (!plan_rows(c_, 1, tk, &n, max_trailing_, idx, plan)) return false;
+    GenParams gp = gp_;
+    gp.language_id = language_id;
+    (void)gp;
+    const int H = c_.hidden;
+    Q3T_HIP(hipMemcpyAsync(proj_idx_, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_));
+    if (!enqueue_text_projection((int)idx.size(), stream_)) return false;
+    float *spk_dev = nullptr;
+    if (spk) {
+        spk_dev = cp_in1_;   // scratch
+        Q3T_HIP(hipMemcpyAsync(spk_dev, spk, H * 4, hipMemcpyHostToDevice, stream_));
+    }
+    // recipe (same as generate)
+    std::vector<RowRecipe> rec;
+    const SlotPlan &p = plan[0];
+    const float *P = proj_out_ + (size_t)p.rb * H;
+    auto prow = [&](int i) { return RowTerm{P + (size_t)i * H, 0}; };
+    auto crow = [&](int id) { return RowTerm{codec_embd_ + (size_t)id * H, 1}; };
+    std::vector<RowTerm> cin;
+    if (language_id < 0) { cin = {crow(c_.nothink), crow(c_.think_bos), crow(c_.think_eos)}; }
+    else { cin = {crow(c_.think), crow(c_.think_bos), crow(language_id), crow(c_.think_eos)}; }
+    if (language_id >= c_.codec_vocab) { set_error("language id out of range"); return false; }
+    if (spk) cin.push_back(RowTerm{spk_dev, 0});
+    cin.push_back(crow(c_.codec_pad));
+    cin.push_back(crow(c_.codec_bos));
+    const int ol = (int)cin.size() - 1, plen = 3 + ol + 1;
+    float *out = prefill_;
+    for (int r = 0; r < 3; ++r) rec.push_back(RowRecipe{out + (size_t)r * H, {prow(3 + r), {nullptr, 0}, {nullptr, 0}}});
+    for (int t = 0; t < ol; ++t) rec.push_back(RowRecipe{out + (size_t)(3 + t) * H, {t == ol - 1 ? prow(0) : prow(2), cin[t], {nullptr, 0}}});
+    rec.push_back(RowRecipe{out + (size_t)(plen - 1) * H, {prow(6), cin.back(), {nullptr, 0}}});
+    for (int i = 0; i < p.tcount; ++i) rec.push_back(RowRecipe{trailing_ + (size_t)i * H, {prow(7 + i), {nullptr, 0}, {nullptr, 0}}});
+    rec.push_back(RowRecipe{trailing_ + (size_t)p.tcount * H, {prow(1), {nullptr, 0}, {nullptr, 0}}});
+    rec.push_back(RowRecipe{tts_pad_, {prow(2), {nullptr, 0}, {nullptr, 0}}});
+    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
+    if (!rows_recipe(recipe_, (int)rec.size(), H, stream_)) return false;
+    Q3T_HIP(hipMemcpyAsync(prefill, prefill_, (size_t)plen * H * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipMemcpyAsync(trailing, trailing_, (size_t)(p.tcount + 1) * H * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipMemcpyAsync(tts_pad, tts_pad_, (size_t)H * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    *prefill_len = plen;
+    *trailing_len = p.tcount + 1;
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ hot path
+bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                      const GenParams &gp, int32_t *codes, int *n_frames) {
+    if (n_utt <= 0) return true;
+    if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
+    const int S = n_utt, H = c_.hidden, NCB = 16;
+    for (int s = 0; s < S; ++s) n_frames[s] = 0;
+    if (gp.max_len <= 0) return true;
+    if (gp.language_id >= c_.codec_vocab) { set_error("language id out of range"); return false; }
+    std::vector<int> idx;
+    std::vector<SlotPlan> plan;
+    if (!plan_rows(c_, S, tokens, n_tokens, max_trailing_, idx, plan)) return false;
+    const bool has_spk = speaker && speaker[0];
+    for (int s = 0; s < S; ++s)
+        if ((speaker && speaker[s]) != has_spk) { set_error("speaker embedding must be given for all or none of the utterances"); return false; }
+    const int n_pre = gp.language_id < 0 ? 3 : 4;
+    const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
+    if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
+    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty && gp.seed == gp_.seed)) {
+        for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+        g_frame_.clear();
+    }
+    gp_ = gp;
+    hipEvent_t e0, e1, e2;
+    hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
+    Q3T_HIP(hipEventRecord(e0, stream_));
+    // ---- text projection for every slot, one batched pass
+    Q3T_HIP(hipMemcpyAsync(proj_idx_, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_));
+    if (!enqueue_text_projection((int)idx.size(), stream_)) return false;
+    // ---- prefill / trailing / pad rows
+    float *spk_dev = cp_in1_;   // scratch [S][H]
+    if (has_spk)
+        for (int s = 0; s < S; ++s) Q3T_HIP(hipMemcpyAsync(spk_dev + (size_t)s * H, speaker[s], H * 4, hipMemcpyHostToDevice, stream_));
+    std::vector<RowRecipe> rec;
+    std::vector<int> tl(S), ntok(S), force(S, gp.force_frames), pos0(S, 0), frame0(S, 0), done0(S, -1);
+    for (int s = 0; s < S; ++s) {
+        const SlotPlan &p = plan[s];
+        const float *P = proj_out_ + (size_t)p.rb * H;
+        auto prow = [&](int i) { return RowTerm{P + (size_t)i * H, 0}; };
+        auto crow = [&](int id) { return RowTerm{codec_embd_ + (size_t)id * H, 1}; };
+        std::vector<RowTerm> cin;
+        if (gp.language_id < 0) cin = {crow(c_.nothink), crow(c_.think_bos), crow(c_.think_eos)};
+        else cin = {crow(c_.think), crow(c_.think_bos), crow(gp.language_id), crow(c_.think_eos)};
+        if (has_spk) cin.push_back(RowTerm{spk_dev + (size_t)s * H, 0});
+        cin.push_back(crow(c_.codec_pad));
+        cin.push_back(crow(c_.codec_bos));
+        const int ol = (int)cin.size() - 1;
+        float *out = prefill_ + (size_t)s * 10 * H;
+        for (int r = 0; r < 3; ++r) rec.push_back(RowRecipe{out + (size_t)r * H, {prow(3 + r), {nullptr, 0}, {nullptr, 0}}});
+        for (int t = 0; t < ol; ++t) rec.push_back(RowRecipe{out + (size_t)(3 + t) * H, {t == ol - 1 ? prow(0) : prow(2), cin[t], {nullptr, 0}}});
+        rec.push_back(RowRecipe{out + (size_t)(plen - 1) * H, {prow(6), cin.back(), {nullptr, 0}}});
+        float *tr = trailing_ + (size_t)s * max_trailing_ * H;
+        for (int i = 0; i < p.tcount; ++i) rec.push_back(RowRecipe{tr + (size_t)i * H, {prow(7 + i), {nullptr, 0}, {nullptr, 0}}});
+        rec.push_back(RowRecipe{tr + (size_t)p.tcount * H, {prow(1), {nullptr, 0}, {nullptr, 0}}});
+        rec.push_back(RowRecipe{tts_pad_ + (size_t)s * H, {prow(2), {nullptr, 0}, {nullptr, 0}}});
+        tl[s] = p.tcount + 1;
+        ntok[s] = p.n;
+    }
+    if ((int)rec.size() > recipe_cap_) { set_error("recipe overflow"); return false; }
+    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
+    if (!rows_recipe(recipe_, (int)rec.size(), H, stream_)) return false;
+    Q3T_HIP(hipMemcpyAsync(trailing_len_, tl.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(n_tokens_, ntok.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(force_, force.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_, done0.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemsetAsync(seen_, 0, (size_t)S * c_.codec_vocab, stream_));
+    Q3T_HIP(hipMemsetAsync(codes_, 0, (size_t)S * codes_max_len_ * NCB * 4, stream_));
+    // ---- prefill: plen talker steps (token-by-token; the step graph is replayed)
+    if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false;
+    std::vector<int> posv(S);
+    for (int t = 0; t < plen; ++t) {
+        Q3T_HIP(hipMemcpy2DAsync(x_, H * 4, prefill_ + (size_t)t * H, (size_t)10 * H * 4, H * 4, S, hipMemcpyDeviceToDevice, stream_));
+        Q3T_HIP(hipMemcpyAsync(pos_, cp_pos_ + (size_t)t * max_slots_, S * 4, hipMemcpyDeviceToDevice, stream_));
+        Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
+    }
+    for (int s = 0; s < S; ++s) posv[s] = plen;
+    if (!set_slot_state(S, posv, frame0)) return false;
+    Q3T_HIP(hipEventRecord(e1, stream_));
+    // ---- frame loop: one graph per frame; done flags polled every 16 frames
+    if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) return false;
+    int *done_h = nullptr;
+    Q3T_HIP(hipHostMalloc(&done_h, S * 4, hipHostMallocDefault));
+    bool all_done = false;
+    for (int f = 0; f < gp.max_len && !all_done; ++f) {
+        Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
+        if ((f + 1) % 16 == 0 && f + 1 < gp.max_len) {
+            Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
+            Q3T_HIP(hipStreamSynchronize(stream_));
+            all_done = true;
+            for (int s = 0; s < S; ++s) all_done = all_done && done_h[s] >= 0;
+        }
+    }
+    Q3T_HIP(hipEventRecord(e2, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipMemcpy2DAsync(codes, (size_t)gp.max_len * NCB * 4, codes_, (size_t)codes_max_len_ * NCB * 4,
+                             (size_t)gp.max_len * NCB * 4, S, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    for (int s = 0; s < S; ++s) n_frames[s] = done_h[s] >= 0 ? std::min(done_h[s], gp.max_len) : gp.max_len;
+    hipHostFree(done_h);
+    float ms1 = 0, ms2 = 0;
+    hipEventElapsedTime(&ms1, e0, e1);
+    hipEventElapsedTime(&ms2, e1, e2);
+    last_prefill_ms = ms1;
+    last_frames_ms = ms2;
+    hipEventDestroy(e0); hipEventDestroy(e1); hipEventDestroy(e2);
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ test entry points
+bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hidden, float *logits) {
+    if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
+    for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
+    const int H = c_.hidden;
+    Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
+    if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false;
+    Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
+    if (hidden) Q3T_HIP(hipMemcpyAsync(hidden, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToHost, stream_));
+    if (logits) Q3T_HIP(hipMemcpyAsync(logits, logits_, (size_t)S * c_.codec_vocab * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
+bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float temperature, int top_k, uint64_t seed,
+                            int frame, int32_t *codes15, float *logits_all) {
+    if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
+    const int H = c_.hidden;
+    for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
+    GenParams gp = gp_;
+    gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
+    gp_ = gp;
+    for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+    g_frame_.clear();
+    Q3T_HIP(hipMemcpyAsync(hidden_, hidden, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
+    std::vector<RowRecipe> rec(S);
+    for (int s = 0; s < S; ++s) rec[s] = RowRecipe{cp_in1_ + (size_t)s * H, {{codec_embd_ + (size_t)cb0[s] * H, 1}, {nullptr, 0}, {nullptr, 0}}};
+    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), S * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
+    if (!rows_recipe(recipe_, S, H, stream_)) return false;
+    std::vector<int> fr(S, frame), dn(S, -1);
+    Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    if (!logits_all) {
+        if (!enqueue_cp_frame(S, stream_)) return false;
+    } else {
+        // same launches as enqueue_cp_frame, with the per-step logits copied out
+        const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
+        Q3T_HIP(hipMemcpyAsync(cpx_, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, stream_));
+        std::vector<float> lg((size_t)S * c_.cp_vocab);
+        for (int p = 0; p < 16; ++p) {
+            if (p == 1) Q3T_HIP(hipMemcpyAsync(cpx_, cp_in1_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, stream_));
+            if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_, rope_, part_, stream_))
+                return false;
+            if (p == 0) continue;
+            const int step = p - 1;
+            GemvParams h;
+            h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
+            h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
+            h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
+            if (!gemv(h, stream_)) return false;
+            Q3T_HIP(hipMemcpyAsync(lg.data(), cp_logits_, lg.size() * 4, hipMemcpyDeviceToHost, stream_));
+            Q3T_HIP(hipStreamSynchronize(stream_));
+            for (int s = 0; s < S; ++s)
+                std::memcpy(logits_all + ((size_t)s * 15 + step) * c_.cp_vocab, lg.data() + (size_t)s * c_.cp_vocab, c_.cp_vocab * 4);
+            CpSelParams cs;
+            cs.logits = cp_logits_; cs.V = c_.cp_vocab; cs.S = S; cs.step = step;
+            cs.tokens = tokens_; cs.codes = codes_; cs.frame = frame_; cs.done = done_;
+            cs.max_len = codes_max_len_; cs.ncb = 16;
+            cs.temperature = temperature; cs.top_k = top_k; cs.seed = seed; cs.utt = utt_;
+            cs.next_table = step < 14 ? cp_embd_[step] : nullptr;
+            cs.x_next = cpx_; cs.H = H;
+            if (!cp_select(cs, stream_)) return false;
+        }
+    }
+    std::vector<int> tk((size_t)S * 16);
+    Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    for (int s = 0; s < S; ++s) for (int i = 0; i < 15; ++i) codes15[s * 15 + i] = tk[(size_t)s * 16 + 1 + i];
+    return true;
+}
+
+bool Engine::cb0_select_host(int S, const float *logits, const uint8_t *seen, const int *frame, const int *n_tokens,
+                             const GenParams &gp, int *tok) {
+    if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
+    const int V = c_.codec_vocab;
+    Q3T_HIP(hipMemcpyAsync(logits_, logits, (size_t)S * V * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(seen_, seen, (size_t)S * V, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(frame_, frame, S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(n_tokens_, n_tokens, S * 4, hipMemcpyHostToDevice, stream_));
+    std::vector<int> force(S, gp.force_frames), dn(S, -1);
+    Q3T_HIP(hipMemcpyAsync(force_, force.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Cb0Params cb;
+    cb.logits = logits_; cb.V = V; cb.S = S; cb.eos = c_.codec_eos;
+    cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
+    cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
+    cb.rep = gp.rep_penalty; cb.temperature = gp.temperature; cb.top_k = gp.top_k; cb.seed = gp.seed; cb.utt = utt_;
+    cb.next_table = codec_embd_; cb.x_next = cp_in1_; cb.H = c_.hidden;
+    if (!cb0_select(cb, stream_)) return false;
+    std::vector<int> tk((size_t)S * 16);
+    Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    for (int s = 0; s < S; ++s) tok[s] = tk[(size_t)s * 16];
+    return true;
+}
+
+}  // namespace q3t

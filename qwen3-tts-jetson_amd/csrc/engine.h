@@ -1,0 +1,121 @@
+// engine.h — MI355X-native runtime of the per-frame decode path (Talker step -> CB0 -> Code Predictor ->
+// step embedding), replacing the reference's TTSTransformer::generate hot loop (src/tts_transformer.cpp:2342-2574)
+// and TRTCodePredictor (src/trt_code_predictor.cpp).  B utterances ("slots") advance in lock-step; every
+// per-frame kernel reads positions / frame counters from device memory so one hipGraph replays every frame.
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gguf.h"
+#include "kernels.h"
+
+namespace q3t {
+
+struct Config {
+    int hidden = 1024, n_layers = 28, n_heads = 16, n_kv = 8, head_dim = 128, inter = 3072;
+    int codec_vocab = 3072, n_codebooks = 16, text_vocab = 151936, text_dim = 2048;
+    int cp_layers = 5, cp_vocab = 2048;
+    float eps = 1e-6f, rope_theta = 1e6f;
+    int codec_pad = 2148, codec_bos = 2149, codec_eos = 2150;
+    int tts_bos = 151672, tts_eos = 151673, tts_pad = 151671;
+    int think = 2154, nothink = 2155, think_bos = 2156, think_eos = 2157;
+};
+
+struct GenParams {
+    int max_len = 4096;
+    int language_id = 2050;
+    float rep_penalty = 1.05f;
+    float temperature = 0.9f;
+    int top_k = 50;
+    uint64_t seed = 0;
+    int force_frames = 0;      // bench: mask EOS until this many frames are produced
+};
+
+struct DevLayer {
+    uint16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+    float *attn_norm = nullptr, *ffn_norm = nullptr, *qn = nullptr, *kn = nullptr;
+};
+
+class Vocoder;
+
+class Engine {
+public:
+    Engine();
+    ~Engine();
+    bool load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx);
+    const Config &cfg() const { return c_; }
+    int max_slots() const { return max_slots_; }
+    int max_ctx() const { return max_ctx_; }
+    hipStream_t stream() const { return stream_; }
+    Vocoder *vocoder() { return voc_.get(); }
+
+    // ---- hot path: prefill + frame loop for n_utt utterances (codes [n_utt][max_len][ncb])
+    bool generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                  const GenParams &gp, int32_t *codes, int *n_frames);
+
+    // ---- stage entry points (host buffers) used by the parity tests
+    bool talker_forward(int S, const float *embd, const int *pos, float *hidden, float *logits);
+    bool codepred_frame(int S, const float *hidden, const int *cb0, float temperature, int top_k, uint64_t seed,
+                        int frame, int32_t *codes15, float *logits_all);
+    bool cb0_select_host(int S, const float *logits, const uint8_t *seen, const int *frame, const int *n_tokens,
+                         const GenParams &gp, int *tokens);
+    bool project_text(int n, const int32_t *toks, float *out);
+    bool prefill_embd(const int32_t *toks, int n, const float *spk, int language_id, float *prefill, int *prefill_len,
+                      float *trailing, int *trailing_len, float *tts_pad);
+
+    // profiling hooks for bench.py: last generate() timings
+    double last_prefill_ms = 0, last_frames_ms = 0;
+
+private:
+    bool upload_weights(const Gguf &g);
+    bool alloc_state();
+    bool enqueue_talker_step(int S, hipStream_t s);
+    bool enqueue_cp_frame(int S, hipStream_t s);
+    bool enqueue_frame(int S, hipStream_t s);
+    bool enqueue_text_projection(int n_rows, hipStream_t s);
+    bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));
+    bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
+
+    Config c_;
+    int device_ = 0, max_slots_ = 0, max_ctx_ = 0, max_trailing_ = 0;
+    hipStream_t stream_ = nullptr;
+    std::vector<void *> allocs_;
+    template <class T> T *dalloc(size_t n);
+
+    // weights
+    std::vector<DevLayer> L_, CP_;
+    uint16_t *text_embd_ = nullptr, *fc1_ = nullptr, *fc2_ = nullptr, *codec_embd_ = nullptr, *codec_head_ = nullptr;
+    float *fc1_b_ = nullptr, *fc2_b_ = nullptr, *out_norm_ = nullptr, *cp_out_norm_ = nullptr;
+    std::vector<uint16_t *> cp_embd_, cp_head_;
+    uint16_t **cp_embd_dev_ = nullptr;
+    float *rope_ = nullptr;
+    int rope_len_ = 0;
+
+    // activations / state (sized for max_slots)
+    float *x_ = nullptr, *qkv_ = nullptr, *logits_ = nullptr, *hidden_ = nullptr, *cpx_ = nullptr, *cp_in1_ = nullptr;
+    float *cp_logits_ = nullptr, *part_ = nullptr;
+    uint16_t *attn_ = nullptr, *hmlp_ = nullptr;
+    uint16_t *kc_ = nullptr, *vc_ = nullptr, *cpkc_ = nullptr, *cpvc_ = nullptr;
+    int *pos_ = nullptr, *frame_ = nullptr, *done_ = nullptr, *token_ = nullptr, *tokens_ = nullptr;
+    int *n_tokens_ = nullptr, *force_ = nullptr, *trailing_len_ = nullptr, *cp_pos_ = nullptr;
+    uint8_t *seen_ = nullptr;
+    uint64_t *utt_ = nullptr;
+    float *trailing_ = nullptr, *tts_pad_ = nullptr, *prefill_ = nullptr;
+    int32_t *codes_ = nullptr;
+    int codes_max_len_ = 0;
+    // text projection scratch
+    int *proj_idx_ = nullptr;
+    uint16_t *proj_h_ = nullptr;
+    float *proj_out_ = nullptr;
+    int proj_cap_ = 0;
+    RowRecipe *recipe_ = nullptr;
+    int recipe_cap_ = 0;
+    GenParams gp_;   // parameters baked into the captured frame graph
+
+    std::map<int, hipGraphExec_t> g_talker_, g_frame_;
+    std::unique_ptr<Vocoder> voc_;
+};
+
+}  // namespace q3t

@@ -1,0 +1,122 @@
+// kernels.h — launchers of the hand-written gfx950 kernels (kernels.hip).
+#pragma once
+#include "q3t_common.h"
+
+namespace q3t {
+
+enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3 };
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_SWIGLU = 3 };
+
+// y[b][n] = epilogue( W[n][:] . f16(prologue(x[b][:])) ),  W f16 row-major [N][K]
+struct GemvParams {
+    const uint16_t *W = nullptr;
+    int N = 0, K = 0, B = 0;
+    int pro = PRO_F16;
+    const void *x = nullptr;      // f16 [B][ldx] (PRO_F16) or f32 [B][ldx]
+    int ldx = 0;
+    const int *x_idx = nullptr;   // optional row gather: row of batch b = x_idx[b]
+    const float *nw = nullptr, *nb = nullptr;  // norm weight / bias (RMS, LN)
+    float eps = 1e-6f;
+    float *side_out = nullptr;    // normalized prologue rows (f32 [B][K]) written by x-block 0
+    int act = ACT_NONE;           // ACT_SWIGLU: rows interleaved in 16-row blocks [gate16 | up16]
+    const float *bias = nullptr, *scale = nullptr;
+    const float *resid = nullptr;  // out = resid[b][n] + (...)
+    int ldr = 0;
+    const float *aux = nullptr;    // out = aux[b][n] + (...)   (applied after resid)
+    int lda = 0;
+    float *out_f32 = nullptr;
+    uint16_t *out_f16 = nullptr;
+    int ldo = 0;
+    int orow_mul = 1, orow_add = 0;  // output row of batch b = b*orow_mul + orow_add
+};
+bool gemv(const GemvParams &p, hipStream_t s);
+
+// Qwen3 attention for one new token per slot (decode / code-predictor pass), fused with q/k head RMSNorm,
+// NEOX RoPE (host cos/sin table), F16 KV append at pos[slot] and split-K flash-decode.
+struct AttnParams {
+    const float *qkv = nullptr;   // [S][(nH + 2 nKV) * D] f32
+    const float *qn = nullptr, *kn = nullptr;  // head-norm weights [D]
+    float eps = 1e-6f;
+    const float *rope = nullptr;  // [max_pos][D] (cos, sin pairs)
+    const int *pos = nullptr;     // [S] position of the new token
+    uint16_t *kc = nullptr, *vc = nullptr;  // cache base of this layer: [S][nKV][n_ctx][D] f16
+    int n_ctx = 0, S = 0, nH = 0, nKV = 0, D = 0;
+    int max_splits = 1;           // grid z; chunk = 256 positions
+    float *part = nullptr;        // [S][nH][max_splits][D + 2]
+    uint16_t *out = nullptr;      // [S][nH*D] f16 (rounded attention output, the O-proj input)
+};
+bool attn_decode(const AttnParams &p, hipStream_t s);
+constexpr int ATTN_CHUNK = 256;
+
+// CB0 logit processing + greedy/sampled selection (tts_transformer.cpp:2417-2499), one block per slot.
+struct Cb0Params {
+    float *logits = nullptr;      // [S][V]
+    int V = 0, S = 0, eos = 2150;
+    uint8_t *seen = nullptr;      // [S][V]
+    const int *frame = nullptr;   // [S]
+    const int *n_tokens = nullptr;  // [S]
+    const int *force_frames = nullptr;  // [S] (bench: EOS masked while frame < force)
+    int *done = nullptr;          // [S] frames emitted when finished (EOS), else -1
+    int *token = nullptr;         // [S][16] frame codes; column 0 = selected CB0
+    int32_t *codes = nullptr;     // [S][max_len][ncb]
+    int max_len = 0, ncb = 16;
+    float rep = 1.05f, temperature = 0.f;
+    int top_k = 50;
+    uint64_t seed = 0;
+    const uint64_t *utt = nullptr;  // [S]
+    // pass-1 input of the code predictor: x_next[s] = table[token]
+    const uint16_t *next_table = nullptr;
+    float *x_next = nullptr;
+    int H = 0;
+};
+bool cb0_select(const Cb0Params &p, hipStream_t s);
+
+// code-predictor token (argmax / top-k sampling, trt_cuda_kernels.cu:18-183 semantics) + next-pass gather
+struct CpSelParams {
+    const float *logits = nullptr;  // [S][V]
+    int V = 0, S = 0, step = 0;     // step = 0..14 -> codebook step+1
+    int *tokens = nullptr;          // [S][16] current frame codes (col step+1 written)
+    int32_t *codes = nullptr;       // [S][max_len][ncb]
+    const int *frame = nullptr, *done = nullptr;
+    int max_len = 0, ncb = 16;
+    float temperature = 0.f;
+    int top_k = 50;
+    uint64_t seed = 0;
+    const uint64_t *utt = nullptr;
+    const uint16_t *next_table = nullptr;  // code_pred.codec_embd[step] (nullptr on the last step)
+    float *x_next = nullptr;
+    int H = 0;
+};
+bool cp_select(const CpSelParams &p, hipStream_t s);
+
+// next talker input: e = codec_embd[c0] + sum_c cp_embd[c-1][c_c] + (frame < trailing_len ? trailing[frame] : tts_pad)
+struct StepEmbdParams {
+    const int *tokens = nullptr;     // [S][16]
+    const uint16_t *codec_embd = nullptr;
+    const uint16_t *const *cp_embd = nullptr;  // device array of 15 table pointers
+    const float *trailing = nullptr;  // [S][max_trailing][H]
+    const int *trailing_len = nullptr;
+    int max_trailing = 0;
+    const float *tts_pad = nullptr;   // [S][H]
+    const int *frame = nullptr;
+    float *out = nullptr;             // [S][H]
+    int S = 0, H = 0, ncb = 16;
+};
+bool step_embd(const StepEmbdParams &p, hipStream_t s);
+
+// pos[s]++, frame[s]++
+bool advance(int *pos, int *frame, int S, hipStream_t s);
+
+// *out = t[0] + t[1] + t[2] (f32 rows or f16 table rows; null terms skipped); recipe built on the host
+struct RowTerm { const void *ptr; int is_f16; };
+struct RowRecipe { float *out; RowTerm t[3]; };
+bool rows_recipe(const RowRecipe *recipe_dev, int n_rows, int H, hipStream_t s);
+
+// src/trt_cuda_kernels.cu drop-ins (C ABI wrappers in capi.cpp)
+void launch_f32_to_f16(const float *in, uint16_t *out, int n, hipStream_t s);
+void launch_argmax_f32(const float *in, int32_t *out, int n, hipStream_t s);
+void launch_embed_lookup(const int32_t *tok, const float *table, float *out, int dim, hipStream_t s);
+void launch_sample_topk_f32(const float *logits, const float *rand_val, int32_t *out, float temperature, int top_k, int n,
+                            hipStream_t s);
+
+}  // namespace q3t

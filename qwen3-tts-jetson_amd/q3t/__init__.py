@@ -1,0 +1,200 @@
+"""Python host mirror of the MI355X Qwen3-TTS decode path (ctypes over include/q3t_backend.h / libq3t.so).
+
+The compute runs in libq3t.so (hand-written gfx950 HIP kernels).  There is NO CPU fallback: importing this
+module fails loudly if the in-tree extension is missing, and every call raises Q3TError with
+q3t_last_error() when the C ABI reports failure (the reference's bool + get_error() convention).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libq3t.so")
+
+VOCODER_FULL = 0
+VOCODER_CHUNK40 = 1
+
+
+class Q3TError(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libq3t.so not built at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "(make -C qwen3-tts-jetson_amd/csrc)")
+
+_lib = C.CDLL(LIB_PATH)
+
+
+class Config(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "hidden", "n_layers", "n_heads", "n_kv_heads", "head_dim", "intermediate", "codec_vocab", "n_codebooks",
+        "text_vocab", "text_dim", "cp_layers", "cp_vocab", "codec_eos", "has_vocoder", "sample_rate", "max_slots",
+        "max_ctx")]
+
+
+class GenParams(C.Structure):
+    _fields_ = [("max_len", C.c_int32), ("language_id", C.c_int32), ("repetition_penalty", C.c_float),
+                ("temperature", C.c_float), ("top_k", C.c_int32), ("seed", C.c_uint64), ("force_frames", C.c_int32)]
+
+
+_P, _I, _F = C.c_void_p, C.c_int, C.c_float
+_fp = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_lib.q3t_last_error.restype = C.c_char_p
+_lib.q3t_default_params.argtypes = [C.POINTER(GenParams)]
+_lib.q3t_ctx_create.argtypes = [C.c_char_p, C.c_char_p, _I, _I, _I, C.POINTER(_P)]
+_lib.q3t_ctx_destroy.argtypes = [_P]
+_lib.q3t_get_config.argtypes = [_P, C.POINTER(Config)]
+_lib.q3t_generate.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
+                              C.POINTER(GenParams), _ip, _ip]
+_lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+_lib.q3t_vocoder_num_samples.restype = C.c_int64
+_lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
+_lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
+_lib.q3t_talker_forward.argtypes = [_P, _I, _fp, _ip, _P, _P]
+_lib.q3t_codepred_frame.argtypes = [_P, _I, _fp, _ip, _F, C.c_int32, C.c_uint64, C.c_int32, _ip, _P]
+_lib.q3t_cb0_select.argtypes = [_P, _I, _fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _ip, _ip,
+                                C.POINTER(GenParams), _ip]
+_lib.q3t_project_text.argtypes = [_P, _I, _ip, _fp]
+_lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32), _fp, C.POINTER(C.c_int32), _fp]
+
+# names the C ABI must export (checked by tests without a GPU)
+EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
+           "q3t_generate", "q3t_last_timing", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
+           "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
+           "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
+
+
+def lib():
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise Q3TError(_lib.q3t_last_error().decode(errors="replace"))
+
+
+def default_params(**kw):
+    p = GenParams()
+    _lib.q3t_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def _addr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Engine:
+    """One device context (TTSTransformer + code predictor + vocoder resident in HBM)."""
+
+    def __init__(self, tts_gguf, tokenizer_gguf=None, device=0, max_slots=1, max_ctx=4096 + 32):
+        h = _P()
+        _check(_lib.q3t_ctx_create(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
+                                   int(device), int(max_slots), int(max_ctx), C.byref(h)))
+        self.h = h
+        c = Config()
+        _check(_lib.q3t_get_config(self.h, C.byref(c)))
+        self.cfg = {n: getattr(c, n) for n, _ in Config._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.q3t_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- hot path
+    def generate(self, prompts, speakers=None, **params):
+        """prompts: list of token-id lists.  Returns list of [n_frames][16] int32 arrays."""
+        p = default_params(**params)
+        n = len(prompts)
+        toks = [np.ascontiguousarray(t, np.int32) for t in prompts]
+        tarr = (C.POINTER(C.c_int32) * n)(*[t.ctypes.data_as(C.POINTER(C.c_int32)) for t in toks])
+        ntok = np.array([len(t) for t in toks], np.int32)
+        sarr = None
+        keep = []
+        if speakers is not None:
+            sp = [np.ascontiguousarray(s, np.float32) for s in speakers]
+            keep = sp
+            sarr = (C.POINTER(C.c_float) * n)(*[s.ctypes.data_as(C.POINTER(C.c_float)) for s in sp])
+        codes = np.zeros((n, p.max_len, 16), np.int32)
+        nf = np.zeros(n, np.int32)
+        _check(_lib.q3t_generate(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf))
+        del keep
+        return [codes[i, :nf[i]].copy() for i in range(n)]
+
+    def last_timing(self):
+        a, b = C.c_double(0), C.c_double(0)
+        _check(_lib.q3t_last_timing(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    # ---- vocoder
+    def vocoder_num_samples(self, n_frames, mode=VOCODER_FULL):
+        return _lib.q3t_vocoder_num_samples(self.h, int(n_frames), int(mode))
+
+    def vocoder(self, codes, mode=VOCODER_FULL):
+        codes = np.ascontiguousarray(codes, np.int32).reshape(-1, 16)
+        n = self.vocoder_num_samples(codes.shape[0], mode)
+        if n < 0:
+            raise Q3TError("vocoder not loaded")
+        pcm = np.zeros(max(n, 1), np.float32)
+        ns = C.c_int64(0)
+        _check(_lib.q3t_vocoder_decode(self.h, codes, codes.shape[0], int(mode), pcm, C.byref(ns)))
+        return pcm[:ns.value]
+
+    # ---- stages
+    def talker_forward(self, embd, pos):
+        embd = np.ascontiguousarray(embd, np.float32).reshape(-1, self.cfg["hidden"])
+        n = embd.shape[0]
+        pos = np.ascontiguousarray(np.broadcast_to(np.asarray(pos, np.int32), (n,)))
+        hid = np.zeros((n, self.cfg["hidden"]), np.float32)
+        lg = np.zeros((n, self.cfg["codec_vocab"]), np.float32)
+        _check(_lib.q3t_talker_forward(self.h, n, embd, pos, _addr(hid), _addr(lg)))
+        return hid, lg
+
+    def codepred_frame(self, hidden, cb0, temperature=0.0, top_k=50, seed=0, frame=0, want_logits=False):
+        hidden = np.ascontiguousarray(hidden, np.float32).reshape(-1, self.cfg["hidden"])
+        n = hidden.shape[0]
+        cb0 = np.ascontiguousarray(np.broadcast_to(np.asarray(cb0, np.int32), (n,)))
+        codes = np.zeros((n, 15), np.int32)
+        lg = np.zeros((n, 15, self.cfg["cp_vocab"]), np.float32) if want_logits else None
+        _check(_lib.q3t_codepred_frame(self.h, n, hidden, cb0, float(temperature), int(top_k), int(seed), int(frame),
+                                       codes, _addr(lg)))
+        return (codes, lg) if want_logits else codes
+
+    def cb0_select(self, logits, seen, frame, n_tokens, **params):
+        p = default_params(**params)
+        logits = np.ascontiguousarray(logits, np.float32).reshape(-1, self.cfg["codec_vocab"])
+        n = logits.shape[0]
+        seen = np.ascontiguousarray(seen, np.uint8).reshape(n, -1)
+        frame = np.ascontiguousarray(np.broadcast_to(np.asarray(frame, np.int32), (n,)))
+        nt = np.ascontiguousarray(np.broadcast_to(np.asarray(n_tokens, np.int32), (n,)))
+        out = np.zeros(n, np.int32)
+        _check(_lib.q3t_cb0_select(self.h, n, logits, seen, frame, nt, C.byref(p), out))
+        return out
+
+    def project_text(self, toks):
+        toks = np.ascontiguousarray(toks, np.int32)
+        out = np.zeros((len(toks), self.cfg["hidden"]), np.float32)
+        _check(_lib.q3t_project_text(self.h, len(toks), toks, out))
+        return out
+
+    def prefill_embd(self, toks, speaker=None, language_id=2050):
+        toks = np.ascontiguousarray(toks, np.int32)
+        H = self.cfg["hidden"]
+        pre = np.zeros((10, H), np.float32)
+        tr = np.zeros((max(1, len(toks) - 8), H), np.float32)
+        pad = np.zeros(H, np.float32)
+        pl, tl = C.c_int32(0), C.c_int32(0)
+        sp = None if speaker is None else np.ascontiguousarray(speaker, np.float32)
+        _check(_lib.q3t_prefill_embd(self.h, toks, len(toks), _addr(sp), int(language_id), pre, C.byref(pl), tr,
+                                     C.byref(tl), pad))
+        return pre[:pl.value], tr[:tl.value], pad
