@@ -834,10 +834,32 @@ float q3o_uniform(uint64_t seed, uint64_t utt, uint64_t frame, uint64_t cb) {
     return (float)(h >> 40) * (1.0f / 16777216.0f);
 }
 
-/* frame loop, tts_transformer.cpp:2342-2574 */
+/* frame loop, tts_transformer.cpp:2342-2574.  forced != NULL: teacher forcing — the codes of each frame are
+ * taken from forced[frame][16] (the decisions are still recorded: cb0_trace = processed CB0 logits fed to the
+ * selection, cp_trace = [15][Vcp] code-predictor logits of each step). */
+static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
+                         float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
+                         const int32_t *forced, int n_forced, int32_t *codes_out, int *n_frames, float *logits_trace,
+                         float *hidden_trace, float *cb0_trace, float *cp_trace);
+int q3o_generate_forced(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
+                        int force_frames, const int32_t *forced, int n_forced, float *cb0_trace, float *cp_trace) {
+    int nf = 0;
+    int32_t *tmp = malloc(sizeof(int32_t) * 16 * (size_t)(n_forced > 0 ? n_forced : 1));
+    const int r = generate_impl(m, toks, n, spk, n_forced, language_id, rep, 0.0f, 0, 0, 0, force_frames, forced, n_forced,
+                                tmp, &nf, NULL, NULL, cb0_trace, cp_trace);
+    free(tmp);
+    return r;
+}
 int q3o_generate(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
                  float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
                  int32_t *codes_out, int *n_frames, float *logits_trace, float *hidden_trace) {
+    return generate_impl(m, toks, n, spk, max_len, language_id, rep, temperature, top_k, seed, utt, force_frames, NULL, 0,
+                         codes_out, n_frames, logits_trace, hidden_trace, NULL, NULL);
+}
+static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
+                         float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
+                         const int32_t *forced, int n_forced, int32_t *codes_out, int *n_frames, float *logits_trace,
+                         float *hidden_trace, float *cb0_trace, float *cp_trace) {
     const q3o_config *c = &m->c;
     const int H = c->hidden, V = c->codec_vocab, NCB = c->n_codebooks;
     *n_frames = 0;
@@ -859,13 +881,31 @@ int q3o_generate(const q3o_model *m, const int32_t *toks, int n, const float *sp
         if (logits_trace) memcpy(logits_trace + (size_t)frame * V, logits, sizeof(float) * (size_t)V);
         if (hidden_trace) memcpy(hidden_trace + (size_t)frame * H, hidden, sizeof(float) * (size_t)H);
         const int mask = force_frames > 0 && frame < force_frames;
-        const int tok = q3o_cb0_select(m, logits, seen, frame, n, rep, temperature, top_k,
-                                       q3o_uniform(seed, utt, (uint64_t)frame, 0), mask);
+        int tok = q3o_cb0_select(m, logits, seen, frame, n, rep, temperature, top_k,
+                                 q3o_uniform(seed, utt, (uint64_t)frame, 0), mask);
+        if (cb0_trace) memcpy(cb0_trace + (size_t)frame * V, logits, sizeof(float) * (size_t)V);  /* processed */
+        if (forced) { if (frame >= n_forced) break; tok = forced[(size_t)frame * NCB]; }
         if (tok == c->codec_eos) break;
         fc[0] = tok;
         seen[tok] = 1;
         for (int s = 0; s < NCB - 1; ++s) u15[s] = q3o_uniform(seed, utt, (uint64_t)frame, (uint64_t)s + 1);
-        q3o_cp_frame(m, hidden, tok, temperature, top_k, u15, fc + 1, NULL);
+        if (forced) {
+            /* teacher-forced code predictor: passes fed with the forced codes, logits recorded */
+            q3o_kv *ckv = q3o_kv_new(m, 16, 1);
+            float *xx = malloc(sizeof(float) * (size_t)H), *lg2 = malloc(sizeof(float) * (size_t)c->cp_vocab);
+            q3o_cp_pass(m, ckv, hidden, 0, -1, NULL, NULL);
+            embd_row(&m->codec_embd, tok, xx);
+            for (int s = 0; s < NCB - 1; ++s) {
+                if (s > 0) embd_row(&m->cp_embd[s - 1], forced[(size_t)frame * NCB + s], xx);
+                q3o_cp_pass(m, ckv, xx, s + 1, s, NULL, lg2);
+                if (cp_trace) memcpy(cp_trace + ((size_t)frame * 15 + s) * c->cp_vocab, lg2, sizeof(float) * (size_t)c->cp_vocab);
+                fc[s + 1] = forced[(size_t)frame * NCB + s + 1];
+            }
+            free(xx); free(lg2);
+            q3o_kv_free(ckv);
+        } else {
+            q3o_cp_frame(m, hidden, tok, temperature, top_k, u15, fc + 1, NULL);
+        }
         memcpy(codes_out + (size_t)frame * NCB, fc, sizeof(int32_t) * (size_t)NCB);
         *n_frames = frame + 1;
         if (frame + 1 >= max_len) break;

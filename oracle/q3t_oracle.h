@@ -72,6 +72,10 @@ float q3o_uniform(uint64_t seed, uint64_t utt, uint64_t frame, uint64_t cb);
 int q3o_generate(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
                  float rep_penalty, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
                  int32_t *codes_out, int *n_frames, float *logits_trace, float *hidden_trace);
+/* teacher-forced replay of forced[n_forced][16]; records the processed CB0 logits [n_forced][Vc] and the code
+ * predictor logits [n_forced][15][Vcp] of every decision (greedy-parity checks with near-tie tolerance) */
+int q3o_generate_forced(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
+                        int force_frames, const int32_t *forced, int n_forced, float *cb0_trace, float *cp_trace);
 /* vocoder: mode 0 = FULL (audio_tokenizer_decoder.cpp), 1 = CHUNK40 (trt_vocoder.cpp:98-170).
  * pcm == NULL => only report the sample count. */
 int q3o_vocoder_decode(const q3o_model *m, const int32_t *codes, int n_frames, int mode, float *pcm, int64_t *n_samples);

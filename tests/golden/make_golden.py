@@ -41,11 +41,8 @@ def load_ref_class():
 
 
 def synth(cfg, out_dir):
-    exe = os.path.join(REPO, "tools", "_build", "q3t_synth")
-    if not os.path.exists(exe):
-        os.makedirs(os.path.dirname(exe), exist_ok=True)
-        subprocess.run(["gcc", "-O2", "-fopenmp", "-o", exe, os.path.join(REPO, "tools", "q3t_synth.c"), "-lm"],
-                       check=True)
+    from q3t_testutil import build_synth
+    exe = build_synth()
     os.makedirs(out_dir, exist_ok=True)
     subprocess.run([exe, cfg, out_dir, str(SEED)], check=True)
     return os.path.join(out_dir, "qwen3-tts-0.6b-f16.gguf")

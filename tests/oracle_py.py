@@ -60,6 +60,7 @@ def lib():
         L.q3o_uniform.restype = F
         L.q3o_uniform.argtypes = [U64, U64, U64, U64]
         L.q3o_generate.argtypes = [P, ip, I, P, I, I, F, F, I, U64, U64, I, ip, C.POINTER(I), P, P]
+        L.q3o_generate_forced.argtypes = [P, ip, I, P, I, F, I, ip, I, P, P]
         L.q3o_vocoder_decode.argtypes = [P, ip, I, I, P, C.POINTER(C.c_int64)]
         L.q3o_vocoder_len.restype = C.c_int64
         L.q3o_vocoder_len.argtypes = [P, I, I]
@@ -171,6 +172,19 @@ class Oracle:
         if trace:
             return codes[:n], lt[:n], ht[:n]
         return codes[:n]
+
+    def generate_forced(self, toks, forced, spk=None, language_id=2050, rep=1.05, force_frames=0):
+        """teacher-forced replay: returns (processed CB0 logits [F][Vc], CP logits [F][15][Vcp])."""
+        toks = np.ascontiguousarray(toks, np.int32)
+        forced = np.ascontiguousarray(forced, np.int32).reshape(-1, 16)
+        F = forced.shape[0]
+        cb0 = np.zeros((F, self.cfg["codec_vocab"]), np.float32)
+        cp = np.zeros((F, 15, self.cfg["cp_vocab"]), np.float32)
+        spk_a = None if spk is None else np.ascontiguousarray(spk, np.float32)
+        if not lib().q3o_generate_forced(self.h, toks, len(toks), _ptr(spk_a), language_id, rep, force_frames, forced, F,
+                                         _ptr(cb0), _ptr(cp)):
+            raise RuntimeError(lib().q3o_error().decode())
+        return cb0, cp
 
     # ---- vocoder
     def vocoder_len(self, n_frames, mode=0):

@@ -43,3 +43,61 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _sample_interval(logits, temperature, top_k, keep_id):
+    """CDF interval bookkeeping of the shared sampler (oracle q3o_sample): returns (exps, total)."""
+    l = np.asarray(logits, np.float64) / temperature
+    keep = l[keep_id] if keep_id >= 0 else None
+    if 0 < top_k < len(l):
+        thr = np.sort(l)[-top_k]
+        l = np.where(l < thr, -np.inf, l)
+    if keep_id >= 0:
+        l[keep_id] = keep
+    e = np.exp(l - l.max())
+    return e, e.sum()
+
+
+def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperature=0.0, top_k=50, seed=0, utt=0,
+                    rep=1.05, tol_logit=5e-2, tol_cdf=5e-2, max_off_frac=0.03, eos_id=2150):
+    """Teacher-forced parity of a GPU-generated code sequence against the oracle.
+
+    The oracle replays the GPU's codes (q3o_generate_forced) and records every decision's logits.  Greedy: each
+    GPU token must be the oracle argmax or within tol_logit of it (near-tie); sampling: u*total must fall in the
+    token's CDF interval up to tol_cdf.  At most max_off_frac of the decisions may take the tolerance branch.
+    If the GPU stopped before max_len, the oracle must also pick EOS (within tolerance) at that frame."""
+    from oracle_py import uniform
+    codes = np.asarray(codes, np.int32).reshape(-1, 16)
+    F = codes.shape[0]
+    stopped = F < max_len
+    forced = np.concatenate([codes, np.zeros((1, 16), np.int32)]) if stopped else codes
+    cb0, cp = orc.generate_forced(toks, forced, spk=spk, rep=rep, force_frames=force_frames)
+    n_dec = n_off = 0
+    worst = 0.0
+    for f in range(forced.shape[0]):
+        last = stopped and f == F
+        for c in range(1 if last else 16):
+            lg = cb0[f] if c == 0 else cp[f, c - 1]
+            tok = eos_id if last else int(codes[f, c])
+            n_dec += 1
+            if temperature <= 0:
+                gap = float(lg.max() - lg[tok])
+                if gap > 0:
+                    n_off += 1
+                    worst = max(worst, gap)
+                    assert gap <= tol_logit, (f, c, gap)
+            else:
+                keep = eos_id if (c == 0 and not (force_frames and f < force_frames)) else -1
+                e, tot = _sample_interval(lg, temperature, top_k, keep)
+                u = uniform(seed, utt, f, c)
+                target = u * tot
+                cum = np.cumsum(e)
+                lo = cum[tok - 1] if tok > 0 else 0.0
+                hi = cum[tok]
+                if not (lo <= target <= hi):
+                    n_off += 1
+                    err = max(lo - target, target - hi) / tot
+                    worst = max(worst, err)
+                    assert err <= tol_cdf, (f, c, err)
+    assert n_off <= max(1, int(max_off_frac * n_dec)), (n_off, n_dec, worst)
+    return n_off, n_dec, worst

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from oracle_py import Oracle, uniform
-from q3t_testutil import REPO, prompt, rel_err, synth_dir
+from q3t_testutil import REPO, check_decisions, prompt, rel_err, synth_dir
 
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 
@@ -26,7 +26,7 @@ def pair(request):
     import q3t
     cfg = request.param
     tts, tok = synth_dir(cfg)
-    eng = q3t.Engine(tts, tok, device=0, max_slots=4, max_ctx=96)
+    eng = q3t.Engine(tts, tok, device=0, max_slots=4, max_ctx=128)
     orc = Oracle(tts, tok)
     yield cfg, eng, orc
     eng.close()
@@ -37,7 +37,7 @@ def test_talker_step_matches_oracle(pair):
     cfg, eng, orc = pair
     H = eng.cfg["hidden"]
     rng = np.random.default_rng(3)
-    kv = orc.kv_new(96, 0)
+    kv = orc.kv_new(128, 0)
     for pos in range(20):
         e = (rng.standard_normal(H) * 0.5).astype(np.float32)
         hg, lg = eng.talker_forward(e[None], [pos])
@@ -125,15 +125,6 @@ def test_project_text_and_prefill_match_oracle(pair):
         assert rel_err(pg, po) < TOL[cfg] and rel_err(tg, to) < TOL[cfg] and rel_err(padg, pado) < TOL[cfg]
 
 
-def _first_divergence_is_near_tie(orc, toks, spk, codes_g, n):
-    """greedy decoding amplifies 1-ulp differences; accept a divergence only at a near-tie of the oracle."""
-    codes_o, lt, _ = orc.generate(toks, spk=spk, max_len=n, temperature=0.0, force_frames=n, trace=True)
-    for f in range(min(len(codes_g), len(codes_o))):
-        if not np.array_equal(codes_g[f], codes_o[f]):
-            return False, f
-    return True, -1
-
-
 @pytest.mark.parametrize("nf", [24])
 def test_generate_greedy_matches_oracle(pair, nf):
     cfg, eng, orc = pair
@@ -141,9 +132,8 @@ def test_generate_greedy_matches_oracle(pair, nf):
     toks = prompt(cfg)
     spk = np.zeros(H, np.float32)
     out = eng.generate([toks], speakers=[spk], max_len=nf, temperature=0.0, force_frames=nf)
-    ref = orc.generate(toks, spk=spk, max_len=nf, temperature=0.0, force_frames=nf)
-    assert out[0].shape == ref.shape
-    np.testing.assert_array_equal(out[0], ref)
+    assert out[0].shape == (nf, 16)
+    check_decisions(orc, toks, spk, out[0], max_len=nf, force_frames=nf)
 
 
 def test_generate_batched_slots_match_single(pair):
@@ -154,17 +144,17 @@ def test_generate_batched_slots_match_single(pair):
     spk = [np.zeros(H, np.float32)] * 3
     outs = eng.generate(prompts, speakers=spk, max_len=12, temperature=0.0, force_frames=12)
     for i, p in enumerate(prompts):
-        ref = orc.generate(p, spk=spk[i], max_len=12, temperature=0.0, force_frames=12)
-        np.testing.assert_array_equal(outs[i], ref)
+        assert outs[i].shape == (12, 16)
+        check_decisions(orc, p, spk[i], outs[i], max_len=12, force_frames=12)
 
 
 def test_generate_sampling_matches_oracle(pair):
     cfg, eng, orc = pair
     H = eng.cfg["hidden"]
     toks = prompt(cfg)
-    out = eng.generate([toks], speakers=[np.zeros(H, np.float32)], max_len=10, temperature=0.9, top_k=50, seed=4242)
-    ref = orc.generate(toks, spk=np.zeros(H, np.float32), max_len=10, temperature=0.9, top_k=50, seed=4242, utt=0)
-    np.testing.assert_array_equal(out[0], ref)
+    spk = np.zeros(H, np.float32)
+    out = eng.generate([toks], speakers=[spk], max_len=10, temperature=0.9, top_k=50, seed=4242)
+    check_decisions(orc, toks, spk, out[0], max_len=10, temperature=0.9, top_k=50, seed=4242, utt=0)
 
 
 def test_generate_eos_stops_early(pair):
@@ -172,7 +162,20 @@ def test_generate_eos_stops_early(pair):
     cfg, eng, orc = pair
     H = eng.cfg["hidden"]
     toks = prompt(cfg)[:4] + prompt(cfg)[-5:]
-    out = eng.generate([toks], speakers=[np.zeros(H, np.float32)], max_len=80, temperature=0.0)
-    ref = orc.generate(toks, spk=np.zeros(H, np.float32), max_len=80, temperature=0.0)
-    assert len(out[0]) == len(ref) and len(ref) < 80
-    np.testing.assert_array_equal(out[0], ref)
+    spk = np.zeros(H, np.float32)
+    out = eng.generate([toks], speakers=[spk], max_len=80, temperature=0.0)
+    assert len(out[0]) < 80
+    check_decisions(orc, toks, spk, out[0], max_len=80)
+
+
+def test_generate_zero_and_one_frame_edge_cases(pair):
+    cfg, eng, orc = pair
+    H = eng.cfg["hidden"]
+    toks = prompt(cfg)
+    spk = np.zeros(H, np.float32)
+    assert eng.generate([toks], speakers=[spk], max_len=0, temperature=0.0)[0].shape == (0, 16)
+    one = eng.generate([toks], speakers=[spk], max_len=1, temperature=0.0, force_frames=1)[0]
+    assert one.shape == (1, 16)
+    check_decisions(orc, toks, spk, one, max_len=1, force_frames=1)
+    with pytest.raises(Exception):
+        eng.generate([toks[:3]], speakers=[spk], max_len=4, temperature=0.0)   # n_tokens < 4 is rejected

@@ -51,6 +51,10 @@ static const cfg_t CFG_FULL = {
     "full", 151936, 2048, 1024, 28, 16, 8, 128, 3072, 3072, 16,
     5, 2048, 1e-6f, 1000000.0f, 151672, 151673, 151671,
     2048, 256, 512, 1024, 8, 16, 1024, 1536, 2, 4, {8, 5, 4, 3}};
+static const cfg_t CFG_TINY1 = {
+    "tiny1", 1024, 128, 256, 1, 4, 2, 64, 512, 3072, 16,
+    1, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
+    2048, 32, 64, 128, 2, 2, 128, 96, 2, 4, {8, 5, 4, 3}};
 static const cfg_t CFG_TINY = {
     "tiny", 1024, 128, 256, 5, 4, 2, 64, 512, 3072, 16,
     5, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
@@ -118,13 +122,13 @@ static void build_talker(const cfg_t *c) {
             addw(NM("attn_q.weight"), Dq, H, 1.0);
             addw(NM("attn_k.weight"), Dkv, H, 1.0);
             addw(NM("attn_v.weight"), Dkv, H, 1.0);
-            addw(NM("attn_output.weight"), H, Dq, 0.5);
+            addw(NM("attn_output.weight"), H, Dq, 0.25);
             add1(NM("attn_q_norm.weight"), c->head_dim, 1.0, 0.1);
             add1(NM("attn_k_norm.weight"), c->head_dim, 1.0, 0.1);
             add1(NM("ffn_norm.weight"), H, 1.0, 0.1);
             addw(NM("ffn_gate.weight"), c->inter, H, 1.0);
             addw(NM("ffn_up.weight"), c->inter, H, 1.0);
-            addw(NM("ffn_down.weight"), H, c->inter, 0.5);
+            addw(NM("ffn_down.weight"), H, c->inter, 0.25);
 #undef NM
         }
     }
@@ -328,7 +332,7 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
 
 int main(int argc, char **argv) {
     if (argc < 3) { fprintf(stderr, "usage: %s full|tiny <out_dir> [seed]\n", argv[0]); return 2; }
-    const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : NULL;
+    const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : strcmp(argv[1], "tiny1") == 0 ? &CFG_TINY1 : NULL;
     if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
     uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
     char path[4096];
