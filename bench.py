@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""bench.py — frames/s + RTF of the MI355X Qwen3-TTS decode path (BASELINE.json metric, configs[1]).
+
+A "step" = one utterance batch through the whole hot path: text projection + prefill, `--frames` audio frames
+(talker step -> CB0 selection -> 16-pass code predictor -> step embedding, one hipGraph per frame) and the
+vocoder over the produced codes.  Inputs (prompt ids) are tiny; weights and all state live in HBM.
+Synthetic 0.6B-shaped weights (tools/q3t_synth.c, seed 0x51E3775), synthetic 16-token prompt, reference
+sampling defaults (temperature 0.9, top-k 50, repetition penalty 1.05) with EOS masked for exactly --frames
+frames (force_frames).
+
+N GPUs: one process per GPU (torchrun), utterances sharded across ranks (weak scaling), barrier + max-over-ranks
+timing.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+SAMPLES_PER_FRAME = 1920           # 24 kHz / 12.5 Hz (src/trt_vocoder.h:50)
+FRAME_SEC = 0.08
+TALKER_WEIGHT_BYTES = 887_095_296  # 28 x 15,728,640 x 2 + 3072 x 1024 x 2
+KV_BYTES_PER_POS = 114_688         # 28 layers x 2 (K,V) x 8 heads x 128 x 2 B
+CP_PASS_BYTES = 5 * 15_728_640 * 2
+CP_HEAD_BYTES = 2048 * 1024 * 2
+HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(tts, tok, prompt, frames, vocoder_mode):
+    """Oracle (C restatement of the reference GGML-CPU path) timed on a bounded sample, extrapolated to the
+    workload: t = t_prefill + frames * (t_frame + t_vocoder_per_frame)."""
+    import numpy as np
+    from oracle_py import Oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    o = Oracle(tts, tok, threads=threads)
+    spk = np.zeros(o.cfg["hidden"], np.float32)
+    kw = dict(spk=spk, temperature=0.9, top_k=50, seed=1, rep=1.05)
+    t0 = time.perf_counter()
+    o.generate(prompt, max_len=1, force_frames=1, **kw)
+    t1 = time.perf_counter()
+    n = 4
+    codes = o.generate(prompt, max_len=1 + n, force_frames=1 + n, **kw)
+    t2 = time.perf_counter()
+    t_frame = ((t2 - t1) - (t1 - t0)) / n
+    t_prefill = max(0.0, (t1 - t0) - t_frame)
+    t_voc = 0.0
+    if vocoder_mode is not None:
+        t3 = time.perf_counter()
+        o.vocoder(codes, vocoder_mode)
+        t_voc = (time.perf_counter() - t3) / len(codes)
+    total = t_prefill + frames * (t_frame + t_voc)
+    o.close()
+    return {"value": round(frames / total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/q3t_oracle.c (GGML-CPU restatement, f16 weights, {threads} OpenMP threads) on the full "
+                      f"0.6B synthetic model: prefill + {1 + n} frames + vocoder of {len(codes)} frames, "
+                      f"extrapolated to {frames} frames (t_prefill {t_prefill:.2f}s, {t_frame * 1e3:.0f} ms/frame, "
+                      f"vocoder {t_voc * 1e3:.0f} ms/frame)",
+            "sample_seconds": round(t2 - t0, 2), "rtf": round(total / (frames * FRAME_SEC), 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
+    ap.add_argument("--vocoder", choices=["full", "chunk40", "none"], default="full")
+    ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
+    ap.add_argument("--cfg", default="full", choices=["full", "tiny"])
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")   # RCCL on ROCm
+    import q3t
+    from q3t_testutil import prompt as make_prompt, synth_dir
+
+    # synthetic GGUFs: written once per node by local rank 0 (same files for every rank)
+    if local_rank == 0:
+        tts, tok = synth_dir(args.cfg)
+    if dist:
+        dist.barrier()
+    if local_rank != 0:
+        tts, tok = synth_dir(args.cfg)
+    voc_mode = {"full": q3t.VOCODER_FULL, "chunk40": q3t.VOCODER_CHUNK40, "none": None}[args.vocoder]
+    eng = q3t.Engine(tts, tok if voc_mode is not None else None, device=local_rank if world > 1 else 0,
+                     max_slots=args.batch, max_ctx=args.frames + 32)
+    B = args.batch
+    prompt = make_prompt(args.cfg)
+    H = eng.cfg["hidden"]
+    prompts = [prompt] * B
+    spks = [np.zeros(H, np.float32)] * B
+    stats = {"prefill_ms": 0.0, "frames_ms": 0.0, "vocoder_ms": 0.0}
+
+    def step(k):
+        codes = eng.generate(prompts, speakers=spks, max_len=args.frames, temperature=0.9, top_k=50,
+                             repetition_penalty=1.05, seed=1000 * rank + k, force_frames=args.frames)
+        pm, fm = eng.last_timing()
+        stats["prefill_ms"] += pm
+        stats["frames_ms"] += fm
+        if voc_mode is not None:
+            t = time.perf_counter()
+            for c in codes:
+                eng.vocoder(c, voc_mode)
+            stats["vocoder_ms"] += (time.perf_counter() - t) * 1e3
+        return codes
+
+    for w in range(args.warmup):
+        step(-1 - w)
+    for k in stats:
+        stats[k] = 0.0
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_frames = world * B * args.frames * args.steps
+    value = total_frames / elapsed
+
+    # ---- roofline of the talker decode step (SURVEY §8(d) definition) at the mid-utterance position
+    p_mid = 10 + args.frames // 2
+    t_talker = eng.time_stage(0, B, p_mid, 20)
+    talker_bytes = TALKER_WEIGHT_BYTES + KV_BYTES_PER_POS * (p_mid + 2) * B
+    achieved = talker_bytes / (t_talker * 1e-3) / 1e9
+    t_cp = eng.time_stage(1, B, p_mid, 10)
+    cp_bytes = 16 * CP_PASS_BYTES + 15 * CP_HEAD_BYTES
+
+    if rank == 0:
+        res = {
+            "metric": "audio frames/sec (12 Hz frames) + RTF, Qwen3-TTS-0.6B batch=1 and batch=8xN",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f16",
+            "data": "synthetic (random-init 0.6B-shaped weights from tools/q3t_synth.c, 16-token prompt)",
+            "config": {"workload": f"configs[1]: Qwen3-TTS-0.6B {B} utterance(s)/GPU x {args.frames} frames, "
+                                   f"talker+code-predictor+vocoder({args.vocoder}) HIP path, temp 0.9 top-k 50",
+                       "utterances_per_gpu": B, "frames": args.frames, "vocoder": args.vocoder,
+                       "parallelism": f"utterance-sharded dp{world}"},
+            "rtf": round(ms_per_step / 1e3 / (args.frames * FRAME_SEC), 5),
+            "x_realtime": round(args.frames * FRAME_SEC * B / (ms_per_step / 1e3), 1),
+            "breakdown_ms_per_step": {k: round(v / args.steps, 2) for k, v in stats.items()},
+            "talker_step_ms": round(t_talker, 4), "cp_frame_ms": round(t_cp, 4),
+            "roofline": {"bound": "hbm", "kernel": "talker decode step (28 layers + codec head, hipGraph replay)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_launch": talker_bytes, "launch_ms": round(t_talker, 4)},
+            "cp_roofline": {"achieved": round(cp_bytes / (t_cp * 1e-3) / 1e9, 1), "unit": "GB/s",
+                            "bytes_per_frame": cp_bytes, "note": "157 MB of CP weights re-read 16x per frame "
+                            "(Infinity-Cache resident), algorithmic bytes / time"},
+        }
+        if args.cpu_baseline == "on" and world == 1:
+            try:
+                res["cpu_baseline"] = cpu_baseline(tts, tok if voc_mode is not None else None, prompt, args.frames,
+                                                   voc_mode)
+            except Exception as e:  # the GPU number stands on its own
+                res["cpu_baseline"] = {"value": None, "error": str(e)}
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,6 +69,10 @@ int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const in
 /* device time (ms) of the last q3t_generate: prefill and frame loop */
 int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms);
 
+/* replay the captured stage graph (0 = talker decode step, 1 = 16-pass code-predictor frame) `iters` times at
+ * KV position `pos` for n_slots slots; *ms = mean device time per replay (HIP events on the context stream) */
+int q3t_time_stage(q3t_ctx *ctx, int stage, int n_slots, int pos, int iters, double *ms);
+
 /* ---- vocoder */
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);
 int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, int32_t n_frames, int mode,

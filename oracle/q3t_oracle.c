@@ -800,6 +800,24 @@ int q3o_cp_frame(const q3o_model *m, const float *hidden, int cb0, float tempera
     return 1;
 }
 
+/* teacher-forced code predictor: passes fed with the given codes, logits of every step recorded */
+int q3o_cp_frame_forced(const q3o_model *m, const float *hidden, int cb0, const int32_t *codes15, float *logits_all) {
+    const q3o_config *c = &m->c;
+    const int H = c->hidden, V = c->cp_vocab;
+    q3o_kv *kv = q3o_kv_new(m, 16, 1);
+    float *x = malloc(sizeof(float) * (size_t)H), *lg = malloc(sizeof(float) * (size_t)V);
+    q3o_cp_pass(m, kv, hidden, 0, -1, NULL, NULL);
+    embd_row(&m->codec_embd, cb0, x);
+    for (int s = 0; s < c->n_codebooks - 1; ++s) {
+        if (s > 0) embd_row(&m->cp_embd[s - 1], codes15[s - 1], x);
+        q3o_cp_pass(m, kv, x, s + 1, s, NULL, lg);
+        if (logits_all) memcpy(logits_all + (size_t)s * V, lg, sizeof(float) * (size_t)V);
+    }
+    free(x); free(lg);
+    q3o_kv_free(kv);
+    return 1;
+}
+
 /* CB0 logit processing, tts_transformer.cpp:2417-2495 */
 int q3o_cb0_select(const q3o_model *m, float *logits, const uint8_t *seen, int frame, int n_tokens, float rep,
                    float temperature, int top_k, float u, int eos_mask) {
@@ -890,19 +908,9 @@ static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const f
         seen[tok] = 1;
         for (int s = 0; s < NCB - 1; ++s) u15[s] = q3o_uniform(seed, utt, (uint64_t)frame, (uint64_t)s + 1);
         if (forced) {
-            /* teacher-forced code predictor: passes fed with the forced codes, logits recorded */
-            q3o_kv *ckv = q3o_kv_new(m, 16, 1);
-            float *xx = malloc(sizeof(float) * (size_t)H), *lg2 = malloc(sizeof(float) * (size_t)c->cp_vocab);
-            q3o_cp_pass(m, ckv, hidden, 0, -1, NULL, NULL);
-            embd_row(&m->codec_embd, tok, xx);
-            for (int s = 0; s < NCB - 1; ++s) {
-                if (s > 0) embd_row(&m->cp_embd[s - 1], forced[(size_t)frame * NCB + s], xx);
-                q3o_cp_pass(m, ckv, xx, s + 1, s, NULL, lg2);
-                if (cp_trace) memcpy(cp_trace + ((size_t)frame * 15 + s) * c->cp_vocab, lg2, sizeof(float) * (size_t)c->cp_vocab);
-                fc[s + 1] = forced[(size_t)frame * NCB + s + 1];
-            }
-            free(xx); free(lg2);
-            q3o_kv_free(ckv);
+            q3o_cp_frame_forced(m, hidden, tok, forced + (size_t)frame * NCB + 1,
+                                cp_trace ? cp_trace + (size_t)frame * 15 * c->cp_vocab : NULL);
+            for (int s = 0; s < NCB - 1; ++s) fc[s + 1] = forced[(size_t)frame * NCB + s + 1];
         } else {
             q3o_cp_frame(m, hidden, tok, temperature, top_k, u15, fc + 1, NULL);
         }

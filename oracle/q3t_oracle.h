@@ -59,6 +59,8 @@ int q3o_cp_pass(const q3o_model *m, q3o_kv *kv, const float *x, int pos, int hea
 /* 15 codes of one frame from the talker hidden + cb0. u15: 15 uniforms (sampling) or NULL for greedy. */
 int q3o_cp_frame(const q3o_model *m, const float *hidden, int cb0, float temperature, int top_k, const float *u15,
                  int32_t *codes, float *logits_all);
+/* same passes fed with the given codes15 (teacher forcing); logits_all [15][Vcp] */
+int q3o_cp_frame_forced(const q3o_model *m, const float *hidden, int cb0, const int32_t *codes15, float *logits_all);
 /* top-k/temperature sampling by inverse CDF (temperature<=0 => first-max argmax). keep_id>=0 survives top-k. */
 int q3o_sample(const float *logits, int n, float temperature, int top_k, float u, int keep_id);
 /* CB0 logit processing (tts_transformer.cpp:2417-2495) on logits in place; seen = [Vc] flags of emitted CB0s.

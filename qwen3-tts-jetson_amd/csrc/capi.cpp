@@ -100,6 +100,14 @@ int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms) {
     return Q3T_OK;
 }
 
+int q3t_time_stage(q3t_ctx *ctx, int stage, int n, int pos, int iters, double *ms) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (!ms) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.time_stage(stage, n, pos, iters, ms) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode) {
     if (!ctx) return -1;
     q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();

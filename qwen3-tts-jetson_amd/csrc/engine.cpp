@@ -14,6 +14,7 @@ Engine::~Engine() {
     if (device_ >= 0) hipSetDevice(device_);
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     voc_.reset();
     for (void *p : allocs_) hipFree(p);
     if (stream_) hipStreamDestroy(stream_);
@@ -563,6 +564,31 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     last_prefill_ms = ms1;
     last_frames_ms = ms2;
     hipEventDestroy(e0); hipEventDestroy(e1); hipEventDestroy(e2);
+    return true;
+}
+
+bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
+    if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
+    std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
+    Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    hipGraphExec_t g = nullptr;
+    if (stage == 0) { if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false; g = g_talker_[S]; }
+    else { if (!graph_for(g_cp_, S, &Engine::enqueue_cp_only)) return false; g = g_cp_[S]; }
+    Q3T_HIP(hipGraphLaunch(g, stream_));   // warm
+    hipEvent_t a, b;
+    Q3T_HIP(hipEventCreate(&a));
+    Q3T_HIP(hipEventCreate(&b));
+    Q3T_HIP(hipEventRecord(a, stream_));
+    for (int i = 0; i < iters; ++i) Q3T_HIP(hipGraphLaunch(g, stream_));
+    Q3T_HIP(hipEventRecord(b, stream_));
+    Q3T_HIP(hipEventSynchronize(b));
+    float t = 0;
+    hipEventElapsedTime(&t, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    *ms = t / iters;
     return true;
 }
 

@@ -65,6 +65,10 @@ public:
     bool prefill_embd(const int32_t *toks, int n, const float *spk, int language_id, float *prefill, int *prefill_len,
                       float *trailing, int *trailing_len, float *tts_pad);
 
+    // replay the captured talker-step (or code-predictor frame) graph `iters` times at position `pos` for S slots and
+    // report the mean device time per replay (HIP events on the context stream)
+    bool time_stage(int stage, int S, int pos, int iters, double *ms);
+
     // profiling hooks for bench.py: last generate() timings
     double last_prefill_ms = 0, last_frames_ms = 0;
 
@@ -114,7 +118,8 @@ private:
     int recipe_cap_ = 0;
     GenParams gp_;   // parameters baked into the captured frame graph
 
-    std::map<int, hipGraphExec_t> g_talker_, g_frame_;
+    bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
+    std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;
     std::unique_ptr<Vocoder> voc_;
 };
 

@@ -55,6 +55,7 @@ def lib():
         L.q3o_prefill_embd.argtypes = [P, ip, I, P, I, fp, C.POINTER(I), fp, C.POINTER(I), fp]
         L.q3o_cp_pass.argtypes = [P, P, fp, I, I, P, P]
         L.q3o_cp_frame.argtypes = [P, fp, I, F, I, P, ip, P]
+        L.q3o_cp_frame_forced.argtypes = [P, fp, I, ip, fp]
         L.q3o_sample.argtypes = [fp, I, F, I, F, I]
         L.q3o_cb0_select.argtypes = [P, fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), I, I, F, F, I, F, I]
         L.q3o_uniform.restype = F
@@ -143,6 +144,12 @@ class Oracle:
         lib().q3o_cp_frame(self.h, np.ascontiguousarray(hidden, np.float32), int(cb0), float(temperature),
                            int(top_k), _ptr(u), codes, _ptr(lg))
         return (codes, lg) if want_logits else codes
+
+    def cp_frame_forced(self, hidden, cb0, codes15):
+        lg = np.zeros((15, self.cfg["cp_vocab"]), np.float32)
+        lib().q3o_cp_frame_forced(self.h, np.ascontiguousarray(hidden, np.float32), int(cb0),
+                                  np.ascontiguousarray(codes15, np.int32), lg)
+        return lg
 
     def cp_pass(self, kv, x, pos, head=-1):
         H = self.cfg["hidden"]

@@ -58,6 +58,23 @@ def _sample_interval(logits, temperature, top_k, keep_id):
     return e, e.sum()
 
 
+def check_token(lg, tok, temperature, top_k, u, keep_id=-1, tol_logit=5e-2, tol_cdf=5e-2):
+    """one decision: 0 if tok is exactly what the oracle logits select, 1 if within tolerance (else AssertionError)."""
+    if temperature <= 0:
+        gap = float(lg.max() - lg[tok])
+        assert gap <= tol_logit, gap
+        return int(gap > 0)
+    e, tot = _sample_interval(lg, temperature, top_k, keep_id)
+    cum = np.cumsum(e)
+    lo = cum[tok - 1] if tok > 0 else 0.0
+    target = u * tot
+    if lo <= target <= cum[tok]:
+        return 0
+    err = max(lo - target, target - cum[tok]) / tot
+    assert err <= tol_cdf, err
+    return 1
+
+
 def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperature=0.0, top_k=50, seed=0, utt=0,
                     rep=1.05, tol_logit=5e-2, tol_cdf=5e-2, max_off_frac=0.03, eos_id=2150):
     """Teacher-forced parity of a GPU-generated code sequence against the oracle.

@@ -1,9 +1,13 @@
 """GPU parity: the HIP path (libq3t.so through the C ABI) against the CPU oracle on identical inputs.
 
 Tolerances: both sides use the reference CPU numerics (f16 weights, f16-rounded matmul inputs, F16 KV, f32
-accumulation); they differ only in f32 summation order, which can move an f16 rounding by one ulp (4.9e-4
-relative) inside the stack.  Hidden states / logits are therefore compared at max-abs error relative to
-the tensor's max |value| <= 3e-3 (tiny) / 5e-3 (full 28-layer talker); token ids must match exactly.
+accumulation) and differ only in f32 summation order.  With f16-rounded activations that difference flips
+individual roundings (4.9e-4 relative) and the random-weight stack amplifies them: the ORACLE ITSELF moves by
+~1e-3 (hidden) / ~1e-2 (logits) when its input is perturbed by 1e-7 (tests/test_oracle_sensitivity.py), while
+in fp32 mode the same perturbation stays at 1e-6.  Hidden/logit comparisons therefore use max-abs error
+relative to max|value| <= 3e-3 (tiny) / 5e-3 (full), logits <= 5e-2 / 8e-2 absolute; token decisions are
+checked teacher-forced: the GPU token must be the oracle's choice or within that tolerance of it (near-tie),
+and only a few percent of decisions may take the tolerance branch.
 """
 import os
 import sys
@@ -12,13 +16,14 @@ import numpy as np
 import pytest
 
 from oracle_py import Oracle, uniform
-from q3t_testutil import REPO, check_decisions, prompt, rel_err, synth_dir
+from q3t_testutil import REPO, check_decisions, check_token, prompt, rel_err, synth_dir
 
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(REPO, "tests", "golden")
 TOL = {"tiny": 3e-3, "full": 5e-3}
+LOGIT_TOL = {"tiny": 5e-2, "full": 8e-2}   # >= 2x the oracle's own sensitivity (test_oracle_sensitivity)
 
 
 @pytest.fixture(scope="module", params=["tiny", "full"])
@@ -61,16 +66,19 @@ def test_talker_step_vs_reference_harness_fp32(pair):
 
 
 def test_codepred_greedy_matches_oracle(pair):
+    """teacher-forced: each GPU code is the oracle argmax given the GPU's previous codes (near-tie tolerance)."""
     cfg, eng, orc = pair
     H = eng.cfg["hidden"]
     rng = np.random.default_rng(5)
     hid = rng.standard_normal((3, H)).astype(np.float32)
     cb0 = np.array([137, 5, 2047], np.int32)
     codes, lg = eng.codepred_frame(hid, cb0, temperature=0.0, want_logits=True)
+    off = 0
     for s in range(3):
-        oc, ol = orc.cp_frame(hid[s], int(cb0[s]), temperature=0.0, want_logits=True)
-        np.testing.assert_array_equal(codes[s], oc)
-        assert rel_err(lg[s], ol) < TOL[cfg]
+        ol = orc.cp_frame_forced(hid[s], int(cb0[s]), codes[s])
+        assert np.abs(lg[s] - ol).max() < LOGIT_TOL[cfg]
+        off += sum(check_token(ol[i], int(codes[s, i]), 0.0, 0, 0.0) for i in range(15))
+    assert off <= 2, off
 
 
 def test_codepred_vs_reference_harness(pair):
@@ -86,12 +94,14 @@ def test_codepred_sampling_matches_oracle(pair):
     H = eng.cfg["hidden"]
     rng = np.random.default_rng(9)
     hid = rng.standard_normal((2, H)).astype(np.float32)
+    off = 0
     for seed, frame in [(11, 0), (12, 7)]:
         codes = eng.codepred_frame(hid, [100, 200], temperature=0.9, top_k=50, seed=seed, frame=frame)
         for s in range(2):
-            u15 = np.array([uniform(seed, s, frame, c + 1) for c in range(15)], np.float32)
-            oc = orc.cp_frame(hid[s], [100, 200][s], temperature=0.9, top_k=50, u15=u15)
-            np.testing.assert_array_equal(codes[s], oc)
+            ol = orc.cp_frame_forced(hid[s], [100, 200][s], codes[s])
+            for i in range(15):
+                off += check_token(ol[i], int(codes[s, i]), 0.9, 50, uniform(seed, s, frame, i + 1))
+    assert off <= 3, off
 
 
 def test_cb0_select_matches_oracle(pair):
