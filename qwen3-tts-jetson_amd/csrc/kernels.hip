@@ -204,10 +204,14 @@ bool gemv(const GemvParams &p, hipStream_t s) {
         set_error("gemv: unsupported shape N=" + std::to_string(p.N) + " K=" + std::to_string(p.K));
         return false;
     }
-    if ((p.K + 127) / 128 * 128 * 2 * 8 > 150 * 1024) { set_error("gemv: K too large for the LDS tile"); return false; }
-    if (p.B == 1) launch_gemv_bt<1>(p, s);
-    else if (p.B == 2) launch_gemv_bt<2>(p, s);
-    else if (p.B <= 4) launch_gemv_bt<4>(p, s);
+    if ((p.K + 127) / 128 * 128 * 2 > 48 * 1024) { set_error("gemv: K too large for the LDS tile"); return false; }
+    // batch tile: up to 8 activation rows in LDS as f16, capped at 48 KB of LDS
+    int bt = p.B == 1 ? 1 : p.B == 2 ? 2 : p.B <= 4 ? 4 : 8;
+    const int Kp = (p.K + 127) / 128 * 128;
+    while (bt > 1 && (size_t)Kp * 2 * bt > 48 * 1024) bt /= 2;
+    if (bt == 1) launch_gemv_bt<1>(p, s);
+    else if (bt == 2) launch_gemv_bt<2>(p, s);
+    else if (bt == 4) launch_gemv_bt<4>(p, s);
     else launch_gemv_bt<8>(p, s);
     Q3T_HIP(hipGetLastError());
     return true;

@@ -16,13 +16,52 @@ public:
     // mode 0 = FULL (GGML decoder semantics), 1 = CHUNK40 (TRT streaming semantics)
     int64_t n_samples(int n_frames, int mode) const;
     bool decode(const int32_t *codes_host, int n_frames, int mode, float *pcm_host, int64_t *n_out);
+    // FULL decode of device-resident codes [F][16] into pcm_dev (capacity >= n_samples(F, 0)); ensure(F) first
     bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s);
+    bool ensure(int n_frames);
     bool loaded() const { return loaded_; }
 
 private:
+    struct Conv { uint16_t *w = nullptr; float *b = nullptr; int k = 0, ic = 0, oc = 0; };   // w: [k][oc][ic]
+    struct Snake { float *a = nullptr, *ib = nullptr; int n = 0; };                          // exp(alpha), exp(-beta)
+    struct Layer {
+        uint16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+        float *attn_norm = nullptr, *ffn_norm = nullptr, *attn_scale = nullptr, *ffn_scale = nullptr;
+    };
+    struct Up {
+        Conv ct;
+        uint16_t *dw = nullptr, *pw1 = nullptr, *pw2 = nullptr;
+        float *dw_b = nullptr, *norm_w = nullptr, *norm_b = nullptr, *gamma = nullptr, *pw1_b = nullptr, *pw2_b = nullptr;
+        int dw_k = 7, pw_dim = 0;
+    };
+    struct Res { Snake a1, a2; Conv c1, c2; int dil = 1; };
+    struct Dec { Snake snake; Conv ct; Res res[3]; int rate = 1; };
+
+    template <class T> T *dalloc(size_t n);
+    int64_t full_len(int F) const;
+    bool run_conv(const Conv &c, const float *x, int T, int pad, int dil, const Snake *sn, float *y, const float *resid,
+                  int act, hipStream_t s);
+    bool run_convT(const Conv &c, const float *x, int T, int stride, int trim, const Snake *sn, float *y, int T_out,
+                   hipStream_t s);
+
     bool loaded_ = false;
     hipStream_t stream_ = nullptr;
-    std::vector<void *> allocs_;
+    std::vector<void *> allocs_, scratch_;
+    int cb_dim_ = 0, cb_size_ = 0, hidden_ = 0, latent_ = 0, n_heads_ = 16, head_dim_ = 64, ffn_ = 0;
+    uint16_t *cb_first_ = nullptr, *cb_rest_[15] = {}, *vq_first_out_ = nullptr, *vq_rest_out_ = nullptr;
+    uint16_t *in_proj_ = nullptr, *out_proj_ = nullptr;
+    float *in_proj_b_ = nullptr, *out_proj_b_ = nullptr, *pre_norm_ = nullptr;
+    Conv pre_conv_, dec0_, dec6_;
+    std::vector<Layer> layers_;
+    Up up_[2];
+    Dec dec_[4];
+    Snake dec5_;
+    // scratch (grown by ensure)
+    int cap_frames_ = 0;
+    float *buf_[3] = {nullptr, nullptr, nullptr};
+    int32_t *codes_ = nullptr;
+    int *cols_ = nullptr;
+    float *pcm_ = nullptr, *rope_ = nullptr;
 };
 
 }  // namespace q3t

@@ -1,0 +1,28 @@
+// vocoder_kernels.h — launchers of the vocoder (tokenizer decoder) kernels.
+#pragma once
+#include "q3t_common.h"
+
+namespace q3t {
+
+constexpr int CONV_MAX_TAPS = 7;
+struct ConvTap { const uint16_t *w; int dj; };   // w: [C_out][C_in] f16 of one kernel tap; input row offset dj
+// y[m*so + ob][co] = act(bias[co] + resid + sum_j sum_ci w_j[co][ci] * f16(snake(x[m + dj][ci])))
+// x: [T_in][C_in] f32 (rows outside [0,T_in) read as 0 = causal zero padding); y: [T_out][C_out] f32
+struct ConvParams {
+    const float *x = nullptr;
+    int T_in = 0, C_in = 0;
+    const float *snake_a = nullptr, *snake_ib = nullptr;   // exp(alpha), exp(-beta) per input channel (nullable)
+    int n_taps = 0;
+    ConvTap taps[CONV_MAX_TAPS];
+    int dmin = 0, dmax = 0;
+    float *y = nullptr;
+    int C_out = 0, M = 0, so = 1, ob = 0;
+    const float *bias = nullptr, *resid = nullptr;
+    int act = 0;   // 1 = tanh
+};
+bool conv(const ConvParams &p, hipStream_t s);
+bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s);
+bool attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s);
+bool codes_cols(const int32_t *codes, int *cols, int F, int ncb, hipStream_t s);
+
+}  // namespace q3t

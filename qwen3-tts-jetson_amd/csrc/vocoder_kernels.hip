@@ -1,1 +1,235 @@
-#include "kernels.h"
+// vocoder_kernels.hip — gfx950 kernels of the Qwen3-TTS tokenizer decoder (src/audio_tokenizer_decoder.cpp:375-802).
+// Activations are time-major [T][C] f32; every conv input is rounded to f16 (ggml im2col F16) and fed to
+// v_mfma_f32_32x32x16_f16 with f16 weights (exact products, f32 accumulation).
+#include "vocoder_kernels.h"
+
+namespace q3t {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+// ======================================================================================= implicit-GEMM conv
+// y[m*so + ob][co] = act( bias[co] + resid + sum_j sum_ci W_j[co][ci] * f16( snake(x[m + dj][ci]) ) )
+// Tile 64 (m) x 64 (co); 4 waves as 2 x 2 of 32 x 32; K-chunk = 32 input channels.
+constexpr int CT_M = 64, CT_N = 64, CT_K = 32, CT_LD = CT_K + 8;   // LDS row: 32 f16 + 16 B pad
+constexpr int CT_MAXWIN = CT_M + 64;
+
+__global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
+    __shared__ __attribute__((aligned(16))) uint16_t xs[CT_MAXWIN * CT_LD];
+    __shared__ __attribute__((aligned(16))) uint16_t ws[CONV_MAX_TAPS * CT_N * CT_LD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = blockIdx.x * CT_M, co0 = blockIdx.y * CT_N;
+    const int win = CT_M + p.dmax - p.dmin;
+    f32x16_t acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    const int r = lane & 31, h = lane >> 5;
+    for (int c0 = 0; c0 < p.C_in; c0 += CT_K) {
+        // ---- stage the input window (snake + f16 rounding fused), 4 channels per thread-step
+        for (int e = tid; e < win * (CT_K / 4); e += 256) {
+            const int row = e / (CT_K / 4), cq = (e % (CT_K / 4)) * 4;
+            const int i = m0 + p.dmin + row;
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            if (i >= 0 && i < p.T_in) {
+                const int ci = c0 + cq;
+                if (ci + 3 < p.C_in && (p.C_in & 3) == 0) {
+                    const float4 u = *reinterpret_cast<const float4 *>(p.x + (size_t)i * p.C_in + ci);
+                    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+                } else {
+                    for (int q = 0; q < 4; ++q) if (ci + q < p.C_in) v[q] = p.x[(size_t)i * p.C_in + ci + q];
+                }
+                if (p.snake_a) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (ci + q < p.C_in) {
+                            const float sn = sinf(v[q] * p.snake_a[ci + q]);
+                            v[q] = v[q] + (sn * sn) * p.snake_ib[ci + q];
+                        }
+                    }
+                }
+            }
+            uint16_t *d = xs + row * CT_LD + cq;
+            d[0] = f2h(v[0]); d[1] = f2h(v[1]); d[2] = f2h(v[2]); d[3] = f2h(v[3]);
+        }
+        // ---- stage the weight tiles of every tap: [tap][co][32 ci]
+        for (int e = tid; e < p.n_taps * CT_N * (CT_K / 8); e += 256) {
+            const int j = e / (CT_N * (CT_K / 8)), rem = e % (CT_N * (CT_K / 8));
+            const int co = rem / (CT_K / 8), c8 = (rem % (CT_K / 8)) * 8;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            const int gco = co0 + co, gci = c0 + c8;
+            if (gco < p.C_out) {
+                const uint16_t *w = p.taps[j].w + (size_t)gco * p.C_in + gci;
+                if (gci + 7 < p.C_in && (p.C_in & 7) == 0) u = *reinterpret_cast<const uint4 *>(w);
+                else {
+                    uint16_t t8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (int q = 0; q < 8; ++q) if (gci + q < p.C_in) t8[q] = w[q];
+                    u = *reinterpret_cast<const uint4 *>(t8);
+                }
+            }
+            *reinterpret_cast<uint4 *>(ws + (j * CT_N + co) * CT_LD + c8) = u;
+        }
+        __syncthreads();
+        for (int j = 0; j < p.n_taps; ++j) {
+            const int arow = wm * 32 + r + (p.taps[j].dj - p.dmin);
+            const uint16_t *ab = xs + arow * CT_LD + 8 * h;
+            const uint16_t *bb = ws + (j * CT_N + wn * 32 + r) * CT_LD + 8 * h;
+#pragma unroll
+            for (int kk = 0; kk < CT_K; kk += 16) {
+                const half8_t a = *reinterpret_cast<const half8_t *>(ab + kk);
+                const half8_t b = *reinterpret_cast<const half8_t *>(bb + kk);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- epilogue (C/D map: col = lane & 31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5))
+    const int co = co0 + wn * 32 + (lane & 31);
+    if (co >= p.C_out) return;
+    const float b = p.bias ? p.bias[co] : 0.0f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+        const int m = m0 + wm * 32 + row;
+        if (m >= p.M) continue;
+        const size_t t = (size_t)m * p.so + p.ob;
+        float v = acc[reg] + b;
+        if (p.resid) v = p.resid[t * p.C_out + co] + v;
+        if (p.act == 1) v = tanhf(v);
+        p.y[t * p.C_out + co] = v;
+    }
+}
+
+bool conv(const ConvParams &p, hipStream_t s) {
+    if (p.M <= 0) return true;
+    if (p.n_taps < 1 || p.n_taps > CONV_MAX_TAPS || p.dmax - p.dmin > CT_MAXWIN - CT_M) {
+        set_error("conv: unsupported tap layout");
+        return false;
+    }
+    const dim3 grid((p.M + CT_M - 1) / CT_M, (p.C_out + CT_N - 1) / CT_N);
+    hipLaunchKernelGGL(k_conv, grid, dim3(256), 0, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+// ======================================================================================= depthwise causal conv
+// y[t][c] = b[c] + sum_j w[c][j] * f16(x[t + j - (K-1)][c])      (ggml_pad_ext + ggml_conv_1d_dw, im2col F16)
+__global__ void __launch_bounds__(256) k_dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)T * C) return;
+    const int t = (int)(idx / C), c = (int)(idx % C);
+    float acc = 0.0f;
+    for (int j = 0; j < K; ++j) {
+        const int i = t + j - (K - 1);
+        if (i >= 0) acc += h2f(w[(size_t)c * K + j]) * f16r(x[(size_t)i * C + c]);
+    }
+    y[idx] = acc + b[c];
+}
+bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s) {
+    const size_t n = (size_t)T * C;
+    if (!n) return true;
+    hipLaunchKernelGGL(k_dwconv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, w, b, y, T, C, K);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+// ======================================================================================= pre-transformer attention
+// causal softmax attention over F frames (apply_pre_tfm_layer, audio_tokenizer_decoder.cpp:412-456): NEOX RoPE
+// (theta 1e4) on q,k, f32 scores (ggml mul_mat of two F32 tensors: no rounding), output rounded to f16.
+// grid (query tiles of 16, heads); 16 lanes per query row, 4 keys / 4 dims per lane.
+__global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH) {
+    constexpr int D = 64, QT = 16, KT = 64;
+    __shared__ float qs[QT][D];
+    __shared__ float ks[KT][D + 1];
+    __shared__ float vs[KT][D + 1];
+    __shared__ float ps[QT][KT];
+    const int h = blockIdx.y, q0 = blockIdx.x * QT;
+    const int tid = threadIdx.x, qi = tid / 16, l16 = tid % 16;
+    const int LD = 3 * nH * D;
+    auto rope_load = [&](const float *src, int pos, int e) -> float {
+        // NEOX pair (e, e+32)
+        const int i = e & 31;
+        const float c = rope[(size_t)pos * D + 2 * i], sn = rope[(size_t)pos * D + 2 * i + 1];
+        const float x0 = src[i], x1 = src[i + 32];
+        return e < 32 ? x0 * c - x1 * sn : x0 * sn + x1 * c;
+    };
+    for (int e = tid; e < QT * D; e += 256) {
+        const int qq = e / D, d = e % D, pos = q0 + qq;
+        qs[qq][d] = pos < F ? rope_load(qkv + (size_t)pos * LD + h * D, pos, d) : 0.0f;
+    }
+    float m = -INFINITY, l = 0.0f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int qpos = q0 + qi;
+    const float scale = 1.0f / sqrtf((float)D);
+    const int kend = min(F, q0 + QT);
+    for (int k0 = 0; k0 < kend; k0 += KT) {
+        __syncthreads();
+        for (int e = tid; e < KT * D; e += 256) {
+            const int kk = e / D, d = e % D, pos = k0 + kk;
+            const float *row = qkv + (size_t)pos * LD;
+            ks[kk][d] = pos < F ? rope_load(row + nH * D + h * D, pos, d) : 0.0f;
+            vs[kk][d] = pos < F ? row[2 * nH * D + h * D + d] : 0.0f;
+        }
+        __syncthreads();
+        float s[4];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int kk = l16 * 4 + t, kpos = k0 + kk;
+            float d = 0.0f;
+#pragma unroll 16
+            for (int e = 0; e < D; ++e) d += ks[kk][e] * qs[qi][e];
+            s[t] = (kpos <= qpos && kpos < F) ? d * scale : -INFINITY;
+            mt = fmaxf(mt, s[t]);
+        }
+        mt = fmaxf(mt, __shfl_xor(mt, 8, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 4, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 2, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 1, 16));
+        const float mn = fmaxf(m, mt);
+        const float corr = (m == -INFINITY) ? 0.0f : expf(m - mn);
+        float ls = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float pv = (s[t] == -INFINITY) ? 0.0f : expf(s[t] - mn);
+            ps[qi][l16 * 4 + t] = pv;
+            ls += pv;
+        }
+        ls = group_sum<16>(ls);
+        l = l * corr + ls;
+        m = mn;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] *= corr;
+        __syncthreads();
+        for (int kk = 0; kk < KT; ++kk) {
+            const float pv = ps[qi][kk];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] += pv * vs[kk][l16 * 4 + t];
+        }
+    }
+    if (qpos < F) {
+        const float inv = 1.0f / l;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) out[(size_t)qpos * nH * D + h * D + l16 * 4 + t] = f2h(acc[t] * inv);
+    }
+}
+bool attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s) {
+    if (D != 64) { set_error("attn_prefill: head_dim must be 64"); return false; }
+    if (F <= 0) return true;
+    hipLaunchKernelGGL(k_attn_prefill, dim3((F + 15) / 16, nH), dim3(256), 0, s, qkv, rope, out, F, nH);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+// codes [F][ncb] -> per-codebook index columns [ncb][F]
+__global__ void k_codes_cols(const int32_t *codes, int *cols, int F, int ncb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < F * ncb) cols[(i % ncb) * F + i / ncb] = codes[i];
+}
+bool codes_cols(const int32_t *codes, int *cols, int F, int ncb, hipStream_t s) {
+    if (F <= 0) return true;
+    hipLaunchKernelGGL(k_codes_cols, dim3((F * ncb + 255) / 256), dim3(256), 0, s, codes, cols, F, ncb);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+}  // namespace q3t

@@ -1,0 +1,67 @@
+"""GPU parity of the vocoder (tokenizer decoder) against the CPU oracle: FULL (GGML decoder semantics,
+audio_tokenizer_decoder.cpp:622-802) and CHUNK40 (TRT streaming semantics, trt_vocoder.cpp:98-170).
+
+PCM tolerance: both sides round every conv/matmul input to f16 and differ only in f32 summation order
+(MFMA vs AVX2); measured max |dPCM| is printed and bounded by PCM_TOL below (PCM is in [-1, 1])."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from q3t_testutil import REPO, synth_dir
+
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+pytestmark = pytest.mark.gpu
+PCM_TOL = {"tiny": 2e-2, "full": 3e-2}
+
+
+@pytest.fixture(scope="module", params=["tiny", "full"])
+def pair(request):
+    import q3t
+    cfg = request.param
+    tts, tok = synth_dir(cfg)
+    eng = q3t.Engine(tts, tok, device=0, max_slots=1, max_ctx=64)
+    orc = Oracle(tts, tok)
+    yield cfg, eng, orc
+    eng.close()
+    orc.close()
+
+
+def _codes(F, seed):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 2048, size=(F, 16), dtype=np.int32)
+
+
+@pytest.mark.parametrize("F", [1, 7, 40])
+def test_vocoder_full_matches_oracle(pair, F):
+    cfg, eng, orc = pair
+    codes = _codes(F, F)
+    g = eng.vocoder(codes, 0)
+    o = orc.vocoder(codes, 0)
+    assert g.shape == o.shape == (eng.vocoder_num_samples(F, 0),)
+    err = float(np.abs(g - o).max())
+    rms = float(np.sqrt(np.mean((g - o) ** 2)))
+    print(f"{cfg} F={F} full: max|d|={err:.3e} rms={rms:.3e} pcm_std={o.std():.3f}")
+    assert err < PCM_TOL[cfg] and rms < PCM_TOL[cfg] / 10
+
+
+def test_vocoder_chunk40_matches_oracle(pair):
+    cfg, eng, orc = pair
+    F = 47   # one full chunk + a ragged 7-frame chunk
+    codes = _codes(F, 3)
+    g = eng.vocoder(codes, 1)
+    o = orc.vocoder(codes, 1)
+    assert g.shape == o.shape == (F * 1920,)
+    err = float(np.abs(g - o).max())
+    print(f"{cfg} chunk40: max|d|={err:.3e}")
+    assert err < PCM_TOL[cfg]
+
+
+def test_vocoder_lengths(pair):
+    cfg, eng, orc = pair
+    for F in (1, 2, 40, 513):
+        assert eng.vocoder_num_samples(F, 0) == orc.vocoder_len(F, 0)
+        assert eng.vocoder_num_samples(F, 1) == F * 1920
+    assert eng.vocoder(np.zeros((0, 16), np.int32), 0).shape == (0,)
