@@ -14,7 +14,7 @@ from q3t_testutil import REPO, synth_dir
 
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
-PCM_TOL = {"tiny": 2e-2, "full": 3e-2}
+PCM_TOL = {"tiny": 1e-2, "full": 1e-2}   # measured max |dPCM| 3.7e-3 / 3.6e-3, rms <= 7e-4
 
 
 @pytest.fixture(scope="module", params=["tiny", "full"])
@@ -44,7 +44,7 @@ def test_vocoder_full_matches_oracle(pair, F):
     err = float(np.abs(g - o).max())
     rms = float(np.sqrt(np.mean((g - o) ** 2)))
     print(f"{cfg} F={F} full: max|d|={err:.3e} rms={rms:.3e} pcm_std={o.std():.3f}")
-    assert err < PCM_TOL[cfg] and rms < PCM_TOL[cfg] / 10
+    assert err < PCM_TOL[cfg] and rms < 2e-3
 
 
 def test_vocoder_chunk40_matches_oracle(pair):
