@@ -1,0 +1,293 @@
+// attn.hip — decode attention of the talker (and of the code predictor when its fused O-projection prologue is not
+// used): one new token per slot, Qwen3 block semantics of src/tts_transformer.cpp:1410-1475 (head RMSNorm over the
+// 128 lanes, NEOX RoPE at pos, F16 KV append, flash_attn_ext with scale 1/sqrt(D), GQA head h -> kv head h/R).
+//
+// MI355X layout: grid (slot, kv head, split), one 256-thread workgroup per ATTN_CHUNK = 64 positions.  Every lane
+// issues its K and V loads (NP x 16 B each) before anything else, so a chunk is ONE memory round trip; D/8 lanes
+// per position, dot products reduced with xor butterflies.  Split partials (m, l, acc) are published with
+// agent-scope (sc1) stores and an arrival ticket; the workgroup whose ticket add comes last combines them in the
+// same launch (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores -> vmcnt(0) -> barrier -> one agent atomic
+// add; the last adder loads the partials with sc1 loads) -- no combine launch, no release/acquire cache flushes.
+#include "kernels.h"
+
+namespace q3t {
+
+template <class V>
+__device__ __forceinline__ V ldg_a(const void *p) {
+    typedef const __attribute__((address_space(1))) V gV;
+    return *(gV *)(p);
+}
+typedef unsigned int u32x4_a __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ldg16(const uint16_t *p) {
+    const u32x4_a v = ldg_a<u32x4_a>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_sc1(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[2 * e] = h2f(w[e] & 0xffff); f[2 * e + 1] = h2f(w[e] >> 16); }
+}
+
+template <int D, int RMAX>
+__global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
+    constexpr int LPP = D / 8;               // lanes per position
+    constexpr int PPP = 256 / LPP;           // positions per pass
+    constexpr int NP = ATTN_CHUNK / PPP;     // passes per chunk
+    constexpr int E = D / 64;                // elements per lane in the one-wave-per-vector prologue
+    const int slot = blockIdx.x, g = blockIdx.y, split = blockIdx.z;
+    constexpr int R = RMAX;   // q heads per kv head
+    const int pos = p.pos[slot];
+    const int j0 = split * ATTN_CHUNK;
+    if (j0 > pos) return;
+    const int nsplit = pos / ATTN_CHUNK + 1;
+    const bool has_pos = split == nsplit - 1;   // this chunk contains the new token
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
+
+    __shared__ float q_s[RMAX][D];
+    __shared__ float kn_s[D], vn_s[D];
+    __shared__ float wred[4][RMAX];
+    __shared__ float ared[4][RMAX][D];
+    __shared__ float cm[RMAX], cl[RMAX];
+    __shared__ float sm[ATTN_MAX_SPLITS][RMAX], sl[ATTN_MAX_SPLITS][RMAX], sw[ATTN_MAX_SPLITS][RMAX];
+    __shared__ unsigned last_s;
+
+    // ---- (1) this chunk's K/V rows: every load issued up front (clamped rows are masked later)
+    const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
+    uint4 kr[NP], vr[NP];
+#pragma unroll
+    for (int pi = 0; pi < NP; ++pi) {
+        const int j = min(j0 + pi * PPP + pg, p.n_ctx - 1);
+        kr[pi] = ldg16(p.kc + head_off + (size_t)j * D + li * 8);
+        vr[pi] = ldg16(p.vc + head_off + (size_t)j * D + li * 8);
+    }
+
+    // ---- (2) head RMSNorm (double sum, ggml_rms_norm) + NEOX RoPE of the R q heads and the new k; f16-rounded
+    const int QKV = (p.nH + 2 * p.nKV) * D;
+    const float *qkv = p.qkv + (size_t)slot * QKV;
+    const float *rope = p.rope + (size_t)pos * D;
+    const int nvec = R + (has_pos ? 2 : 0);
+    for (int v = wave; v < nvec; v += 4) {
+        if (v == R + 1) {   // the new v row: f16-rounded, no norm
+#pragma unroll
+            for (int e = 0; e < E; ++e) vn_s[lane + 64 * e] = f16r(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
+            continue;
+        }
+        const bool isk = v == R;
+        const float *src = isk ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
+        const float *w = isk ? p.kn : p.qn;
+        float x[E];
+        double ss = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { x[e] = src[lane + 64 * e]; ss += (double)(x[e] * x[e]); }
+        ss = wave_sum_d(ss);
+        const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+        float y[E];
+        if constexpr (D == 128) {
+            const float c = rope[2 * lane], s = rope[2 * lane + 1];
+            y[0] = x[0] * c - x[1] * s;
+            y[1] = x[0] * s + x[1] * c;
+        } else {
+            const int i = lane & 31;
+            const float c = rope[2 * i], s = rope[2 * i + 1];
+            const float other = __shfl_xor(x[0], 32, 64);
+            y[0] = lane < 32 ? x[0] * c - other * s : other * s + x[0] * c;
+        }
+        float *dst = isk ? kn_s : q_s[v];
+#pragma unroll
+        for (int e = 0; e < E; ++e) dst[lane + 64 * e] = f16r(y[e]);
+    }
+    __syncthreads();
+    if (has_pos)   // KV append at pos (the only block that touches position pos)
+        for (int e = t; e < D; e += 256) {
+            p.kc[head_off + (size_t)pos * D + e] = f2h(kn_s[e]);
+            p.vc[head_off + (size_t)pos * D + e] = f2h(vn_s[e]);
+        }
+
+    // ---- (3) scores of this lane's NP positions for the R heads
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    float q8[RMAX][8];
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q8[h][e] = h < R ? q_s[h][li * 8 + e] : 0.0f;
+    float sc[NP][RMAX];
+    bool ok[NP];
+#pragma unroll
+    for (int pi = 0; pi < NP; ++pi) {
+        const int j = j0 + pi * PPP + pg;
+        ok[pi] = j <= pos;
+        float k8[8];
+        if (j == pos) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) k8[e] = kn_s[li * 8 + e];
+        } else {
+            unpack8(kr[pi], k8);
+        }
+#pragma unroll
+        for (int h = 0; h < RMAX; ++h) {
+            float s = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += k8[e] * q8[h][e];
+            s = group_sum<LPP>(s);
+            sc[pi][h] = ok[pi] ? s * kq_scale : -INFINITY;
+        }
+    }
+    // ---- (4) chunk max / exp / sum per head (xor over the position bits of the wave, then LDS over waves)
+    float M[RMAX], L[RMAX];
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h) {
+        float m = sc[0][h];
+#pragma unroll
+        for (int pi = 1; pi < NP; ++pi) m = fmaxf(m, sc[pi][h]);
+#pragma unroll
+        for (int o = LPP; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (lane == 0) wred[wave][h] = m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h) M[h] = fmaxf(fmaxf(wred[0][h], wred[1][h]), fmaxf(wred[2][h], wred[3][h]));
+    __syncthreads();
+    float pr[NP][RMAX];
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h) {
+        float l = 0.0f;
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            pr[pi][h] = ok[pi] ? expf(sc[pi][h] - M[h]) : 0.0f;
+            l += pr[pi][h];
+        }
+#pragma unroll
+        for (int o = LPP; o < 64; o <<= 1) l += __shfl_xor(l, o, 64);
+        if (lane == 0) wred[wave][h] = l;
+    }
+    // ---- (5) P.V over this lane's positions, reduced over the position groups
+    float acc[RMAX][8];
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
+#pragma unroll
+    for (int pi = 0; pi < NP; ++pi) {
+        const int j = j0 + pi * PPP + pg;
+        float v8[8];
+        if (j == pos) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v8[e] = vn_s[li * 8 + e];
+        } else {
+            unpack8(vr[pi], v8);
+        }
+#pragma unroll
+        for (int h = 0; h < RMAX; ++h)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[h][e] += pr[pi][h] * (ok[pi] ? v8[e] : 0.0f);
+    }
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float a = acc[h][e];
+#pragma unroll
+            for (int o = LPP; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+            if (lane < LPP && h < R) ared[wave][h][li * 8 + e] = a;
+        }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h) L[h] = (wred[0][h] + wred[1][h]) + (wred[2][h] + wred[3][h]);
+
+    const int RD = R * D;
+    if (nsplit == 1) {
+        for (int o = t; o < RD; o += 256) {
+            const int h = o / D, d = o % D;
+            const float a = (ared[0][h][d] + ared[1][h][d]) + (ared[2][h][d] + ared[3][h][d]);
+            p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(a / L[h]);
+        }
+        return;
+    }
+    // ---- (6) publish the partial with sc1 stores, take a ticket; the last arrival combines
+    float *part = p.part + (((size_t)slot * p.nKV + g) * p.max_splits) * R * (D + 2);
+    for (int o = t; o < RD; o += 256) {
+        const int h = o / D, d = o % D;
+        const float a = (ared[0][h][d] + ared[1][h][d]) + (ared[2][h][d] + ared[3][h][d]);
+        st_sc1(part + ((size_t)split * R + h) * (D + 2) + d, a);
+    }
+    if (t < R) {
+        st_sc1(part + ((size_t)split * R + t) * (D + 2) + D, M[t]);
+        st_sc1(part + ((size_t)split * R + t) * (D + 2) + D + 1, L[t]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned *ticket = p.ticket + (size_t)slot * p.nKV + g;
+    if (t == 0) last_s = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nsplit - 1);
+    __syncthreads();
+    if (!last_s) return;
+    // combine (the last arrival): every partial load is issued in parallel (sc1 loads, L2-served)
+    for (int i = t; i < nsplit * R; i += 256) {
+        const int s = i / R, h = i % R;
+        sm[s][h] = ld_sc1(part + ((size_t)s * R + h) * (D + 2) + D);
+        sl[s][h] = ld_sc1(part + ((size_t)s * R + h) * (D + 2) + D + 1);
+    }
+    __syncthreads();
+    if (t < R) {
+        float mx = -INFINITY;
+        for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, sm[s][t]);
+        float lt = 0.0f;
+        for (int s = 0; s < nsplit; ++s) lt += sl[s][t] * expf(sm[s][t] - mx);
+        cm[t] = mx;
+        cl[t] = lt;
+    }
+    __syncthreads();
+    for (int i = t; i < nsplit * R; i += 256) {
+        const int s = i / R, h = i % R;
+        sw[s][h] = expf(sm[s][h] - cm[h]);
+    }
+    __syncthreads();
+    for (int o = t; o < RD; o += 256) {
+        const int h = o / D, d = o % D;
+        float a = 0.0f;
+        for (int s0 = 0; s0 < nsplit; s0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = s0 + u < nsplit ? ld_sc1(part + ((size_t)(s0 + u) * R + h) * (D + 2) + d) : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (s0 + u < nsplit) a += v[u] * sw[s0 + u][h];
+        }
+        p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(a / cl[h]);
+    }
+    if (t == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+bool attn_decode(const AttnParams &p, hipStream_t s) {
+    if (p.nH % p.nKV != 0 || p.nH / p.nKV > 4 || (p.D != 64 && p.D != 128)) {
+        set_error("attn_decode: unsupported head layout");
+        return false;
+    }
+    if (p.max_splits * ATTN_CHUNK < p.n_ctx || p.max_splits > ATTN_MAX_SPLITS || !p.part || !p.ticket) {
+        set_error("attn_decode: split buffers too small");
+        return false;
+    }
+    const dim3 grid(p.S, p.nKV, p.max_splits);
+    const int R = p.nH / p.nKV;
+#define Q3T_ATTN_LAUNCH(DD, RR) hipLaunchKernelGGL((k_attn<DD, RR>), grid, dim3(256), 0, s, p)
+    if (p.D == 128) {
+        if (R == 1) Q3T_ATTN_LAUNCH(128, 1);
+        else if (R == 2) Q3T_ATTN_LAUNCH(128, 2);
+        else if (R == 4) Q3T_ATTN_LAUNCH(128, 4);
+        else { set_error("attn_decode: q/kv head ratio must be 1, 2 or 4"); return false; }
+    } else {
+        if (R == 1) Q3T_ATTN_LAUNCH(64, 1);
+        else if (R == 2) Q3T_ATTN_LAUNCH(64, 2);
+        else if (R == 4) Q3T_ATTN_LAUNCH(64, 4);
+        else { set_error("attn_decode: q/kv head ratio must be 1, 2 or 4"); return false; }
+    }
+#undef Q3T_ATTN_LAUNCH
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+}  // namespace q3t

@@ -2,6 +2,7 @@
 #include "engine.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "vocoder.h"
@@ -41,10 +42,17 @@ bool check_shape(const GgufTensor *t, const char *name, int64_t cols, int64_t ro
 }
 }  // namespace
 
+static bool env_flag(const char *name, bool dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) != 0 : dflt;
+}
+
 bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx) {
     device_ = device;
+    cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
+    if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
     Q3T_HIP(hipSetDevice(device));
     Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     Gguf g;
@@ -80,6 +88,8 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
         return false;
     }
     if (c_.n_codebooks != 16) { set_error("n_codebooks must be 16"); return false; }
+    // the fused code-predictor attention prologue is specialised to the 0.6B head layout (16 q / 8 kv heads x 128)
+    cp_fused_attn_ = cp_fused_attn_ && c_.n_heads == 16 && c_.n_kv == 8 && c_.head_dim == 128;
     if (!upload_weights(g)) return false;
     if (!alloc_state()) return false;
     if (!tok_gguf.empty()) {
@@ -162,8 +172,12 @@ bool Engine::upload_weights(const Gguf &g) {
         snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
         if (!(cp_head_[i] = up16(b, H, c_.cp_vocab))) return false;
     }
-    cp_embd_dev_ = dalloc<uint16_t *>(15);
-    Q3T_HIP(hipMemcpy(cp_embd_dev_, cp_embd_.data(), 15 * sizeof(uint16_t *), hipMemcpyHostToDevice));
+    // the 16 tables of the step embedding: codec_embd (code 0) + code_pred.codec_embd[0..14] (codes 1..15)
+    std::vector<uint16_t *> tabs16(16);
+    tabs16[0] = codec_embd_;
+    for (int i = 0; i < 15; ++i) tabs16[1 + i] = cp_embd_[i];
+    tabs16_dev_ = dalloc<uint16_t *>(16);
+    Q3T_HIP(hipMemcpy(tabs16_dev_, tabs16.data(), 16 * sizeof(uint16_t *), hipMemcpyHostToDevice));
     // RoPE cos/sin table with ggml_rope_cache_init's f32 recurrence (theta *= theta_scale), NEOX pairs
     rope_len_ = std::max(max_ctx_, 16);
     std::vector<float> rope((size_t)rope_len_ * D);
@@ -194,6 +208,7 @@ bool Engine::alloc_state() {
     cp_in1_ = dalloc<float>((size_t)S * H);
     cp_logits_ = dalloc<float>((size_t)S * c_.cp_vocab);
     part_ = dalloc<float>((size_t)S * c_.n_heads * max_splits * (D + 2));
+    ticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
     attn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
     hmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
     const size_t kv_layer = (size_t)S * c_.n_kv * max_ctx_ * D;
@@ -237,26 +252,44 @@ bool Engine::alloc_state() {
 // ------------------------------------------------------------------------------------------ one decoder stack
 // 5 launches per layer: [RMSNorm+QKV GEMV] [head-norm+RoPE+KV-append+attention] [O GEMV + residual]
 // [RMSNorm+gate/up GEMV+SwiGLU] [down GEMV + residual]   (tts_transformer.cpp:1410-1494)
+// `in0` (optional) replaces layer 0's activation source: a gather prologue or another f32 buffer, with the raw
+// rows written to x (the residual stream) by the QKV kernel itself.
+struct StackInput {
+    int pro = PRO_RMS;
+    const float *x = nullptr;
+    GatherSum gs;
+};
 static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, float *qkv,
                           uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc, size_t kv_layer, int n_ctx,
-                          int max_splits, const int *pos, const float *rope, float *part, hipStream_t s) {
+                          int max_splits, const int *pos, const float *rope, float *part, unsigned *ticket,
+                          hipStream_t s, const StackInput *in0 = nullptr, bool fused_cp_attn = false) {
     const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
     for (size_t il = 0; il < layers.size(); ++il) {
         const DevLayer &l = layers[il];
         GemvParams g;
         g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
         g.pro = PRO_RMS; g.x = x; g.ldx = H; g.nw = l.attn_norm; g.eps = c.eps;
+        if (il == 0 && in0) {
+            g.pro = in0->pro; g.x = in0->x; g.gs = in0->gs; g.raw_out = x;
+        }
         g.out_f32 = qkv; g.ldo = QKV;
         if (!gemv(g, s)) return false;
-        AttnParams a;
-        a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
-        a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
-        a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
-        a.max_splits = max_splits; a.part = part; a.out = attn;
-        if (!attn_decode(a, s)) return false;
         GemvParams o;
         o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
-        o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
+        if (fused_cp_attn) {
+            // code predictor: attention recomputed inside the O-projection prologue (<= 16 positions)
+            o.pro = PRO_CPATT;
+            o.att.qkv = qkv; o.att.ld = QKV; o.att.qn = l.qn; o.att.kn = l.kn; o.att.eps = c.eps;
+            o.att.rope = rope; o.att.pos = pos; o.att.kc = kc + il * kv_layer; o.att.vc = vc + il * kv_layer;
+        } else {
+            AttnParams a;
+            a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
+            a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
+            a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
+            a.max_splits = max_splits; a.part = part; a.ticket = ticket; a.out = attn;
+            if (!attn_decode(a, s)) return false;
+            o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
+        }
         o.resid = x; o.ldr = H; o.out_f32 = x; o.ldo = H;
         if (!gemv(o, s)) return false;
         GemvParams gu;
@@ -273,11 +306,23 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
     return true;
 }
 
-bool Engine::enqueue_talker_step(int S, hipStream_t s) {
+bool Engine::enqueue_talker_step(int S, hipStream_t s) { return enqueue_talker(S, s, false); }
+
+// gather_input: the step embedding (tts_transformer.cpp:2529-2553) is assembled by layer 0's QKV prologue from the
+// frame's 16 codes (PRO_RMS_G16) instead of being read from x_
+bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
-    if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_, s))
+    StackInput in0;
+    if (gather_input) {
+        in0.pro = PRO_RMS_G16;
+        in0.gs.tok = tokens_; in0.gs.tok_ld = 16; in0.gs.tabs = tabs16_dev_;
+        in0.gs.tr = trailing_; in0.gs.tr_len = trailing_len_; in0.gs.frame = frame_;
+        in0.gs.tr_ld = max_trailing_ * H; in0.gs.pad = tts_pad_;
+    }
+    if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_, ticket_, s,
+                       gather_input ? &in0 : nullptr))
         return false;
     // final RMSNorm (hidden_states, side output) + codec_head -> logits  (:1496-1505)
     GemvParams h;
@@ -287,15 +332,25 @@ bool Engine::enqueue_talker_step(int S, hipStream_t s) {
     return gemv(h, s);
 }
 
-// 16 passes of the 5-layer code predictor, token chosen on device each pass (trt_code_predictor.cpp:484-600)
-bool Engine::enqueue_cp_frame(int S, hipStream_t s) {
+// 16 passes of the 5-layer code predictor, token chosen on device each pass (trt_code_predictor.cpp:484-600).
+// Pass inputs are assembled by layer 0's QKV prologue: pass 0 the talker hidden state, pass 1 codec_embd[code 0],
+// pass p >= 2 code_pred.codec_embd[p-2][code p-1]; the raw row lands in cpx_ (the pass's residual stream).
+// logits_host (tests only, never captured): every head's logits copied out after its GEMV.
+bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
-    Q3T_HIP(hipMemcpyAsync(cpx_, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, s));
+    std::vector<float> lg;
     for (int p = 0; p < 16; ++p) {
-        if (p == 1) Q3T_HIP(hipMemcpyAsync(cpx_, cp_in1_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, s));
+        StackInput in0;
+        if (p == 0) {
+            in0.pro = PRO_RMS; in0.x = hidden_;
+        } else {
+            in0.pro = PRO_RMS_G1;
+            in0.gs.tok = tokens_; in0.gs.tok_ld = 16; in0.gs.tok_col0 = p - 1;
+            in0.gs.tab0 = p == 1 ? codec_embd_ : cp_embd_[p - 2];
+        }
         if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_,
-                           rope_, part_, s))
+                           rope_, part_, ticket_, s, &in0, cp_fused_attn_))
             return false;
         if (p == 0) continue;
         const int step = p - 1;
@@ -304,13 +359,19 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s) {
         h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
         if (!gemv(h, s)) return false;
+        if (logits_host) {
+            lg.resize((size_t)S * c_.cp_vocab);
+            Q3T_HIP(hipMemcpyAsync(lg.data(), cp_logits_, lg.size() * 4, hipMemcpyDeviceToHost, s));
+            Q3T_HIP(hipStreamSynchronize(s));
+            for (int b = 0; b < S; ++b)
+                std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
+        }
         CpSelParams cs;
         cs.logits = cp_logits_; cs.V = c_.cp_vocab; cs.S = S; cs.step = step;
         cs.tokens = tokens_; cs.codes = codes_; cs.frame = frame_; cs.done = done_;
         cs.max_len = codes_max_len_; cs.ncb = 16;
         cs.temperature = gp_.temperature; cs.top_k = gp_.top_k; cs.seed = gp_.seed; cs.utt = utt_;
-        cs.next_table = step < 14 ? cp_embd_[step] : nullptr;
-        cs.x_next = cpx_; cs.H = H;
+        cs.H = H;
         if (!cp_select(cs, s)) return false;
     }
     return true;
@@ -322,15 +383,10 @@ bool Engine::enqueue_frame(int S, hipStream_t s) {
     cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
     cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
     cb.rep = gp_.rep_penalty; cb.temperature = gp_.temperature; cb.top_k = gp_.top_k; cb.seed = gp_.seed; cb.utt = utt_;
-    cb.next_table = codec_embd_; cb.x_next = cp_in1_; cb.H = c_.hidden;
+    cb.H = c_.hidden;
     if (!cb0_select(cb, s)) return false;
     if (!enqueue_cp_frame(S, s)) return false;
-    StepEmbdParams se;
-    se.tokens = tokens_; se.codec_embd = codec_embd_; se.cp_embd = cp_embd_dev_;
-    se.trailing = trailing_; se.trailing_len = trailing_len_; se.max_trailing = max_trailing_;
-    se.tts_pad = tts_pad_; se.frame = frame_; se.out = x_; se.S = S; se.H = c_.hidden; se.ncb = 16;
-    if (!step_embd(se, s)) return false;
-    if (!enqueue_talker_step(S, s)) return false;
+    if (!enqueue_talker(S, s, true)) return false;
     return advance(pos_, frame_, S, s);
 }
 
@@ -618,45 +674,13 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     g_frame_.clear();
     Q3T_HIP(hipMemcpyAsync(hidden_, hidden, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
-    std::vector<RowRecipe> rec(S);
-    for (int s = 0; s < S; ++s) rec[s] = RowRecipe{cp_in1_ + (size_t)s * H, {{codec_embd_ + (size_t)cb0[s] * H, 1}, {nullptr, 0}, {nullptr, 0}}};
-    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), S * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
-    if (!rows_recipe(recipe_, S, H, stream_)) return false;
+    std::vector<int> tk0((size_t)S * 16, 0);
+    for (int s = 0; s < S; ++s) tk0[(size_t)s * 16] = cb0[s];
+    Q3T_HIP(hipMemcpyAsync(tokens_, tk0.data(), tk0.size() * 4, hipMemcpyHostToDevice, stream_));
     std::vector<int> fr(S, frame), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
-    if (!logits_all) {
-        if (!enqueue_cp_frame(S, stream_)) return false;
-    } else {
-        // same launches as enqueue_cp_frame, with the per-step logits copied out
-        const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
-        Q3T_HIP(hipMemcpyAsync(cpx_, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, stream_));
-        std::vector<float> lg((size_t)S * c_.cp_vocab);
-        for (int p = 0; p < 16; ++p) {
-            if (p == 1) Q3T_HIP(hipMemcpyAsync(cpx_, cp_in1_, (size_t)S * H * 4, hipMemcpyDeviceToDevice, stream_));
-            if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_, rope_, part_, stream_))
-                return false;
-            if (p == 0) continue;
-            const int step = p - 1;
-            GemvParams h;
-            h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
-            h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
-            h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
-            if (!gemv(h, stream_)) return false;
-            Q3T_HIP(hipMemcpyAsync(lg.data(), cp_logits_, lg.size() * 4, hipMemcpyDeviceToHost, stream_));
-            Q3T_HIP(hipStreamSynchronize(stream_));
-            for (int s = 0; s < S; ++s)
-                std::memcpy(logits_all + ((size_t)s * 15 + step) * c_.cp_vocab, lg.data() + (size_t)s * c_.cp_vocab, c_.cp_vocab * 4);
-            CpSelParams cs;
-            cs.logits = cp_logits_; cs.V = c_.cp_vocab; cs.S = S; cs.step = step;
-            cs.tokens = tokens_; cs.codes = codes_; cs.frame = frame_; cs.done = done_;
-            cs.max_len = codes_max_len_; cs.ncb = 16;
-            cs.temperature = temperature; cs.top_k = top_k; cs.seed = seed; cs.utt = utt_;
-            cs.next_table = step < 14 ? cp_embd_[step] : nullptr;
-            cs.x_next = cpx_; cs.H = H;
-            if (!cp_select(cs, stream_)) return false;
-        }
-    }
+    if (!enqueue_cp_frame(S, stream_, logits_all)) return false;
     std::vector<int> tk((size_t)S * 16);
     Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
@@ -680,7 +704,7 @@ bool Engine::cb0_select_host(int S, const float *logits, const uint8_t *seen, co
     cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
     cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
     cb.rep = gp.rep_penalty; cb.temperature = gp.temperature; cb.top_k = gp.top_k; cb.seed = gp.seed; cb.utt = utt_;
-    cb.next_table = codec_embd_; cb.x_next = cp_in1_; cb.H = c_.hidden;
+    cb.H = c_.hidden;
     if (!cb0_select(cb, stream_)) return false;
     std::vector<int> tk((size_t)S * 16);
     Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));

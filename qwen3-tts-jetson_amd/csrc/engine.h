@@ -76,7 +76,8 @@ private:
     bool upload_weights(const Gguf &g);
     bool alloc_state();
     bool enqueue_talker_step(int S, hipStream_t s);
-    bool enqueue_cp_frame(int S, hipStream_t s);
+    bool enqueue_talker(int S, hipStream_t s, bool gather_input);
+    bool enqueue_cp_frame(int S, hipStream_t s, float *logits_host = nullptr);
     bool enqueue_frame(int S, hipStream_t s);
     bool enqueue_text_projection(int n_rows, hipStream_t s);
     bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));
@@ -93,13 +94,14 @@ private:
     uint16_t *text_embd_ = nullptr, *fc1_ = nullptr, *fc2_ = nullptr, *codec_embd_ = nullptr, *codec_head_ = nullptr;
     float *fc1_b_ = nullptr, *fc2_b_ = nullptr, *out_norm_ = nullptr, *cp_out_norm_ = nullptr;
     std::vector<uint16_t *> cp_embd_, cp_head_;
-    uint16_t **cp_embd_dev_ = nullptr;
+    uint16_t **tabs16_dev_ = nullptr;   // codec_embd + code_pred.codec_embd[0..14]
     float *rope_ = nullptr;
     int rope_len_ = 0;
 
     // activations / state (sized for max_slots)
     float *x_ = nullptr, *qkv_ = nullptr, *logits_ = nullptr, *hidden_ = nullptr, *cpx_ = nullptr, *cp_in1_ = nullptr;
     float *cp_logits_ = nullptr, *part_ = nullptr;
+    unsigned *ticket_ = nullptr;   // split-attention arrival counters [S][n_kv]
     uint16_t *attn_ = nullptr, *hmlp_ = nullptr;
     uint16_t *kc_ = nullptr, *vc_ = nullptr, *cpkc_ = nullptr, *cpvc_ = nullptr;
     int *pos_ = nullptr, *frame_ = nullptr, *done_ = nullptr, *token_ = nullptr, *tokens_ = nullptr;
@@ -117,6 +119,7 @@ private:
     RowRecipe *recipe_ = nullptr;
     int recipe_cap_ = 0;
     GenParams gp_;   // parameters baked into the captured frame graph
+    bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
     std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;

@@ -4,8 +4,40 @@
 
 namespace q3t {
 
-enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3 };
+// PRO_RMS_G1 / PRO_RMS_G16: RMSNorm over a GatherSum source (1 table row / 16 table rows + trailing-or-pad row)
+// PRO_CPATT: the code predictor's whole attention (head RMSNorm + RoPE + KV append + softmax(QK^T)V over <= 16
+// positions) computed in the O-projection's prologue from the raw QKV rows (GemvParams::att)
+enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3, PRO_RMS_G1 = 4, PRO_RMS_G16 = 5, PRO_CPATT = 6 };
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_SWIGLU = 3 };
+
+// f32 activation row assembled on the fly by the gather prologues:
+//   PRO_RMS_G1:  x[b] = tab0[tok[b * tok_ld + tok_col0]]                       (code-predictor pass input,
+//                trt_code_predictor.cpp:552-592)
+//   PRO_RMS_G16: x[b] = tabs[0][tok[b][0]] + ... + tabs[15][tok[b][15]] + (frame[b] < tr_len[b] ? tr[b][frame[b]]
+//                : pad[b])  (the talker step embedding, tts_transformer.cpp:2529-2553; tok_ld must be 16)
+// f16 table rows converted and summed left to right in f32.
+struct GatherSum {
+    const int *tok = nullptr;
+    int tok_ld = 16, tok_col0 = 0;
+    const uint16_t *tab0 = nullptr;        // G1: the table
+    const uint16_t *const *tabs = nullptr; // G16: device array of 16 tables [V][K]
+    const float *tr = nullptr;             // optional f32 term: [B][tr_ld] rows of K, indexed by frame
+    const int *tr_len = nullptr, *frame = nullptr;
+    int tr_ld = 0;
+    const float *pad = nullptr;            // [B][K]
+};
+
+// PRO_CPATT source: one new token per slot at position pos[b] (< 16) over a 16-position F16 cache
+// (scripts/export_code_predictor.py:132-231 step semantics; 16 q heads / 8 kv heads / D 128 only)
+struct CpAttnSrc {
+    const float *qkv = nullptr;           // [B][ld] raw Q | K | V rows of the QKV GEMV
+    int ld = 0;
+    const float *qn = nullptr, *kn = nullptr;  // head-norm weights [128]
+    float eps = 1e-6f;
+    const float *rope = nullptr;          // [pos][128] (cos, sin) pairs
+    const int *pos = nullptr;             // [B]
+    uint16_t *kc = nullptr, *vc = nullptr;  // this layer's cache [B][8][16][128] f16
+};
 
 // y[b][n] = epilogue( W[n][:] . f16(prologue(x[b][:])) ),  W f16 row-major [N][K]
 struct GemvParams {
@@ -17,7 +49,10 @@ struct GemvParams {
     const int *x_idx = nullptr;   // optional row gather: row of batch b = x_idx[b]
     const float *nw = nullptr, *nb = nullptr;  // norm weight / bias (RMS, LN)
     float eps = 1e-6f;
+    GatherSum gs;                 // PRO_RMS_G1 / PRO_RMS_G16 source
+    CpAttnSrc att;                // PRO_CPATT source
     float *side_out = nullptr;    // normalized prologue rows (f32 [B][K]) written by x-block 0
+    float *raw_out = nullptr;     // raw (pre-norm) f32 prologue rows [B][K] written by x-block 0
     int act = ACT_NONE;           // ACT_SWIGLU: rows interleaved in 16-row blocks [gate16 | up16]
     const float *bias = nullptr, *scale = nullptr;
     const float *resid = nullptr;  // out = resid[b][n] + (...)
@@ -30,9 +65,11 @@ struct GemvParams {
     int orow_mul = 1, orow_add = 0;  // output row of batch b = b*orow_mul + orow_add
 };
 bool gemv(const GemvParams &p, hipStream_t s);
+void gemv_set_min_blocks(int n);   // tuning hook (tools/dev/kbench)
 
-// Qwen3 attention for one new token per slot (decode / code-predictor pass), fused with q/k head RMSNorm,
-// NEOX RoPE (host cos/sin table), F16 KV append at pos[slot] and split-K flash-decode.
+// Qwen3 attention for one new token per slot (talker decode / unfused code-predictor pass), fused with q/k head
+// RMSNorm, NEOX RoPE (host cos/sin table), F16 KV append at pos[slot] and split-K flash-decode over ATTN_CHUNK-position
+// chunks; the last split to finish (agent-scope ticket) combines the partials in the same launch (attn.hip).
 struct AttnParams {
     const float *qkv = nullptr;   // [S][(nH + 2 nKV) * D] f32
     const float *qn = nullptr, *kn = nullptr;  // head-norm weights [D]
@@ -41,12 +78,14 @@ struct AttnParams {
     const int *pos = nullptr;     // [S] position of the new token
     uint16_t *kc = nullptr, *vc = nullptr;  // cache base of this layer: [S][nKV][n_ctx][D] f16
     int n_ctx = 0, S = 0, nH = 0, nKV = 0, D = 0;
-    int max_splits = 1;           // grid z; chunk = 256 positions
-    float *part = nullptr;        // [S][nH][max_splits][D + 2]
+    int max_splits = 1;           // grid z = ceil(n_ctx / ATTN_CHUNK)
+    float *part = nullptr;        // [S][nKV][max_splits][R][D + 2] split partials (m, l, acc)
+    unsigned *ticket = nullptr;   // [S][nKV] arrival counters, zero between launches
     uint16_t *out = nullptr;      // [S][nH*D] f16 (rounded attention output, the O-proj input)
 };
 bool attn_decode(const AttnParams &p, hipStream_t s);
-constexpr int ATTN_CHUNK = 256;
+constexpr int ATTN_CHUNK = 64;
+constexpr int ATTN_MAX_SPLITS = 160;   // n_ctx <= 10240
 
 // CB0 logit processing + greedy/sampled selection (tts_transformer.cpp:2417-2499), one block per slot.
 struct Cb0Params {
