@@ -143,8 +143,10 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float m = sc[0][h];
 #pragma unroll
         for (int pi = 1; pi < NP; ++pi) m = fmaxf(m, sc[pi][h]);
+        if constexpr (LPP == 16) m = rows_max(m);
+        else
 #pragma unroll
-        for (int o = LPP; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            for (int o = LPP; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
         if (lane == 0) wred[wave][h] = m;
     }
     __syncthreads();
@@ -160,8 +162,10 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
             pr[pi][h] = ok[pi] ? expf(sc[pi][h] - M[h]) : 0.0f;
             l += pr[pi][h];
         }
+        if constexpr (LPP == 16) l = rows_sum(l);
+        else
 #pragma unroll
-        for (int o = LPP; o < 64; o <<= 1) l += __shfl_xor(l, o, 64);
+            for (int o = LPP; o < 64; o <<= 1) l += __shfl_xor(l, o, 64);
         if (lane == 0) wred[wave][h] = l;
     }
     // ---- (5) P.V over this lane's positions, reduced over the position groups
@@ -190,8 +194,10 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             float a = acc[h][e];
+            if constexpr (LPP == 16) a = rows_sum(a);
+            else
 #pragma unroll
-            for (int o = LPP; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+                for (int o = LPP; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
             if (lane < LPP && h < R) ared[wave][h][li * 8 + e] = a;
         }
     __syncthreads();

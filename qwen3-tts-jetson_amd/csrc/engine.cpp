@@ -50,6 +50,7 @@ static bool env_flag(const char *name, bool dflt) {
 bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx) {
     device_ = device;
     cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
+    fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
     if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
@@ -209,6 +210,7 @@ bool Engine::alloc_state() {
     cp_logits_ = dalloc<float>((size_t)S * c_.cp_vocab);
     part_ = dalloc<float>((size_t)S * c_.n_heads * max_splits * (D + 2));
     ticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
+    sel_ticket_ = dalloc<unsigned>((size_t)S);
     attn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
     hmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
     const size_t kv_layer = (size_t)S * c_.n_kv * max_ctx_ * D;
@@ -306,11 +308,25 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
     return true;
 }
 
-bool Engine::enqueue_talker_step(int S, hipStream_t s) { return enqueue_talker(S, s, false); }
+bool Engine::enqueue_talker_step(int S, hipStream_t s) { return enqueue_talker(S, s, false, false); }
+
+SelectSpec Engine::select_spec(int mode, const GenParams &gp, int frame_offset, int step) const {
+    SelectSpec sp;
+    sp.mode = mode;
+    sp.V = mode == SEL_CB0 ? c_.codec_vocab : c_.cp_vocab;
+    sp.ticket = sel_ticket_;
+    sp.tokens = tokens_; sp.codes = codes_; sp.max_len = codes_max_len_; sp.ncb = 16;
+    sp.frame = frame_; sp.frame_offset = frame_offset; sp.done = done_;
+    sp.temperature = gp.temperature; sp.top_k = gp.top_k; sp.seed = gp.seed; sp.utt = utt_;
+    sp.step = step;
+    sp.seen = seen_; sp.n_tokens = n_tokens_; sp.force_frames = force_; sp.eos = c_.codec_eos; sp.rep = gp.rep_penalty;
+    return sp;
+}
 
 // gather_input: the step embedding (tts_transformer.cpp:2529-2553) is assembled by layer 0's QKV prologue from the
 // frame's 16 codes (PRO_RMS_G16) instead of being read from x_
-bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input) {
+// select_next: the codec head's last workgroup also selects CB0 of the NEXT frame (frame_ + 1) in the same launch
+bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
@@ -329,6 +345,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input) {
     h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = S;
     h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_;
     h.out_f32 = logits_; h.ldo = c_.codec_vocab;
+    if (select_next) h.sel = select_spec(SEL_CB0, gp_, 1, 0);
     return gemv(h, s);
 }
 
@@ -358,6 +375,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
         h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
+        if (fused_select_) h.sel = select_spec(SEL_CP, gp_, 0, step);
         if (!gemv(h, s)) return false;
         if (logits_host) {
             lg.resize((size_t)S * c_.cp_vocab);
@@ -366,27 +384,17 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
             for (int b = 0; b < S; ++b)
                 std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
         }
-        CpSelParams cs;
-        cs.logits = cp_logits_; cs.V = c_.cp_vocab; cs.S = S; cs.step = step;
-        cs.tokens = tokens_; cs.codes = codes_; cs.frame = frame_; cs.done = done_;
-        cs.max_len = codes_max_len_; cs.ncb = 16;
-        cs.temperature = gp_.temperature; cs.top_k = gp_.top_k; cs.seed = gp_.seed; cs.utt = utt_;
-        cs.H = H;
-        if (!cp_select(cs, s)) return false;
+        if (!fused_select_ && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
     }
     return true;
 }
 
+// one frame = [CB0 select] -> 16 code-predictor passes -> talker step -> pos/frame advance.  With fused selection
+// the CB0 of frame f+1 is chosen inside frame f's talker head launch (frame 0's by generate() after the prefill).
 bool Engine::enqueue_frame(int S, hipStream_t s) {
-    Cb0Params cb;
-    cb.logits = logits_; cb.V = c_.codec_vocab; cb.S = S; cb.eos = c_.codec_eos;
-    cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
-    cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
-    cb.rep = gp_.rep_penalty; cb.temperature = gp_.temperature; cb.top_k = gp_.top_k; cb.seed = gp_.seed; cb.utt = utt_;
-    cb.H = c_.hidden;
-    if (!cb0_select(cb, s)) return false;
+    if (!fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, s)) return false;
     if (!enqueue_cp_frame(S, s)) return false;
-    if (!enqueue_talker(S, s, true)) return false;
+    if (!enqueue_talker(S, s, true, fused_select_)) return false;
     return advance(pos_, frame_, S, s);
 }
 
@@ -592,6 +600,7 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     }
     for (int s = 0; s < S; ++s) posv[s] = plen;
     if (!set_slot_state(S, posv, frame0)) return false;
+    if (fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, stream_)) return false;
     Q3T_HIP(hipEventRecord(e1, stream_));
     // ---- frame loop: one graph per frame; done flags polled every 16 frames
     if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) return false;
@@ -699,13 +708,7 @@ bool Engine::cb0_select_host(int S, const float *logits, const uint8_t *seen, co
     std::vector<int> force(S, gp.force_frames), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(force_, force.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
-    Cb0Params cb;
-    cb.logits = logits_; cb.V = V; cb.S = S; cb.eos = c_.codec_eos;
-    cb.seen = seen_; cb.frame = frame_; cb.n_tokens = n_tokens_; cb.force_frames = force_;
-    cb.done = done_; cb.token = tokens_; cb.codes = codes_; cb.max_len = codes_max_len_; cb.ncb = 16;
-    cb.rep = gp.rep_penalty; cb.temperature = gp.temperature; cb.top_k = gp.top_k; cb.seed = gp.seed; cb.utt = utt_;
-    cb.H = c_.hidden;
-    if (!cb0_select(cb, stream_)) return false;
+    if (!select_tokens(select_spec(SEL_CB0, gp, 0, 0), logits_, S, stream_)) return false;
     std::vector<int> tk((size_t)S * 16);
     Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));

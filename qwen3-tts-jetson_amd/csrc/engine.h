@@ -76,7 +76,8 @@ private:
     bool upload_weights(const Gguf &g);
     bool alloc_state();
     bool enqueue_talker_step(int S, hipStream_t s);
-    bool enqueue_talker(int S, hipStream_t s, bool gather_input);
+    bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next);
+    SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;
     bool enqueue_cp_frame(int S, hipStream_t s, float *logits_host = nullptr);
     bool enqueue_frame(int S, hipStream_t s);
     bool enqueue_text_projection(int n_rows, hipStream_t s);
@@ -102,6 +103,7 @@ private:
     float *x_ = nullptr, *qkv_ = nullptr, *logits_ = nullptr, *hidden_ = nullptr, *cpx_ = nullptr, *cp_in1_ = nullptr;
     float *cp_logits_ = nullptr, *part_ = nullptr;
     unsigned *ticket_ = nullptr;   // split-attention arrival counters [S][n_kv]
+    unsigned *sel_ticket_ = nullptr;   // fused head+select arrival counters [S]
     uint16_t *attn_ = nullptr, *hmlp_ = nullptr;
     uint16_t *kc_ = nullptr, *vc_ = nullptr, *cpkc_ = nullptr, *cpvc_ = nullptr;
     int *pos_ = nullptr, *frame_ = nullptr, *done_ = nullptr, *token_ = nullptr, *tokens_ = nullptr;
@@ -119,6 +121,7 @@ private:
     RowRecipe *recipe_ = nullptr;
     int recipe_cap_ = 0;
     GenParams gp_;   // parameters baked into the captured frame graph
+    bool fused_select_ = true;    // Q3T_FUSED_SELECT=0: separate selection launches
     bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }

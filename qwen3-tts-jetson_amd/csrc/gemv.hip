@@ -17,6 +17,7 @@
 // prologue shapes, tools/dev/kbench).  Large-K or wide-batch calls
 // (prefill, vocoder) take the streaming loop (NL = 0).
 #include "kernels.h"
+#include "select.h"
 
 #include <cstdlib>
 
@@ -182,8 +183,11 @@ __device__ __forceinline__ void cpatt_finish(const GemvParams &p, int b, bool va
         const float4 v = a.raw[i];
         const float x[4] = {v.x, v.y, v.z, v.w};
         double ss = (double)(x[0] * x[0]) + (double)(x[1] * x[1]) + (double)(x[2] * x[2]) + (double)(x[3] * x[3]);
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        ss += dpp_d<DPP_XOR1>(ss);   // all-reduce over the 32-lane half-wave that holds this head
+        ss += dpp_d<DPP_XOR2>(ss);
+        ss += dpp_d<DPP_HALF_MIRROR>(ss);
+        ss += dpp_d<DPP_MIRROR>(ss);
+        ss += xrow16_d(ss);
         const float scale = 1.0f / sqrtf((float)(ss / CPA_D) + A.eps);
         const float4 w = i < 2 ? a.qn : a.kn;
         const float w4[4] = {w.x, w.y, w.z, w.w};
@@ -197,7 +201,7 @@ __device__ __forceinline__ void cpatt_finish(const GemvParams &p, int b, bool va
         float o4[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const float mine = y[i][e], other = __shfl_xor(mine, 16, 64);
+            const float mine = y[i][e], other = xrow16(mine);
             const float c = cs[2 * e], s = cs[2 * e + 1];
             o4[e] = f16r(lo ? mine * c - other * s : other * s + mine * c);
         }
@@ -236,8 +240,7 @@ __device__ __forceinline__ void cpatt_finish(const GemvParams &p, int b, bool va
         }
         const float s = j <= pos ? acc * (1.0f / sqrtf((float)CPA_D)) : -INFINITY;
         float m = s;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 16));
+        m = group_max<16>(m);
         const float e = j <= pos ? expf(s - m) : 0.0f;
         const float ls = group_sum<16>(e);
         sc[h * CPA_POS + j] = e;
@@ -305,8 +308,8 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
     int rows[RPG];
     bool unit_ok = true;
     const int unit = blockIdx.x * GPB + g;
-    if (RPG == 2 && p.act == ACT_SWIGLU) {
-        // gate/up interleaved in 16-row blocks: unit u -> gate row (u/16)*32 + u%16, up row +16
+    if constexpr (RPG == 2) {
+        // SwiGLU: gate/up interleaved in 16-row blocks: unit u -> gate row (u/16)*32 + u%16, up row +16
         unit_ok = unit < N / 2;
         const int u = min(unit, N / 2 - 1);
         rows[0] = (u >> 4) * 32 + (u & 15);
@@ -557,47 +560,74 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
 #pragma unroll
                 for (int b = 0; b < BT; ++b) red[((kslice * GPB + g) * RPG + i) * BT + b] = acc[i][b];
         __syncthreads();
-        if (kslice != 0) return;
+        if (kslice == 0)
 #pragma unroll
-        for (int i = 0; i < RPG; ++i)
+            for (int i = 0; i < RPG; ++i)
 #pragma unroll
-            for (int b = 0; b < BT; ++b) {
-                float s = 0.0f;
+                for (int b = 0; b < BT; ++b) {
+                    float s = 0.0f;
 #pragma unroll
-                for (int q = 0; q < KS; ++q) s += red[((q * GPB + g) * RPG + i) * BT + b];
-                acc[i][b] = s;
-            }
+                    for (int q = 0; q < KS; ++q) s += red[((q * GPB + g) * RPG + i) * BT + b];
+                    acc[i][b] = s;
+                }
     }
+    constexpr bool kSel = RPG == 1 && PRO == PRO_RMS;   // head GEMVs may select the token in the same launch
+    const bool sel = kSel && p.sel.mode != SEL_NONE;
 
     // ---------------- (5) epilogue: lane l16 of each group writes batch column l16
+    if (kslice == 0) {
 #pragma unroll
-    for (int bi = 0; bi < BT; ++bi) {
-        if (bi != l16 || bi >= nb) continue;
-        const int bb = b0 + bi;
-        const size_t orow = (size_t)bb * p.orow_mul + p.orow_add;
-        if (p.act == ACT_SWIGLU) {
-            if constexpr (RPG == 2) {
-                if (unit_ok) {
-                    const float h = silu_f(acc[0][bi]) * acc[1][bi];
-                    if (p.out_f16) p.out_f16[orow * p.ldo + unit] = f2h(h);
-                    else p.out_f32[orow * p.ldo + unit] = h;
+        for (int bi = 0; bi < BT; ++bi) {
+            if (bi != l16 || bi >= nb) continue;
+            const int bb = b0 + bi;
+            const size_t orow = (size_t)bb * p.orow_mul + p.orow_add;
+            if (p.act == ACT_SWIGLU) {
+                if constexpr (RPG == 2) {
+                    if (unit_ok) {
+                        const float h = silu_f(acc[0][bi]) * acc[1][bi];
+                        if (p.out_f16) p.out_f16[orow * p.ldo + unit] = f2h(h);
+                        else p.out_f32[orow * p.ldo + unit] = h;
+                    }
                 }
+                continue;
             }
-            continue;
-        }
 #pragma unroll
-        for (int i = 0; i < RPG; ++i) {
-            const int rr = rows[i];
-            if (rr >= N) continue;
-            float v = acc[i][bi];
-            if (p.bias) v += e_bias[i];
-            if (p.act == ACT_SILU) v = silu_f(v);
-            else if (p.act == ACT_GELU) v = gelu_ggml(v);
-            if (p.scale) v *= e_scale[i];
-            if (p.resid) v = e_res[i] + v;
-            if (p.aux) v = e_aux[i] + v;
-            if (p.out_f16) p.out_f16[orow * p.ldo + rr] = f2h(v);
-            else p.out_f32[orow * p.ldo + rr] = v;
+            for (int i = 0; i < RPG; ++i) {
+                const int rr = rows[i];
+                if (rr >= N) continue;
+                float v = acc[i][bi];
+                if (p.bias) v += e_bias[i];
+                if (p.act == ACT_SILU) v = silu_f(v);
+                else if (p.act == ACT_GELU) v = gelu_ggml(v);
+                if (p.scale) v *= e_scale[i];
+                if (p.resid) v = e_res[i] + v;
+                if (p.aux) v = e_aux[i] + v;
+                if (p.out_f16) p.out_f16[orow * p.ldo + rr] = f2h(v);
+                else if (sel) __hip_atomic_store(p.out_f32 + orow * p.ldo + rr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else p.out_f32[orow * p.ldo + rr] = v;
+            }
+        }
+    }
+
+    // ---------------- (6) fused token selection: sc1 logits stores -> vmcnt(0) -> barrier -> one agent-scope ticket
+    // add per workgroup; the last adder loads the logits with sc1 loads and selects (MI355X_MICROARCH.md, hand-off
+    // table row 1).
+    if constexpr (kSel) {
+        if (sel) {
+            SelLds &S = *reinterpret_cast<SelLds *>(att_lds);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0)
+                S.last = __hip_atomic_fetch_add(p.sel.ticket + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                         gridDim.x - 1;
+            __syncthreads();
+            if (S.last) {
+                for (int b = 0; b < nb; ++b) {
+                    select_slot<true>(p.sel, p.out_f32 + (size_t)(b0 + b) * p.ldo, b0 + b, S);
+                    __syncthreads();
+                }
+                if (tid == 0) __hip_atomic_store(p.sel.ticket + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -660,6 +690,12 @@ bool gemv(const GemvParams &p, hipStream_t s) {
         return false;
     }
     if (swiglu && p.pro != PRO_RMS) { set_error("gemv: SwiGLU needs the RMSNorm prologue"); return false; }
+    if (p.sel.mode != SEL_NONE &&
+        (p.pro != PRO_RMS || swiglu || !p.out_f32 || p.out_f16 || p.orow_mul != 1 || p.orow_add != 0 || p.ldo != p.N ||
+         p.sel.V != p.N || p.N > 256 * SEL_VPT_MAX || !p.sel.ticket)) {
+        set_error("gemv: fused selection needs an RMS-prologue head writing f32 logits [B][N] and a ticket buffer");
+        return false;
+    }
     const bool g1 = p.pro == PRO_RMS_G1, g16 = p.pro == PRO_RMS_G16;
     if (p.pro == PRO_CPATT) {
         const CpAttnSrc &A = p.att;
@@ -703,7 +739,8 @@ bool gemv(const GemvParams &p, hipStream_t s) {
     int nl = nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 8 ? 8 : 0;
     if (bt > 2 || Kp > 4096) nl = 0;
     const dim3 grid((unsigned)((units + (16 / ks) - 1) / (16 / ks)), (unsigned)gy);
-    const size_t lds = (size_t)bt * Kp * 2 + 16 * rpg * bt * 4 + 8 * sizeof(double) + (p.pro == PRO_CPATT ? CPA_LDS : 0);
+    const size_t lds = (size_t)bt * Kp * 2 + 16 * rpg * bt * 4 + 8 * sizeof(double) +
+                       (p.pro == PRO_CPATT ? CPA_LDS : 0) + (p.sel.mode != SEL_NONE ? sizeof(SelLds) : 0);
     if (bt == 1) launch_bt<1>(p, rpg, ks, nl, grid, lds, s);
     else if (bt == 2) launch_bt<2>(p, rpg, ks, nl, grid, lds, s);
     else if (bt == 4) launch_bt<4>(p, rpg, ks, nl, grid, lds, s);

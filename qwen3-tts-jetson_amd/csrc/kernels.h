@@ -10,6 +10,36 @@ namespace q3t {
 enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3, PRO_RMS_G1 = 4, PRO_RMS_G16 = 5, PRO_CPATT = 6 };
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_SWIGLU = 3 };
 
+// Token selection (select.h): SEL_CB0 = CB0 logit processing + selection (src/tts_transformer.cpp:2416-2499),
+// SEL_CP = code-predictor token of pass step+1 (trt_code_predictor.cpp:552-592 / k_sample_topk_f32 semantics).
+// Used by the standalone select launch (one 256-thread workgroup per slot) and fused into the head GEMV, where
+// the last head workgroup to finish (arrival ticket) selects in the same launch.
+enum SelMode { SEL_NONE = 0, SEL_CP = 1, SEL_CB0 = 2 };
+struct SelectSpec {
+    int mode = SEL_NONE;
+    int V = 0;
+    unsigned *ticket = nullptr;     // fused: [gridDim.y] arrival counters (zero between launches)
+    int *tokens = nullptr;          // [S][16] frame codes (CB0: col 0; CP: col step+1)
+    int32_t *codes = nullptr;       // [S][max_len][ncb]
+    int max_len = 0, ncb = 16;
+    const int *frame = nullptr;     // [S]
+    int frame_offset = 0;           // selected token belongs to frame[s] + frame_offset
+    int *done = nullptr;            // [S] frame of EOS, else -1 (slots with done >= 0 are skipped)
+    float temperature = 0.f;
+    int top_k = 50;
+    uint64_t seed = 0;
+    const uint64_t *utt = nullptr;  // [S]
+    int step = 0;                   // SEL_CP: 0..14
+    // SEL_CB0
+    uint8_t *seen = nullptr;        // [S][V]
+    const int *n_tokens = nullptr;  // [S]
+    const int *force_frames = nullptr;  // [S] (bench: EOS masked while frame < force)
+    int eos = 2150;
+    float rep = 1.05f;
+};
+// standalone: logits [S][V] -> one workgroup per slot
+bool select_tokens(const SelectSpec &sp, const float *logits, int S, hipStream_t s);
+
 // f32 activation row assembled on the fly by the gather prologues:
 //   PRO_RMS_G1:  x[b] = tab0[tok[b * tok_ld + tok_col0]]                       (code-predictor pass input,
 //                trt_code_predictor.cpp:552-592)
@@ -51,6 +81,7 @@ struct GemvParams {
     float eps = 1e-6f;
     GatherSum gs;                 // PRO_RMS_G1 / PRO_RMS_G16 source
     CpAttnSrc att;                // PRO_CPATT source
+    SelectSpec sel;               // PRO_RMS heads: select in the last workgroup (logits -> out_f32)
     float *side_out = nullptr;    // normalized prologue rows (f32 [B][K]) written by x-block 0
     float *raw_out = nullptr;     // raw (pre-norm) f32 prologue rows [B][K] written by x-block 0
     int act = ACT_NONE;           // ACT_SWIGLU: rows interleaved in 16-row blocks [gate16 | up16]
@@ -87,61 +118,7 @@ bool attn_decode(const AttnParams &p, hipStream_t s);
 constexpr int ATTN_CHUNK = 64;
 constexpr int ATTN_MAX_SPLITS = 160;   // n_ctx <= 10240
 
-// CB0 logit processing + greedy/sampled selection (tts_transformer.cpp:2417-2499), one block per slot.
-struct Cb0Params {
-    float *logits = nullptr;      // [S][V]
-    int V = 0, S = 0, eos = 2150;
-    uint8_t *seen = nullptr;      // [S][V]
-    const int *frame = nullptr;   // [S]
-    const int *n_tokens = nullptr;  // [S]
-    const int *force_frames = nullptr;  // [S] (bench: EOS masked while frame < force)
-    int *done = nullptr;          // [S] frames emitted when finished (EOS), else -1
-    int *token = nullptr;         // [S][16] frame codes; column 0 = selected CB0
-    int32_t *codes = nullptr;     // [S][max_len][ncb]
-    int max_len = 0, ncb = 16;
-    float rep = 1.05f, temperature = 0.f;
-    int top_k = 50;
-    uint64_t seed = 0;
-    const uint64_t *utt = nullptr;  // [S]
-    // pass-1 input of the code predictor: x_next[s] = table[token]
-    const uint16_t *next_table = nullptr;
-    float *x_next = nullptr;
-    int H = 0;
-};
-bool cb0_select(const Cb0Params &p, hipStream_t s);
 
-// code-predictor token (argmax / top-k sampling, trt_cuda_kernels.cu:18-183 semantics) + next-pass gather
-struct CpSelParams {
-    const float *logits = nullptr;  // [S][V]
-    int V = 0, S = 0, step = 0;     // step = 0..14 -> codebook step+1
-    int *tokens = nullptr;          // [S][16] current frame codes (col step+1 written)
-    int32_t *codes = nullptr;       // [S][max_len][ncb]
-    const int *frame = nullptr, *done = nullptr;
-    int max_len = 0, ncb = 16;
-    float temperature = 0.f;
-    int top_k = 50;
-    uint64_t seed = 0;
-    const uint64_t *utt = nullptr;
-    const uint16_t *next_table = nullptr;  // code_pred.codec_embd[step] (nullptr on the last step)
-    float *x_next = nullptr;
-    int H = 0;
-};
-bool cp_select(const CpSelParams &p, hipStream_t s);
-
-// next talker input: e = codec_embd[c0] + sum_c cp_embd[c-1][c_c] + (frame < trailing_len ? trailing[frame] : tts_pad)
-struct StepEmbdParams {
-    const int *tokens = nullptr;     // [S][16]
-    const uint16_t *codec_embd = nullptr;
-    const uint16_t *const *cp_embd = nullptr;  // device array of 15 table pointers
-    const float *trailing = nullptr;  // [S][max_trailing][H]
-    const int *trailing_len = nullptr;
-    int max_trailing = 0;
-    const float *tts_pad = nullptr;   // [S][H]
-    const int *frame = nullptr;
-    float *out = nullptr;             // [S][H]
-    int S = 0, H = 0, ncb = 16;
-};
-bool step_embd(const StepEmbdParams &p, hipStream_t s);
 
 // pos[s]++, frame[s]++
 bool advance(int *pos, int *frame, int S, hipStream_t s);

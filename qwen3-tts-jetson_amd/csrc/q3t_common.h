@@ -45,25 +45,99 @@ __device__ __forceinline__ uint4 ld_nt16(const void *ptr) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// ---------------------------------------------------------------- wave-level reductions (gfx950)
+// DPP row ops (VALU, no LDS round trip) inside 16-lane rows; v_permlane16/32_swap (CDNA4) across rows.  The generic
+// __shfl_xor lowers to ds_bpermute_b32 (an LDS-crossbar round trip per step), measured ~0.9 us for a 6-step wave
+// reduction on the selection path -- too slow for the latency-bound decode chain.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const unsigned lo = dpp_u<CTRL>((unsigned)u), hi = dpp_u<CTRL>((unsigned)(u >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+// value of the same lane in the partner row (lane ^ 16) / partner half (lane ^ 32)
+__device__ __forceinline__ unsigned xrow16_u(unsigned v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((threadIdx.x >> 4) & 1) ? (unsigned)r[0] : (unsigned)r[1];
+}
+__device__ __forceinline__ unsigned xrow32_u(unsigned v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return ((threadIdx.x >> 5) & 1) ? (unsigned)r[0] : (unsigned)r[1];
+}
+__device__ __forceinline__ float xrow16(float v) { return __builtin_bit_cast(float, xrow16_u(__builtin_bit_cast(unsigned, v))); }
+__device__ __forceinline__ float xrow32(float v) { return __builtin_bit_cast(float, xrow32_u(__builtin_bit_cast(unsigned, v))); }
+__device__ __forceinline__ double xrow16_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    return __builtin_bit_cast(double, ((uint64_t)xrow16_u((unsigned)(u >> 32)) << 32) | xrow16_u((unsigned)u));
+}
+__device__ __forceinline__ double xrow32_d(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    return __builtin_bit_cast(double, ((uint64_t)xrow32_u((unsigned)(u >> 32)) << 32) | xrow32_u((unsigned)u));
+}
+
 template <int W>
-__device__ __forceinline__ float group_sum(float v) {   // xor-butterfly inside aligned groups of W lanes
-#pragma unroll
-    for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, W);
+__device__ __forceinline__ float group_sum(float v) {   // all-reduce inside aligned groups of W lanes
+    static_assert(W == 4 || W == 8 || W == 16 || W == 32 || W == 64, "group width");
+    v += dpp_f<DPP_XOR1>(v);
+    v += dpp_f<DPP_XOR2>(v);
+    if constexpr (W >= 8) v += dpp_f<DPP_HALF_MIRROR>(v);
+    if constexpr (W >= 16) v += dpp_f<DPP_MIRROR>(v);
+    if constexpr (W >= 32) v += xrow16(v);
+    if constexpr (W >= 64) v += xrow32(v);
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+template <int W>
+__device__ __forceinline__ float group_max(float v) {
+    v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+    v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+    if constexpr (W >= 8) v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+    if constexpr (W >= 16) v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+    if constexpr (W >= 32) v = fmaxf(v, xrow16(v));
+    if constexpr (W >= 64) v = fmaxf(v, xrow32(v));
     return v;
 }
+__device__ __forceinline__ float wave_max(float v) { return group_max<64>(v); }
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += dpp_d<DPP_XOR1>(v);
+    v += dpp_d<DPP_XOR2>(v);
+    v += dpp_d<DPP_HALF_MIRROR>(v);
+    v += dpp_d<DPP_MIRROR>(v);
+    v += xrow16_d(v);
+    v += xrow32_d(v);
     return v;
 }
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// sum / max over the lanes {l, l^16, l^32, l^48} (same position in the 4 rows), result in every lane
+__device__ __forceinline__ float rows_sum(float v) { v += xrow16(v); return v + xrow32(v); }
+__device__ __forceinline__ float rows_max(float v) { v = fmaxf(v, xrow16(v)); return fmaxf(v, xrow32(v)); }
+__device__ __forceinline__ double rows_sum_d(double v) { v += xrow16_d(v); return v + xrow32_d(v); }
+
+// wave inclusive scan (row_shr DPP within rows, row_bcast15/31 across rows: the GCN scan idiom)
+__device__ __forceinline__ unsigned wave_scan_incl_u(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ float wave_scan_incl_f(float v) {
+    v += dpp_f<0x111>(v);
+    v += dpp_f<0x112>(v);
+    v += dpp_f<0x114>(v);
+    v += dpp_f<0x118>(v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false));
     return v;
 }
 

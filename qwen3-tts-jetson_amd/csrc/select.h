@@ -1,0 +1,273 @@
+// select.h — token selection of the decode path on one 256-thread workgroup (device code, included by the kernel
+// translation units).  Thread t owns the contiguous indices [t*vpt, t*vpt + vpt), vpt = ceil(V / 256) <= 16, in
+// registers, so the inverse-CDF scan runs in index order exactly like the reference's sequential loop.
+//
+//   argmax         first maximum (strict '>' scan, src/tts_transformer.cpp:2051-2061)
+//   top-k sampling /T -> k-th largest by 3-pass radix select on order-preserving keys (11/11/10-bit digits),
+//                  `< thr -> -inf` so ties survive (:2456-2464), optional kept id restored (EOS, :2466-2470),
+//                  exp(v - max), inverse CDF with u * total (:2474-2495; CP: trt_cuda_kernels.cu:120-183)
+//   CB0 processing control-range mask, repetition penalty over the seen set, EOS ramp, bench EOS mask
+//                  (src/tts_transformer.cpp:2416-2445)
+#pragma once
+#include "kernels.h"
+
+namespace q3t {
+
+constexpr int SEL_VPT_MAX = 16;   // V <= 4096
+
+struct SelLds {
+    unsigned hist[2048];
+    float fred[4];
+    int ired[4];
+    unsigned ures[4];
+    unsigned sres[2];
+    float wsum[4];
+    unsigned last;
+};
+
+__device__ __forceinline__ uint32_t sel_fkey(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float sel_keyf(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ float sel_block_max(float v, SelLds &S) {
+    v = wave_max(v);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) S.fred[wave] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(S.fred[0], S.fred[1]), fmaxf(S.fred[2], S.fred[3]));
+}
+
+// (value, index) max with lowest-index tie break over the whole wave (DPP in rows, permlane swaps across rows)
+template <int CTRL>
+__device__ __forceinline__ void sel_pair_step(float &bv, int &bi) {
+    const float ov = dpp_f<CTRL>(bv);
+    const int oi = (int)dpp_u<CTRL>((unsigned)bi);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+__device__ __forceinline__ void sel_pair_reduce(float &bv, int &bi) {
+    sel_pair_step<DPP_XOR1>(bv, bi);
+    sel_pair_step<DPP_XOR2>(bv, bi);
+    sel_pair_step<DPP_HALF_MIRROR>(bv, bi);
+    sel_pair_step<DPP_MIRROR>(bv, bi);
+    float ov = xrow16(bv);
+    int oi = (int)xrow16_u((unsigned)bi);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    ov = xrow32(bv);
+    oi = (int)xrow32_u((unsigned)bi);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+}
+
+// first index of the maximum
+__device__ __forceinline__ int sel_argmax(const float (&v)[SEL_VPT_MAX], int n, int vpt, SelLds &S) {
+    const int t = threadIdx.x;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        const int i = t * vpt + e;
+        if (e < vpt && i < n && (v[e] > bv || bi == 0x7fffffff)) { bv = v[e]; bi = i; }
+    }
+    // NaN-free inputs: strict '>' keeps the first index of a tie inside the thread; across threads the lower index wins
+    sel_pair_reduce(bv, bi);
+    const int lane = t & 63, wave = t >> 6;
+    __syncthreads();
+    if (lane == 0) { S.fred[wave] = bv; S.ired[wave] = bi; }
+    __syncthreads();
+    bv = S.fred[0];
+    bi = S.ired[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w)
+        if (S.fred[w] > bv || (S.fred[w] == bv && S.ired[w] < bi)) { bv = S.fred[w]; bi = S.ired[w]; }
+    return bi == 0x7fffffff ? 0 : bi;
+}
+
+// block inclusive scan over 256 threads (in thread order) of a per-thread count; returns the exclusive prefix,
+// *total = the block total
+__device__ __forceinline__ unsigned sel_scan_u(unsigned loc, unsigned *total, SelLds &S) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned incl = wave_scan_incl_u(loc);
+    __syncthreads();
+    if (lane == 63) S.ures[wave] = incl;
+    __syncthreads();
+    unsigned pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { if (w < wave) pre += S.ures[w]; tot += S.ures[w]; }
+    *total = tot;
+    return pre + incl - loc;
+}
+
+// k-th largest value (1-based k) of v[0..n) by 3-pass MSB radix select (digits of 11, 11 and 10 bits)
+__device__ float sel_kth_largest(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, SelLds &S) {
+    const int t = threadIdx.x;
+    uint32_t keys[SEL_VPT_MAX];
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) keys[e] = (e < vpt && t * vpt + e < n) ? sel_fkey(v[e]) : 0u;
+    uint32_t prefix = 0, pmask = 0;
+    int kk = k;
+    const int shifts[3] = {21, 10, 0};
+    const int bits[3] = {11, 11, 10};
+#pragma unroll
+    for (int ps = 0; ps < 3; ++ps) {
+        const int shift = shifts[ps], nb = 1 << bits[ps], bpt = nb / 256;
+        const uint32_t dmask = (uint32_t)nb - 1u;
+        for (int i = t; i < nb; i += 256) S.hist[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e)
+            if (e < vpt && t * vpt + e < n && (keys[e] & pmask) == prefix) atomicAdd(&S.hist[(keys[e] >> shift) & dmask], 1u);
+        __syncthreads();
+        // thread t owns digits nb-1-t*bpt .. nb-bpt-t*bpt (descending): count of keys with a larger digit = prefix
+        unsigned c[8], loc = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { c[q] = q < bpt ? S.hist[nb - 1 - t * bpt - q] : 0u; loc += c[q]; }
+        unsigned tot;
+        unsigned cum = sel_scan_u(loc, &tot, S);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (q < bpt && cum < (unsigned)kk && (unsigned)kk <= cum + c[q]) {
+                S.sres[0] = (unsigned)(nb - 1 - t * bpt - q);
+                S.sres[1] = cum;
+            }
+            cum += c[q];
+        }
+        __syncthreads();
+        const uint32_t d = S.sres[0];
+        kk -= (int)S.sres[1];
+        prefix |= d << shift;
+        pmask |= dmask << shift;
+        __syncthreads();
+    }
+    return sel_keyf(prefix);
+}
+
+// temperature -> top-k -> keep_id restored -> exp -> inverse CDF with u (v is modified)
+__device__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float temperature, int top_k, float u, int keep_id,
+                          SelLds &S) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = v[e] / temperature;
+    // the kept logit (after /T) is restored after top-k by its owner thread
+    const int keep_owner = keep_id >= 0 ? keep_id / vpt : -1;
+    float keep_v = 0.0f;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (t == keep_owner && t * vpt + e == keep_id) keep_v = v[e];
+    if (top_k > 0 && top_k < n) {
+        const float thr = sel_kth_largest(v, n, vpt, top_k, S);
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e)
+            if (v[e] < thr) v[e] = -INFINITY;
+    }
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (t == keep_owner && t * vpt + e == keep_id) v[e] = keep_v;
+    float m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (e < vpt && t * vpt + e < n) m = fmaxf(m, v[e]);
+    m = sel_block_max(m, S);
+    float loc = 0.0f;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        const bool in = e < vpt && t * vpt + e < n;
+        v[e] = in ? expf(v[e] - m) : 0.0f;
+        loc += v[e];
+    }
+    // block exclusive scan of the per-thread sums (index order)
+    const int lane = t & 63, wave = t >> 6;
+    const float incl = wave_scan_incl_f(loc);
+    __syncthreads();
+    if (lane == 63) S.wsum[wave] = incl;
+    if (t == 0) S.ures[0] = 0x7fffffffu;
+    __syncthreads();
+    float wpre = 0.0f, total = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { if (w < wave) wpre += S.wsum[w]; total += S.wsum[w]; }
+    const float target = u * total;
+    float cum = wpre + incl - loc;
+    int found = 0x7fffffff;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        if (found != 0x7fffffff || e >= vpt) continue;
+        cum += v[e];
+        if (cum >= target && v[e] > 0.0f) found = t * vpt + e;
+    }
+    if (found != 0x7fffffff) atomicMin(reinterpret_cast<int *>(&S.ures[0]), found);
+    __syncthreads();
+    const int r = (int)S.ures[0];
+    return r == 0x7fffffff ? n - 1 : r;
+}
+
+// load one slot's logits row into the owner registers (SC1: agent-scope loads of a row published in this launch)
+template <bool SC1>
+__device__ __forceinline__ void sel_load(const float *row, int n, int vpt, float (&v)[SEL_VPT_MAX]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        const int i = t * vpt + e;
+        const bool in = e < vpt && i < n;
+        if constexpr (SC1) v[e] = in ? __hip_atomic_load(row + (in ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -INFINITY;
+        else v[e] = in ? row[i] : -INFINITY;
+    }
+}
+
+// select the token of slot s from its logits row and record it (SelectSpec semantics, kernels.h)
+template <bool SC1>
+__device__ void select_slot(const SelectSpec &sp, const float *row, int s, SelLds &S) {
+    if (sp.done[s] >= 0) return;   // uniform over the workgroup
+    const int t = threadIdx.x, V = sp.V, vpt = (V + 255) / 256;
+    const int frame = sp.frame[s] + sp.frame_offset;
+    float v[SEL_VPT_MAX];
+    sel_load<SC1>(row, V, vpt, v);
+    int keep = -1;
+    float u;
+    if (sp.mode == SEL_CB0) {
+        const int EOS = sp.eos;
+        const uint8_t *seen = sp.seen + (size_t)s * V;
+        float m = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e) {
+            const int i = t * vpt + e;
+            if (e >= vpt || i >= V) continue;
+            float x = v[e];
+            if (i >= V - 1024 && i != EOS) x = -INFINITY;                          // :2418-2422
+            if (sp.rep != 1.0f && seen[i]) x = x > 0.0f ? x / sp.rep : x * sp.rep;  // :2425-2435
+            v[e] = x;
+            m = fmaxf(m, x);
+        }
+        m = sel_block_max(m, S);
+        const int expected = max(20, sp.n_tokens[s] * 4);                          // :2439-2445
+        const bool masked = frame < sp.force_frames[s];
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e) {
+            if (t * vpt + e != EOS || e >= vpt) continue;
+            if (frame >= expected) {
+                const float ramp = fminf(1.0f, (float)(frame - expected) / (float)expected);
+                v[e] += ramp * ((m + 5.0f) - v[e]);
+            }
+            if (masked) v[e] = -INFINITY;
+        }
+        keep = masked ? -1 : EOS;
+        u = uniform24(sp.seed, sp.utt[s], (uint64_t)frame, 0);
+    } else {
+        u = uniform24(sp.seed, sp.utt[s], (uint64_t)frame, (uint64_t)sp.step + 1);
+    }
+    const int tok = sp.temperature <= 0.0f ? sel_argmax(v, V, vpt, S)
+                                           : sel_sample(v, V, vpt, sp.temperature, sp.top_k, u, keep, S);
+    if (t != 0) return;
+    if (sp.mode == SEL_CB0) {
+        sp.tokens[s * 16] = tok;
+        if (tok == sp.eos) { sp.done[s] = frame; return; }
+        sp.seen[(size_t)s * V + tok] = 1;
+        if (frame < sp.max_len) sp.codes[((size_t)s * sp.max_len + frame) * sp.ncb] = tok;
+    } else {
+        sp.tokens[s * 16 + sp.step + 1] = tok;
+        if (frame < sp.max_len) sp.codes[((size_t)s * sp.max_len + frame) * sp.ncb + sp.step + 1] = tok;
+    }
+}
+
+}  // namespace q3t

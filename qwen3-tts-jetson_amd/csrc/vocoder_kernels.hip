@@ -181,10 +181,7 @@ __global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, const fl
             s[t] = (kpos <= qpos && kpos < F) ? d * scale : -INFINITY;
             mt = fmaxf(mt, s[t]);
         }
-        mt = fmaxf(mt, __shfl_xor(mt, 8, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 4, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 2, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 1, 16));
+        mt = group_max<16>(mt);
         const float mn = fmaxf(m, mt);
         const float corr = (m == -INFINITY) ? 0.0f : expf(m - mn);
         float ls = 0.0f;

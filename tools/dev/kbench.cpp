@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "select.h"
 
 using namespace q3t;
 
@@ -66,6 +67,44 @@ static double time_graph(int reps, const std::function<bool(int)> &fn, int iters
 }
 
 __global__ void k_empty(int *p) { if (p && threadIdx.x == 12345) p[0] = 1; }
+
+// piecewise s_memtime profile of the sampling path (thread 0 records)
+__global__ void __launch_bounds__(256) k_sel_prof(const float *lg, int n, float T, int topk, long long *out) {
+    __shared__ SelLds S;
+    const int vpt = (n + 255) / 256;
+    long long ts[8];
+    ts[0] = __builtin_amdgcn_s_memtime();
+    float v[SEL_VPT_MAX];
+    sel_load<false>(lg, n, vpt, v);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    ts[1] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = v[e] / T;
+    ts[2] = __builtin_amdgcn_s_memtime();
+    float thr = -INFINITY;
+    if (topk > 0) thr = sel_kth_largest(v, n, vpt, topk, S);
+    ts[3] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) if (v[e] < thr) v[e] = -INFINITY;
+    float m = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) if (e < vpt) m = fmaxf(m, v[e]);
+    m = sel_block_max(m, S);
+    ts[4] = __builtin_amdgcn_s_memtime();
+    float loc = 0.0f;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) { v[e] = e < vpt ? expf(v[e] - m) : 0.0f; loc += v[e]; }
+    ts[5] = __builtin_amdgcn_s_memtime();
+    unsigned tot;
+    const unsigned pre = sel_scan_u((unsigned)(loc * 1000.0f), &tot, S);
+    ts[6] = __builtin_amdgcn_s_memtime();
+    const int r = sel_argmax(v, n, vpt, S);
+    ts[7] = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) out[i] = ts[i];
+        out[8] = r + pre;
+    }
+}
 
 int main(int argc, char **argv) {
     CK(hipSetDevice(0));
@@ -139,33 +178,40 @@ int main(int argc, char **argv) {
     }
     // ---- selection kernels
     {
-        const int V = 2048, S = 1;
+        const int S = 1;
         float *lg = dev<float>((size_t)S * 3072, 4.0f);
         int *tokens = dev<int>((size_t)S * 16), *frame = dev<int>(S), *done = dev<int>(S);
         CK(hipMemset(done, 0xff, S * 4));
         int32_t *codes = dev<int32_t>((size_t)S * 64 * 16);
         uint64_t *utt = dev<uint64_t>(S);
-        for (float T : {0.0f, 0.9f}) {
-            const double us = time_graph(15, [&](int i) {
-                CpSelParams cs;
-                cs.logits = lg; cs.V = V; cs.S = S; cs.step = i % 15; cs.tokens = tokens; cs.codes = codes;
-                cs.frame = frame; cs.done = done; cs.max_len = 64; cs.temperature = T; cs.top_k = 50; cs.seed = 1; cs.utt = utt;
-                return cp_select(cs, st);
-            });
-            printf("cp_select T=%.1f: %.2f us\n", T, us);
-        }
         uint8_t *seen = dev<uint8_t>((size_t)S * 3072);
         CK(hipMemset(seen, 0, 3072));
         int *ntok = dev<int>(S), *force = dev<int>(S);
-        for (float T : {0.0f, 0.9f}) {
-            const double us = time_graph(10, [&](int) {
-                Cb0Params cb;
-                cb.logits = lg; cb.V = 3072; cb.S = S; cb.seen = seen; cb.frame = frame; cb.n_tokens = ntok; cb.force_frames = force;
-                cb.done = done; cb.token = tokens; cb.codes = codes; cb.max_len = 64; cb.temperature = T; cb.top_k = 50; cb.utt = utt;
-                return cb0_select(cb, st);
-            });
-            printf("cb0_select T=%.1f: %.2f us\n", T, us);
+        for (int mode : {SEL_CP, SEL_CB0}) {
+            for (int variant = 0; variant < 3; ++variant) {
+                const float T = variant == 0 ? 0.0f : 0.9f;
+                const int topk = variant == 2 ? 0 : 50;
+                SelectSpec sp;
+                sp.mode = mode; sp.V = mode == SEL_CP ? 2048 : 3072; sp.tokens = tokens; sp.codes = codes; sp.max_len = 64;
+                sp.frame = frame; sp.done = done; sp.temperature = T; sp.top_k = topk; sp.seed = 1; sp.utt = utt;
+                sp.seen = seen; sp.n_tokens = ntok; sp.force_frames = force;
+                const double us = time_graph(15, [&](int i) { sp.step = i % 15; return select_tokens(sp, lg, S, st); });
+                printf("select %s T=%.1f top_k=%d: %.2f us\n", mode == SEL_CP ? "cp " : "cb0", T, topk, us);
+            }
         }
+    }
+    {
+        float *lg = dev<float>(4096, 4.0f);
+        long long *o = dev<long long>(16);
+        std::vector<long long> h(16);
+        for (int n : {2048, 3072})
+            for (int topk : {0, 50}) {
+                for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(k_sel_prof, dim3(1), dim3(256), 0, st, lg, n, 0.9f, topk, o);
+                CK(hipStreamSynchronize(st));
+                CK(hipMemcpy(h.data(), o, 16 * 8, hipMemcpyDeviceToHost));
+                printf("sel_prof n=%d topk=%d (s_memtime ticks): load %lld div %lld kth %lld max %lld exp %lld scan %lld argmax %lld\n", n, topk,
+                       h[1] - h[0], h[2] - h[1], h[3] - h[2], h[4] - h[3], h[5] - h[4], h[6] - h[5], h[7] - h[6]);
+            }
     }
     printf("done\n");
     return 0;
