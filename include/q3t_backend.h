@@ -66,6 +66,8 @@ int q3t_get_config(const q3t_ctx *ctx, q3t_config *out);
  * codes: [n_utt][p->max_len][16] int32 row-major [frame][codebook]; n_frames[u] = frames produced. */
 int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                  const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames);
+/* wait until every operation queued on the context's device has finished (hipDeviceSynchronize) */
+int q3t_synchronize(q3t_ctx *ctx);
 /* device time (ms) of the last q3t_generate: prefill and frame loop */
 int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms);
 

@@ -93,6 +93,17 @@ int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const in
     GUARD_END
 }
 
+int q3t_synchronize(q3t_ctx *ctx) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (hipSetDevice(ctx->engine.device()) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        q3t::set_error("q3t_synchronize: device synchronize failed");
+        return Q3T_ERR;
+    }
+    return Q3T_OK;
+    GUARD_END
+}
+
 int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms) {
     CHECK_CTX(ctx);
     if (prefill_ms) *prefill_ms = ctx->engine.last_prefill_ms;

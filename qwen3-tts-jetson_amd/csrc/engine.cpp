@@ -2,6 +2,7 @@
 #include "engine.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -51,6 +52,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     device_ = device;
     cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
     fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
+    if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
     if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
@@ -601,6 +603,8 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     for (int s = 0; s < S; ++s) posv[s] = plen;
     if (!set_slot_state(S, posv, frame0)) return false;
     if (fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, stream_)) return false;
+    const bool dbg = std::getenv("Q3T_DEBUG") != nullptr;
+    if (dbg) { fprintf(stderr, "[q3t] prefill enqueued (plen %d)\n", plen); fflush(stderr); }
     Q3T_HIP(hipEventRecord(e1, stream_));
     // ---- frame loop: one graph per frame; done flags polled every 16 frames
     if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) return false;
@@ -609,7 +613,8 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     bool all_done = false;
     for (int f = 0; f < gp.max_len && !all_done; ++f) {
         Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
-        if ((f + 1) % 16 == 0 && f + 1 < gp.max_len) {
+        if (dbg) { fprintf(stderr, "[q3t] frame %d launched\n", f); fflush(stderr); }
+        if ((f + 1) % poll_every_ == 0 && f + 1 < gp.max_len) {
             Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
             Q3T_HIP(hipStreamSynchronize(stream_));
             all_done = true;
@@ -617,10 +622,15 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
         }
     }
     Q3T_HIP(hipEventRecord(e2, stream_));
+    if (dbg) { fprintf(stderr, "[q3t] frame loop enqueued\n"); fflush(stderr); }
     Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
-    Q3T_HIP(hipMemcpy2DAsync(codes, (size_t)gp.max_len * NCB * 4, codes_, (size_t)codes_max_len_ * NCB * 4,
-                             (size_t)gp.max_len * NCB * 4, S, hipMemcpyDeviceToHost, stream_));
+    // one 1-D copy per slot into the caller's [n_utt][max_len][16] buffer (a pitched 2-D copy into pageable host memory
+    // was observed to overrun the destination under rocprofv3 on ROCm 7.2)
+    for (int s = 0; s < S; ++s)
+        Q3T_HIP(hipMemcpyAsync(codes + (size_t)s * gp.max_len * NCB, codes_ + (size_t)s * codes_max_len_ * NCB,
+                               (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
+    if (dbg) { fprintf(stderr, "[q3t] frame loop done\n"); fflush(stderr); }
     for (int s = 0; s < S; ++s) n_frames[s] = done_h[s] >= 0 ? std::min(done_h[s], gp.max_len) : gp.max_len;
     hipHostFree(done_h);
     float ms1 = 0, ms2 = 0;

@@ -47,6 +47,7 @@ public:
     bool load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx);
     const Config &cfg() const { return c_; }
     int max_slots() const { return max_slots_; }
+    int device() const { return device_; }
     int max_ctx() const { return max_ctx_; }
     hipStream_t stream() const { return stream_; }
     Vocoder *vocoder() { return voc_.get(); }
@@ -121,6 +122,7 @@ private:
     RowRecipe *recipe_ = nullptr;
     int recipe_cap_ = 0;
     GenParams gp_;   // parameters baked into the captured frame graph
+    int poll_every_ = 16;        // frames between done-flag polls (Q3T_POLL_EVERY)
     bool fused_select_ = true;    // Q3T_FUSED_SELECT=0: separate selection launches
     bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
 

@@ -15,8 +15,12 @@ namespace q3t {
 
 constexpr int SEL_VPT_MAX = 16;   // V <= 4096
 
-struct SelLds {
-    unsigned hist[2048];
+constexpr int SEL_CAND = 256;     // boundary-bin candidate list of the top-k threshold search
+
+struct alignas(16) SelLds {
+    unsigned hist[4096];
+    uint32_t cand[SEL_CAND];
+    unsigned ncand;
     float fred[4];
     int ired[4];
     unsigned ures[4];
@@ -100,48 +104,101 @@ __device__ __forceinline__ unsigned sel_scan_u(unsigned loc, unsigned *total, Se
     return pre + incl - loc;
 }
 
-// k-th largest value (1-based k) of v[0..n) by 3-pass MSB radix select (digits of 11, 11 and 10 bits)
+// one MSB radix pass over the keys matching (prefix, pmask): finds the digit (bits [shift, shift+bits)) that holds the
+// kk-th largest key; returns the number of matching keys with a larger digit through *above
+__device__ __forceinline__ uint32_t sel_radix_pass(const uint32_t (&keys)[SEL_VPT_MAX], int n, int vpt, uint32_t prefix,
+                                                   uint32_t pmask, int shift, int bits, int kk, unsigned *above, SelLds &S) {
+    const int t = threadIdx.x, nb = 1 << bits, bpt = nb / 256;
+    const uint32_t dmask = (uint32_t)nb - 1u;
+    for (int i = t * 4; i < nb; i += 1024) *reinterpret_cast<uint4 *>(&S.hist[i]) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (e < vpt && t * vpt + e < n && (keys[e] & pmask) == prefix) atomicAdd(&S.hist[(keys[e] >> shift) & dmask], 1u);
+    __syncthreads();
+    // thread t owns digits nb-1-t*bpt .. nb-bpt-t*bpt (descending; contiguous 16-B reads)
+    unsigned c[16], loc = 0;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+        uint4 h4 = make_uint4(0, 0, 0, 0);
+        if (q4 * 4 < bpt) h4 = *reinterpret_cast<const uint4 *>(&S.hist[nb - t * bpt - 4 - q4 * 4]);
+        c[q4 * 4 + 0] = h4.w; c[q4 * 4 + 1] = h4.z; c[q4 * 4 + 2] = h4.y; c[q4 * 4 + 3] = h4.x;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { if (q >= bpt) c[q] = 0; loc += c[q]; }
+    unsigned tot;
+    unsigned cum = sel_scan_u(loc, &tot, S);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        if (q < bpt && cum < (unsigned)kk && (unsigned)kk <= cum + c[q]) {
+            S.sres[0] = (unsigned)(nb - 1 - t * bpt - q);
+            S.sres[1] = cum;
+        }
+        cum += c[q];
+    }
+    if (t == 0) S.ncand = 0;
+    __syncthreads();
+    *above = S.sres[1];
+    return S.sres[0];
+}
+
+// k-th largest value (1-based k) of v[0..n): one 12-bit MSB histogram pass (4096 bins: sign, exponent, 3 mantissa
+// bits), then an exact rank among the few keys of the boundary bin (LDS candidate list); a boundary bin with more
+// than SEL_CAND keys (degenerate inputs) falls back to two more 10-bit radix passes.
 __device__ float sel_kth_largest(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, SelLds &S) {
     const int t = threadIdx.x;
     uint32_t keys[SEL_VPT_MAX];
 #pragma unroll
     for (int e = 0; e < SEL_VPT_MAX; ++e) keys[e] = (e < vpt && t * vpt + e < n) ? sel_fkey(v[e]) : 0u;
-    uint32_t prefix = 0, pmask = 0;
-    int kk = k;
-    const int shifts[3] = {21, 10, 0};
-    const int bits[3] = {11, 11, 10};
+    unsigned above;
+    const uint32_t d0 = sel_radix_pass(keys, n, vpt, 0u, 0u, 20, 12, k, &above, S);
+    uint32_t prefix = d0 << 20, pmask = 0xFFFu << 20;
+    int kk = k - (int)above;
+    // candidates of the boundary bin
 #pragma unroll
-    for (int ps = 0; ps < 3; ++ps) {
-        const int shift = shifts[ps], nb = 1 << bits[ps], bpt = nb / 256;
-        const uint32_t dmask = (uint32_t)nb - 1u;
-        for (int i = t; i < nb; i += 256) S.hist[i] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < SEL_VPT_MAX; ++e)
-            if (e < vpt && t * vpt + e < n && (keys[e] & pmask) == prefix) atomicAdd(&S.hist[(keys[e] >> shift) & dmask], 1u);
-        __syncthreads();
-        // thread t owns digits nb-1-t*bpt .. nb-bpt-t*bpt (descending): count of keys with a larger digit = prefix
-        unsigned c[8], loc = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) { c[q] = q < bpt ? S.hist[nb - 1 - t * bpt - q] : 0u; loc += c[q]; }
-        unsigned tot;
-        unsigned cum = sel_scan_u(loc, &tot, S);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (q < bpt && cum < (unsigned)kk && (unsigned)kk <= cum + c[q]) {
-                S.sres[0] = (unsigned)(nb - 1 - t * bpt - q);
-                S.sres[1] = cum;
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (e < vpt && t * vpt + e < n && (keys[e] & pmask) == prefix) {
+            const unsigned i = atomicAdd(&S.ncand, 1u);
+            if (i < SEL_CAND) S.cand[i] = keys[e];
+        }
+    __syncthreads();
+    const unsigned nc = S.ncand;
+    if (nc <= 64) {
+        // one wave ranks the candidates with readlane broadcasts (no LDS round trips in the loop)
+        if (t < 64) {
+            const uint32_t me = t < (int)nc ? S.cand[t] : 0u;
+            unsigned gt = 0, eq = 0;
+            for (unsigned j = 0; j < nc; ++j) {
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)me, (int)j);
+                gt += o > me;
+                eq += o == me;
             }
-            cum += c[q];
+            if (t < (int)nc && gt < (unsigned)kk && (unsigned)kk <= gt + eq) S.sres[0] = me;   // same key for all writers
         }
         __syncthreads();
-        const uint32_t d = S.sres[0];
-        kk -= (int)S.sres[1];
-        prefix |= d << shift;
-        pmask |= dmask << shift;
+        const uint32_t r = S.sres[0];
         __syncthreads();
+        return sel_keyf(r);
     }
-    return sel_keyf(prefix);
+    if (nc <= SEL_CAND) {
+        if (t < (int)nc) {
+            const uint32_t me = S.cand[t];
+            unsigned gt = 0, eq = 0;
+#pragma unroll 8
+            for (unsigned j = 0; j < nc; ++j) { const uint32_t o = S.cand[j]; gt += o > me; eq += o == me; }
+            if (gt < (unsigned)kk && (unsigned)kk <= gt + eq) S.sres[0] = me;
+        }
+        __syncthreads();
+        const uint32_t r = S.sres[0];
+        __syncthreads();
+        return sel_keyf(r);
+    }
+    const uint32_t d1 = sel_radix_pass(keys, n, vpt, prefix, pmask, 10, 10, kk, &above, S);
+    prefix |= d1 << 10;
+    pmask |= 0x3FFu << 10;
+    kk -= (int)above;
+    const uint32_t d2 = sel_radix_pass(keys, n, vpt, prefix, pmask, 0, 10, kk, &above, S);
+    return sel_keyf(prefix | d2);
 }
 
 // temperature -> top-k -> keep_id restored -> exp -> inverse CDF with u (v is modified)
@@ -149,7 +206,8 @@ __device__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float tempera
                           SelLds &S) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = v[e] / temperature;
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (e < vpt) v[e] = v[e] / temperature;
     // the kept logit (after /T) is restored after top-k by its owner thread
     const int keep_owner = keep_id >= 0 ? keep_id / vpt : -1;
     float keep_v = 0.0f;

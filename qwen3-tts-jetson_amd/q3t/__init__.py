@@ -49,6 +49,7 @@ _lib.q3t_ctx_destroy.argtypes = [_P]
 _lib.q3t_get_config.argtypes = [_P, C.POINTER(Config)]
 _lib.q3t_generate.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
                               C.POINTER(GenParams), _ip, _ip]
+_lib.q3t_synchronize.argtypes = [_P]
 _lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
 _lib.q3t_vocoder_num_samples.restype = C.c_int64
@@ -63,7 +64,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
-           "q3t_generate", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
+           "q3t_generate", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -131,6 +132,9 @@ class Engine:
         _check(_lib.q3t_generate(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf))
         del keep
         return [codes[i, :nf[i]].copy() for i in range(n)]
+
+    def synchronize(self):
+        _check(_lib.q3t_synchronize(self.h))
 
     def last_timing(self):
         a, b = C.c_double(0), C.c_double(0)

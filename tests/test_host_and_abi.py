@@ -57,8 +57,8 @@ def test_library_exports_every_header_symbol():
 def test_ctx_create_without_gpu_fails_loudly():
     """No CPU fallback: creating a context needs the HIP device; on a GPU-less host the call returns Q3T_ERR with a
     message (it must not crash and must not silently compute on the CPU)."""
-    import torch
-    if torch.cuda.is_available():
+    import hip_py
+    if hip_py.device_count() > 0:
         pytest.skip("a GPU is visible")
     sys.path.insert(0, PKG)
     import q3t

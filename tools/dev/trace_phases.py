@@ -41,3 +41,23 @@ for ph in ("cp", "talker"):
     print(f"  sum of kernel time per frame {tot / 1e3:.1f} us")
 sp = spans["frame"]
 print(f"== frame: {len(sp)} frames, mean span {sum(sp) / max(1, len(sp)) / 1e3:.1f} us (k_advance excluded)")
+
+# ---- time_stage replays at the end of a bench trace: 21 talker-step replays (1 warm + 20 timed, 141 kernels each)
+# then 11 code-predictor-frame replays (1 warm + 10 timed).  Mean replay span = first kernel start -> last kernel end.
+TR, CR = 21, 11
+CPK = max(1, round(sum(len(f) - TALKER_KERNELS for f in frames) / max(1, len(frames)))) if frames else 335
+qrows = [r for r in rows if not r[2].startswith("__amd")]   # runtime copy/fill kernels of time_stage's setup
+tail = qrows[-(TR * TALKER_KERNELS + CR * CPK):] if len(qrows) >= TR * TALKER_KERNELS + CR * CPK else []
+if tail:
+    talk = tail[:TR * TALKER_KERNELS]
+    reps = [talk[i * TALKER_KERNELS:(i + 1) * TALKER_KERNELS] for i in range(TR)][1:]
+    spans_r = [r[-1][1] - r[0][0] for r in reps]
+    busy_r = [sum(e - s for s, e, *_ in r) for r in reps]
+    print(f"== time_stage talker replays: {len(reps)} timed, mean span {sum(spans_r) / len(reps) / 1e3:.1f} us, "
+          f"mean kernel-busy {sum(busy_r) / len(reps) / 1e3:.1f} us; first kernel {reps[0][0][2]}, last {reps[0][-1][2]}")
+    agg_r = collections.defaultdict(list)
+    for r in reps:
+        for s, e, n, gx, gy in r:
+            agg_r[f"{n} g{gx}x{gy}"].append(e - s)
+    for k, v in sorted(agg_r.items(), key=lambda kv: -sum(kv[1])):
+        print(f"  {len(v) / len(reps):6.1f}/replay x {sum(v) / len(v) / 1e3:7.2f} us = {sum(v) / len(reps) / 1e3:8.1f} us  {k}")
