@@ -9,7 +9,10 @@ sampling defaults (temperature 0.9, top-k 50, repetition penalty 1.05) with EOS 
 frames (force_frames).
 
 N GPUs: one process per GPU (torchrun), utterances sharded across ranks (weak scaling), barrier + max-over-ranks
-timing.  Rank 0 prints ONE JSON line.
+timing.  Rank 0 prints ONE JSON line.  Multi-GPU start-up: local rank 0 reads the GGUF files, every
+other rank parses only their headers and receives the packed weight blobs by RCCL broadcast over xGMI; barriers and
+the max-over-ranks of the timer are RCCL all-reduces on the same communicator.  The 128-byte RCCL unique id travels
+through a node-local file (single-node contract); no framework runtime is loaded beside libq3t.so.
 """
 import argparse
 import json
@@ -77,6 +80,72 @@ def cpu_baseline(tts, tok, prompt, frames, vocoder_mode):
             "all_cores": {"cores": allc, **res[allc]}}
 
 
+# ------------------------------------------------------------------------------------------ multi-process plumbing
+class LocalCtrl:
+    """world 1: nothing to synchronise across processes."""
+    def barrier(self):
+        pass
+
+    def max(self, v):
+        return v
+
+
+class RcclCtrl:
+    """barrier / max-over-ranks as RCCL all-reduces on the shared context's communicator."""
+    def __init__(self, eng):
+        self.eng = eng
+
+    def barrier(self):
+        self.eng.allreduce_max([0.0])
+
+    def max(self, v):
+        return float(self.eng.allreduce_max([v])[0])
+
+
+def timed_steps(ctrl, sync, step, steps):
+    """The contract's timed region: device fence + barrier, K steps, device fence + barrier, max over ranks."""
+    sync()
+    ctrl.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    ctrl.barrier()
+    return ctrl.max(time.perf_counter() - t0)
+
+
+def _uid_path():
+    # one file per torchrun job: every rank of a job shares MASTER_PORT and the launching agent (parent pid)
+    return os.path.join(os.environ.get("Q3T_UID_DIR", "/tmp"),
+                        f"q3t_rccl_uid_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
+
+
+def exchange_uid(rank, make_uid, timeout=300.0):
+    """rank 0 publishes the RCCL unique id (atomic rename); the other ranks poll for it."""
+    path = _uid_path()
+    if rank == 0:
+        uid = make_uid()
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return uid
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > timeout:
+            raise RuntimeError(f"rank {rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s")
+        time.sleep(0.05)
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def release_uid():
+    try:
+        os.remove(_uid_path())
+    except OSError:
+        pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,25 +165,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
-    dist = None
-    if world > 1:
-        # control plane only (barriers, max-over-ranks of a host timer): gloo over TCP.  The data path needs no
-        # collective (utterances are sharded); no framework HIP runtime is loaded next to libq3t.so.
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
     import q3t
     from q3t_testutil import prompt as make_prompt, synth_dir
 
-    # synthetic GGUFs: written once per node by local rank 0 (same files for every rank)
-    if local_rank == 0:
-        tts, tok = synth_dir(args.cfg)
-    if dist:
-        dist.barrier()
-    if local_rank != 0:
-        tts, tok = synth_dir(args.cfg)
     voc_mode = {"full": q3t.VOCODER_FULL, "chunk40": q3t.VOCODER_CHUNK40, "none": None}[args.vocoder]
-    eng = q3t.Engine(tts, tok if voc_mode is not None else None, device=local_rank if world > 1 else 0,
-                     max_slots=args.batch, max_ctx=max(args.frames, args.roofline_pos) + 32)
+    max_ctx = max(args.frames, args.roofline_pos) + 32
+    weights = "local GGUF read"
+    if world > 1:
+        # rank 0 writes the synthetic GGUFs (node-local), then publishes the RCCL id; the others wait for it
+        if rank == 0:
+            tts, tok = synth_dir(args.cfg)
+        uid = exchange_uid(rank, q3t.comm_unique_id if rank == 0 else None)
+        if rank != 0:
+            tts, tok = synth_dir(args.cfg)
+        eng = q3t.Engine.shared(tts, tok if voc_mode is not None else None, local_rank, args.batch, max_ctx,
+                                rank, world, uid)
+        if rank == 0:
+            release_uid()
+        weights = f"rank 0 GGUF read + RCCL broadcast to {world - 1} rank(s)"
+        ctrl = RcclCtrl(eng)
+    else:
+        tts, tok = synth_dir(args.cfg)
+        eng = q3t.Engine(tts, tok if voc_mode is not None else None, device=0, max_slots=args.batch, max_ctx=max_ctx)
+        ctrl = LocalCtrl()
     B = args.batch
     prompt = make_prompt(args.cfg)
     H = eng.cfg["hidden"]
@@ -139,21 +212,7 @@ def main():
         step(-1 - w)
     for k in stats:
         stats[k] = 0.0
-    eng.synchronize()   # every engine call is stream-synchronous; this is the explicit device fence of the contract
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    eng.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(ctrl, eng.synchronize, step, args.steps)
     ms_per_step = elapsed / args.steps * 1e3
     total_frames = world * B * args.frames * args.steps
     value = total_frames / elapsed
@@ -176,7 +235,7 @@ def main():
             "config": {"workload": f"configs[1]: Qwen3-TTS-0.6B {B} utterance(s)/GPU x {args.frames} frames, "
                                    f"talker+code-predictor+vocoder({args.vocoder}) HIP path, temp 0.9 top-k 50",
                        "utterances_per_gpu": B, "frames": args.frames, "vocoder": args.vocoder,
-                       "parallelism": f"utterance-sharded dp{world}"},
+                       "parallelism": f"utterance-sharded dp{world}", "weights": weights},
             "rtf": round(ms_per_step / 1e3 / (args.frames * FRAME_SEC), 5),
             "x_realtime": round(args.frames * FRAME_SEC * B / (ms_per_step / 1e3), 1),
             "breakdown_ms_per_step": {k: round(v / args.steps, 2) for k, v in stats.items()},
@@ -200,8 +259,6 @@ def main():
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
     eng.close()
-    if dist:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

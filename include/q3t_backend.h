@@ -11,6 +11,11 @@
  *                         AudioTokenizerDecoder::load_model (src/audio_tokenizer_decoder.h:165) +
  *                         TRTCodePredictor::load_engine/upload_* (src/trt_code_predictor.h:31-50)
  *   q3t_generate          TTSTransformer::generate (src/tts_transformer.h:233-241, .cpp:2342-2574)
+ *   q3t_generate_stream   the same with frame_callback_t on_frames / callback_interval (src/tts_transformer.h:224,
+ *                         .cpp:2517-2523, 2563-2570; caller qwen3_tts.cpp:437-463: the TRT streaming vocoder)
+ *   q3t_comm_unique_id,   SURVEY §8(e) multi-GPU start-up (no reference counterpart: the reference is one process
+ *   q3t_ctx_create_shared on one Jetson): RCCL broadcast of rank 0's packed weight blobs over xGMI
+ *   q3t_ctx_create_replica, q3t_comm_allreduce_max
  *   q3t_talker_forward    TTSTransformer::forward_step (src/tts_transformer.h:189-192, .cpp:1952-2028)
  *   q3t_codepred_frame    TTSTransformer::predict_codes_autoregressive (src/tts_transformer.h:203-207) /
  *                         TRTCodePredictor::run_greedy_loop / run_sampling_loop (src/trt_code_predictor.h:68-79)
@@ -59,6 +64,18 @@ void q3t_default_params(q3t_gen_params *p);
 int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf /* may be NULL: no vocoder */, int device,
                    int max_slots, int max_ctx, q3t_ctx **out);
 void q3t_ctx_destroy(q3t_ctx *ctx);
+
+/* ---- multi-GPU (one process per GPU): rank 0 calls q3t_comm_unique_id and hands the bytes to the other ranks by any
+ * host channel; every rank then calls q3t_ctx_create_shared.  Only rank 0 reads tensor bytes from the GGUF files; the
+ * other ranks parse the headers, lay out identical weight blobs and receive them by ncclBroadcast (RCCL over xGMI). */
+#define Q3T_COMM_ID_BYTES 128
+int q3t_comm_unique_id(uint8_t *id /* [Q3T_COMM_ID_BYTES] */);
+int q3t_ctx_create_shared(const char *tts_gguf, const char *tokenizer_gguf, int device, int max_slots, int max_ctx,
+                          int rank, int world, const uint8_t *id, q3t_ctx **out);
+/* a second context whose weight blobs are copied device-to-device from src's (same or peer device, no file reads) */
+int q3t_ctx_create_replica(q3t_ctx *src, int device, int max_slots, int max_ctx, q3t_ctx **out);
+/* element-wise max over the ranks of a shared context (n <= 64 host doubles; also a barrier); no-op otherwise */
+int q3t_comm_allreduce_max(q3t_ctx *ctx, double *values, int n);
 int q3t_get_config(const q3t_ctx *ctx, q3t_config *out);
 
 /* ---- hot path: prefill + frame loop for n_utt utterances batched in lock-step.
@@ -66,6 +83,14 @@ int q3t_get_config(const q3t_ctx *ctx, q3t_config *out);
  * codes: [n_utt][p->max_len][16] int32 row-major [frame][codebook]; n_frames[u] = frames produced. */
 int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                  const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames);
+/* streaming: on_frames(user, u, codes [n][16], n, 16) is called on the caller's thread every `interval` frames of
+ * utterance u with its newest `interval` frames, and once more after the loop with the remainder (< interval
+ * frames, or the frames before EOS); returning 0 stops utterance u after the frames delivered so far.  The callback
+ * may call q3t_vocoder_decode on the same context (it runs behind the frames already queued). */
+typedef int (*q3t_frame_cb)(void *user, int32_t utterance, const int32_t *codes, int32_t n_frames, int32_t n_codebooks);
+int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
+                        const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
+                        q3t_frame_cb on_frames, void *user, int32_t interval);
 /* wait until every operation queued on the context's device has finished (hipDeviceSynchronize) */
 int q3t_synchronize(q3t_ctx *ctx);
 /* device time (ms) of the last q3t_generate: prefill and frame loop */

@@ -3,11 +3,14 @@
 
 #include <exception>
 
+#include "comm.h"
 #include "engine.h"
 #include "vocoder.h"
 
 struct q3t_ctx {
     q3t::Engine engine;
+    q3t::Comm *comm = nullptr;   // set by q3t_ctx_create_shared
+    ~q3t_ctx() { q3t::comm_destroy(comm); }
 };
 
 namespace {
@@ -66,6 +69,54 @@ int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf, int device,
     GUARD_END
 }
 
+int q3t_comm_unique_id(uint8_t *id) {
+    GUARD_BEGIN
+    if (!id) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return q3t::comm_unique_id(id) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_ctx_create_shared(const char *tts_gguf, const char *tokenizer_gguf, int device, int max_slots, int max_ctx,
+                          int rank, int world, const uint8_t *id, q3t_ctx **out) {
+    GUARD_BEGIN
+    if (!out || !tts_gguf || !id) { q3t::set_error("null argument"); return Q3T_ERR; }
+    *out = nullptr;
+    q3t_ctx *c = new q3t_ctx();
+    if (!q3t::comm_init(&c->comm, world, rank, id, device) ||
+        !c->engine.load(tts_gguf, tokenizer_gguf ? tokenizer_gguf : "", device, max_slots, max_ctx, rank != 0) ||
+        !q3t::comm_bcast_arenas(c->comm, c->engine.weight_arenas(), c->engine.stream())) {
+        delete c;
+        return Q3T_ERR;
+    }
+    *out = c;
+    return Q3T_OK;
+    GUARD_END
+}
+
+int q3t_ctx_create_replica(q3t_ctx *src, int device, int max_slots, int max_ctx, q3t_ctx **out) {
+    GUARD_BEGIN
+    if (!out || !src) { q3t::set_error("null argument"); return Q3T_ERR; }
+    *out = nullptr;
+    q3t_ctx *c = new q3t_ctx();
+    if (!c->engine.load(src->engine.tts_path(), src->engine.tok_path(), device, max_slots, max_ctx, true) ||
+        !c->engine.copy_weights_from(src->engine)) {
+        delete c;
+        return Q3T_ERR;
+    }
+    *out = c;
+    return Q3T_OK;
+    GUARD_END
+}
+
+int q3t_comm_allreduce_max(q3t_ctx *ctx, double *values, int n) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (n > 0 && !values) { q3t::set_error("null argument"); return Q3T_ERR; }
+    if (!ctx->comm) return Q3T_OK;   // a single-process context: nothing to reduce
+    return q3t::comm_allreduce_max(ctx->comm, values, n, ctx->engine.stream()) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
 void q3t_ctx_destroy(q3t_ctx *ctx) { delete ctx; }
 
 int q3t_get_config(const q3t_ctx *ctx, q3t_config *o) {
@@ -90,6 +141,17 @@ int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const in
     CHECK_CTX(ctx);
     if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.generate(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
+                        const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
+                        q3t_frame_cb on_frames, void *user, int32_t interval) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.generate(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames, on_frames, user, interval)
+               ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
 

@@ -48,8 +48,12 @@ static bool env_flag(const char *name, bool dflt) {
     return e ? std::atoi(e) != 0 : dflt;
 }
 
-bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx) {
+bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
+                  bool recv_weights) {
     device_ = device;
+    tts_path_ = tts_gguf;
+    tok_path_ = tok_gguf;
+    wa_.recv = recv_weights;
     cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
     fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
     if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
@@ -97,54 +101,67 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     if (!alloc_state()) return false;
     if (!tok_gguf.empty()) {
         voc_.reset(new Vocoder());
-        if (!voc_->load(tok_gguf, stream_)) return false;
+        if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
     return true;
 }
 
+std::vector<WeightArena *> Engine::weight_arenas() {
+    std::vector<WeightArena *> v{&wa_};
+    if (voc_ && voc_->loaded()) v.push_back(&voc_->weights());
+    return v;
+}
+
 bool Engine::upload_weights(const Gguf &g) {
     const int H = c_.hidden, D = c_.head_dim, Dq = c_.n_heads * D, Dkv = c_.n_kv * D, I = c_.inter;
     if (I % 16 != 0 || H % 8 != 0) { set_error("unsupported hidden/intermediate size"); return false; }
+    // every weight goes into the arena (one blob: the unit of the RCCL broadcast); receiving ranks touch only the
+    // GGUF headers, never the tensor bytes
+    size_t total = 0;
+    for (const GgufTensor &t : g.tensors()) total += (t.nbytes() + 255) & ~(size_t)255;
+    if (!wa_.reserve(total + ((size_t)1 << 20))) return false;
+    const bool recv = wa_.recv;
     auto up16 = [&](const char *name, int64_t cols, int64_t rows) -> uint16_t * {
         const GgufTensor *t = g.find(name);
         if (!check_shape(t, name, cols, rows, GGML_TYPE_F16)) return nullptr;
-        uint16_t *d = dalloc<uint16_t>((size_t)cols * rows);
-        if (!d || hipMemcpy(d, t->data, t->nbytes(), hipMemcpyHostToDevice) != hipSuccess) { set_error(std::string("upload ") + name); return nullptr; }
+        uint16_t *d = wa_.alloc<uint16_t>((size_t)cols * rows);
+        if (!d || !wa_.put(d, t->data, t->nbytes())) return nullptr;
         return d;
     };
     auto up32 = [&](const char *name, int64_t n) -> float * {
         const GgufTensor *t = g.find(name);
         if (!t || t->type != GGML_TYPE_F32 || t->nelements() != n) { set_error(std::string("bad f32 tensor ") + name); return nullptr; }
-        float *d = dalloc<float>((size_t)n);
-        if (!d || hipMemcpy(d, t->data, t->nbytes(), hipMemcpyHostToDevice) != hipSuccess) { set_error(std::string("upload ") + name); return nullptr; }
+        float *d = wa_.alloc<float>((size_t)n);
+        if (!d || !wa_.put(d, t->data, t->nbytes())) return nullptr;
         return d;
     };
     auto rows16 = [&](const std::string &name, int64_t cols, int64_t rows, std::vector<uint16_t> &dst, size_t at) -> bool {
         const GgufTensor *t = g.find(name);
         if (!check_shape(t, name.c_str(), cols, rows, GGML_TYPE_F16)) return false;
-        std::memcpy(dst.data() + at, t->data, t->nbytes());
+        if (!recv) std::memcpy(dst.data() + at, t->data, t->nbytes());
         return true;
     };
     auto layer = [&](const char *pfx, int i, DevLayer &l) -> bool {
         char b[160];
         auto nm = [&](const char *s) { snprintf(b, sizeof b, "%s.blk.%d.%s", pfx, i, s); return std::string(b); };
         // fused [Wq; Wk; Wv] rows
-        std::vector<uint16_t> qkv((size_t)(Dq + 2 * Dkv) * H);
+        const size_t n_qkv = (size_t)(Dq + 2 * Dkv) * H;
+        std::vector<uint16_t> qkv(recv ? 0 : n_qkv);
         if (!rows16(nm("attn_q.weight"), H, Dq, qkv, 0) || !rows16(nm("attn_k.weight"), H, Dkv, qkv, (size_t)Dq * H) ||
             !rows16(nm("attn_v.weight"), H, Dkv, qkv, (size_t)(Dq + Dkv) * H))
             return false;
-        l.qkv = dalloc<uint16_t>(qkv.size());
-        Q3T_HIP(hipMemcpy(l.qkv, qkv.data(), qkv.size() * 2, hipMemcpyHostToDevice));
+        if (!(l.qkv = wa_.alloc<uint16_t>(n_qkv)) || !wa_.put(l.qkv, qkv.data(), n_qkv * 2)) return false;
         // gate/up interleaved in 16-row blocks (k_gemv ACT_SWIGLU layout)
-        std::vector<uint16_t> gate((size_t)I * H), up((size_t)I * H), gu((size_t)2 * I * H);
+        const size_t n_gu = (size_t)2 * I * H;
+        std::vector<uint16_t> gate(recv ? 0 : (size_t)I * H), up(recv ? 0 : (size_t)I * H), gu(recv ? 0 : n_gu);
         if (!rows16(nm("ffn_gate.weight"), H, I, gate, 0) || !rows16(nm("ffn_up.weight"), H, I, up, 0)) return false;
-        for (int blk = 0; blk < I / 16; ++blk) {
-            std::memcpy(gu.data() + (size_t)(blk * 32) * H, gate.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
-            std::memcpy(gu.data() + (size_t)(blk * 32 + 16) * H, up.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
-        }
-        l.gu = dalloc<uint16_t>(gu.size());
-        Q3T_HIP(hipMemcpy(l.gu, gu.data(), gu.size() * 2, hipMemcpyHostToDevice));
+        if (!recv)
+            for (int blk = 0; blk < I / 16; ++blk) {
+                std::memcpy(gu.data() + (size_t)(blk * 32) * H, gate.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
+                std::memcpy(gu.data() + (size_t)(blk * 32 + 16) * H, up.data() + (size_t)(blk * 16) * H, (size_t)16 * H * 2);
+            }
+        if (!(l.gu = wa_.alloc<uint16_t>(n_gu)) || !wa_.put(l.gu, gu.data(), n_gu * 2)) return false;
         if (!(l.o = up16(nm("attn_output.weight").c_str(), Dq, H))) return false;
         if (!(l.down = up16(nm("ffn_down.weight").c_str(), I, H))) return false;
         if (!(l.attn_norm = up32(nm("attn_norm.weight").c_str(), H))) return false;
@@ -526,8 +543,19 @@ bool Engine::prefill_embd(const int32_t *toks, int n, const float *spk, int lang
 }
 
 // ------------------------------------------------------------------------------------------ hot path
+bool Engine::copy_weights_from(Engine &src) {
+    std::vector<WeightArena *> a = weight_arenas(), b = src.weight_arenas();
+    if (a.size() != b.size()) { set_error("copy_weights_from: contexts differ in vocoder presence"); return false; }
+    for (size_t i = 0; i < a.size(); ++i) {
+        if (a[i]->used != b[i]->used) { set_error("copy_weights_from: weight blobs differ in size"); return false; }
+        Q3T_HIP(hipMemcpyPeerAsync(a[i]->base, device_, b[i]->base, src.device_, a[i]->used, stream_));
+    }
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
 bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
-                      const GenParams &gp, int32_t *codes, int *n_frames) {
+                      const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval) {
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
     const int S = n_utt, H = c_.hidden, NCB = 16;
@@ -610,10 +638,56 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) return false;
     int *done_h = nullptr;
     Q3T_HIP(hipHostMalloc(&done_h, S * 4, hipHostMallocDefault));
+    // streaming (frame callback): chunk [start, start+interval) of every slot copied to pinned memory behind the
+    // frame that completes it; delivered one chunk late so the GPU keeps running the queued frames meanwhile
+    const bool stream_cb = on_frames && interval > 0;
+    struct Chunk { int start; int32_t *codes; int *done; hipEvent_t ev; };
+    std::vector<Chunk> pend;
+    std::vector<Chunk> pool;
+    std::vector<int> delivered(S, 0), stop_at(S, -1);
+    int n_live = S;
+    auto deliver = [&](Chunk &c) -> bool {
+        Q3T_HIP(hipEventSynchronize(c.ev));
+        for (int s = 0; s < S; ++s) {
+            if (stop_at[s] >= 0) continue;
+            const int nf = c.done[s] >= 0 ? c.done[s] : gp.max_len;
+            if (nf < c.start + interval) continue;   // partial chunks go to the final flush, as in the reference
+            delivered[s] = c.start + interval;
+            if (!on_frames(user, s, c.codes + (size_t)s * interval * NCB, interval, NCB)) {
+                stop_at[s] = c.start + interval;
+                const int d = stop_at[s];
+                Q3T_HIP(hipMemcpyAsync(done_ + s, &d, 4, hipMemcpyHostToDevice, stream_));
+                Q3T_HIP(hipStreamSynchronize(stream_));   // &d is a stack value
+                --n_live;
+            }
+        }
+        pool.push_back(c);
+        return true;
+    };
     bool all_done = false;
-    for (int f = 0; f < gp.max_len && !all_done; ++f) {
+    for (int f = 0; f < gp.max_len && !all_done && n_live > 0; ++f) {
         Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
         if (dbg) { fprintf(stderr, "[q3t] frame %d launched\n", f); fflush(stderr); }
+        if (stream_cb && (f + 1) % interval == 0) {
+            Chunk c;
+            if (!pool.empty()) { c = pool.back(); pool.pop_back(); }
+            else {
+                Q3T_HIP(hipHostMalloc(&c.codes, (size_t)S * interval * NCB * 4, hipHostMallocDefault));
+                Q3T_HIP(hipHostMalloc(&c.done, S * 4, hipHostMallocDefault));
+                Q3T_HIP(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+            }
+            c.start = f + 1 - interval;
+            for (int s = 0; s < S; ++s)
+                Q3T_HIP(hipMemcpyAsync(c.codes + (size_t)s * interval * NCB, codes_ + ((size_t)s * codes_max_len_ + c.start) * NCB,
+                                       (size_t)interval * NCB * 4, hipMemcpyDeviceToHost, stream_));
+            Q3T_HIP(hipMemcpyAsync(c.done, done_, S * 4, hipMemcpyDeviceToHost, stream_));
+            Q3T_HIP(hipEventRecord(c.ev, stream_));
+            pend.push_back(c);
+            if (pend.size() > 1) {
+                if (!deliver(pend.front())) return false;
+                pend.erase(pend.begin());
+            }
+        }
         if ((f + 1) % poll_every_ == 0 && f + 1 < gp.max_len) {
             Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
             Q3T_HIP(hipStreamSynchronize(stream_));
@@ -633,6 +707,16 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     if (dbg) { fprintf(stderr, "[q3t] frame loop done\n"); fflush(stderr); }
     for (int s = 0; s < S; ++s) n_frames[s] = done_h[s] >= 0 ? std::min(done_h[s], gp.max_len) : gp.max_len;
     hipHostFree(done_h);
+    if (stream_cb) {
+        for (Chunk &c : pend) if (!deliver(c)) return false;
+        pend.clear();
+        for (int s = 0; s < S; ++s) {
+            if (stop_at[s] >= 0) { n_frames[s] = std::min(n_frames[s], stop_at[s]); continue; }
+            if (n_frames[s] > delivered[s])   // final flush (tts_transformer.cpp:2563-2570)
+                on_frames(user, s, codes + ((size_t)s * gp.max_len + delivered[s]) * NCB, n_frames[s] - delivered[s], NCB);
+        }
+        for (Chunk &c : pool) { hipHostFree(c.codes); hipHostFree(c.done); hipEventDestroy(c.ev); }
+    }
     float ms1 = 0, ms2 = 0;
     hipEventElapsedTime(&ms1, e0, e1);
     hipEventElapsedTime(&ms2, e1, e2);

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "arena.h"
 #include "gguf.h"
 #include "kernels.h"
 
@@ -44,17 +45,31 @@ class Engine {
 public:
     Engine();
     ~Engine();
-    bool load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx);
+    // recv_weights: lay out the weight arenas from the GGUF headers only; the bytes are filled afterwards by
+    // copy_weights_from() or an RCCL broadcast of weight_arenas()
+    bool load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
+              bool recv_weights = false);
+    // the packed weight blobs (talker + code predictor + embeddings; vocoder), in broadcast order
+    std::vector<WeightArena *> weight_arenas();
     const Config &cfg() const { return c_; }
     int max_slots() const { return max_slots_; }
     int device() const { return device_; }
+    const std::string &tts_path() const { return tts_path_; }
+    const std::string &tok_path() const { return tok_path_; }
     int max_ctx() const { return max_ctx_; }
     hipStream_t stream() const { return stream_; }
     Vocoder *vocoder() { return voc_.get(); }
 
     // ---- hot path: prefill + frame loop for n_utt utterances (codes [n_utt][max_len][ncb])
+    // on_frames (frame_callback_t, src/tts_transformer.h:224): called every `interval` frames per utterance with its
+    // newest `interval` frames, plus one final flush of the remainder; returning 0 stops that utterance
+    // (src/tts_transformer.cpp:2517-2523, 2563-2570)
+    typedef int (*FrameCb)(void *user, int slot, const int32_t *codes, int n_frames, int n_codebooks);
     bool generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
-                  const GenParams &gp, int32_t *codes, int *n_frames);
+                  const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames = nullptr,
+                  void *user = nullptr, int interval = 40);
+    // fill this context's weight arenas (laid out with recv_weights) from another context's, device to device
+    bool copy_weights_from(Engine &src);
 
     // ---- stage entry points (host buffers) used by the parity tests
     bool talker_forward(int S, const float *embd, const int *pos, float *hidden, float *logits);
@@ -86,9 +101,11 @@ private:
     bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
 
     Config c_;
+    std::string tts_path_, tok_path_;
     int device_ = 0, max_slots_ = 0, max_ctx_ = 0, max_trailing_ = 0;
     hipStream_t stream_ = nullptr;
     std::vector<void *> allocs_;
+    WeightArena wa_;
     template <class T> T *dalloc(size_t n);
 
     // weights

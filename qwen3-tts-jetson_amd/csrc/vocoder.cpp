@@ -26,43 +26,49 @@ namespace {
 const uint16_t *f16p(const GgufTensor *t) { return static_cast<const uint16_t *>(t->data); }
 }  // namespace
 
-bool Vocoder::load(const std::string &path, hipStream_t s) {
+bool Vocoder::load(const std::string &path, hipStream_t s, bool recv_weights) {
     stream_ = s;
     Gguf g;
     if (!g.open(path)) { set_error(g.error()); return false; }
+    wa_.recv = recv_weights;
+    const bool recv = recv_weights;   // shapes only: the tensor bytes are never read on receiving ranks
+    size_t total = 0;
+    for (const GgufTensor &t : g.tensors()) total += (t.nbytes() + 255) & ~(size_t)255;
+    if (!wa_.reserve(total + ((size_t)1 << 20))) return false;
     auto T = [&](const std::string &n) -> const GgufTensor * {
         const GgufTensor *t = g.find(n);
         if (!t) set_error("missing vocoder tensor " + n);
         return t;
     };
     auto up16 = [&](const void *src, size_t n) -> uint16_t * {
-        uint16_t *d = dalloc<uint16_t>(n);
-        if (d && hipMemcpy(d, src, n * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        uint16_t *d = wa_.alloc<uint16_t>(n);
+        if (d && !wa_.put(d, src, n * 2)) return nullptr;
         return d;
     };
-    auto up32v = [&](const std::vector<float> &v) -> float * {
-        float *d = dalloc<float>(v.size());
-        if (d && hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    auto up32n = [&](const float *src, size_t n) -> float * {
+        float *d = wa_.alloc<float>(n);
+        if (d && !wa_.put(d, src, n * 4)) return nullptr;
         return d;
     };
     auto vec = [&](const std::string &n, int64_t expect) -> float * {
         const GgufTensor *t = T(n);
         if (!t) return nullptr;
         if (t->type != GGML_TYPE_F32 || (expect > 0 && t->nelements() != expect)) { set_error("bad f32 tensor " + n); return nullptr; }
-        std::vector<float> v((const float *)t->data, (const float *)t->data + t->nelements());
-        return up32v(v);
+        return up32n((const float *)t->data, (size_t)t->nelements());
     };
     // conv weight ne [K, C_in, C_out] (PyTorch [oc][ic][k]) -> per-tap [K][C_out][C_in]
     auto conv_w = [&](const std::string &n, Conv &c) -> bool {
         const GgufTensor *t = T(n);
         if (!t || t->type != GGML_TYPE_F16 || t->n_dims != 3) { set_error("bad conv " + n); return false; }
         c.k = (int)t->ne[0]; c.ic = (int)t->ne[1]; c.oc = (int)t->ne[2];
-        std::vector<uint16_t> w((size_t)c.k * c.oc * c.ic);
+        const size_t nw = (size_t)c.k * c.oc * c.ic;
+        std::vector<uint16_t> w(recv ? 0 : nw);
         const uint16_t *src = f16p(t);
-        for (int oc = 0; oc < c.oc; ++oc)
-            for (int ic = 0; ic < c.ic; ++ic)
-                for (int k = 0; k < c.k; ++k) w[((size_t)k * c.oc + oc) * c.ic + ic] = src[((size_t)oc * c.ic + ic) * c.k + k];
-        c.w = up16(w.data(), w.size());
+        if (!recv)
+            for (int oc = 0; oc < c.oc; ++oc)
+                for (int ic = 0; ic < c.ic; ++ic)
+                    for (int k = 0; k < c.k; ++k) w[((size_t)k * c.oc + oc) * c.ic + ic] = src[((size_t)oc * c.ic + ic) * c.k + k];
+        c.w = up16(w.data(), nw);
         return c.w != nullptr;
     };
     // conv-transpose weight ne [K, C_out, C_in] (PyTorch [ic][oc][k]) -> per-tap [K][C_out][C_in]
@@ -70,12 +76,14 @@ bool Vocoder::load(const std::string &path, hipStream_t s) {
         const GgufTensor *t = T(n);
         if (!t || t->type != GGML_TYPE_F16 || t->n_dims != 3) { set_error("bad conv_t " + n); return false; }
         c.k = (int)t->ne[0]; c.oc = (int)t->ne[1]; c.ic = (int)t->ne[2];
-        std::vector<uint16_t> w((size_t)c.k * c.oc * c.ic);
+        const size_t nw = (size_t)c.k * c.oc * c.ic;
+        std::vector<uint16_t> w(recv ? 0 : nw);
         const uint16_t *src = f16p(t);
-        for (int ic = 0; ic < c.ic; ++ic)
-            for (int oc = 0; oc < c.oc; ++oc)
-                for (int k = 0; k < c.k; ++k) w[((size_t)k * c.oc + oc) * c.ic + ic] = src[((size_t)ic * c.oc + oc) * c.k + k];
-        c.w = up16(w.data(), w.size());
+        if (!recv)
+            for (int ic = 0; ic < c.ic; ++ic)
+                for (int oc = 0; oc < c.oc; ++oc)
+                    for (int k = 0; k < c.k; ++k) w[((size_t)k * c.oc + oc) * c.ic + ic] = src[((size_t)ic * c.oc + oc) * c.k + k];
+        c.w = up16(w.data(), nw);
         return c.w != nullptr;
     };
     auto mat = [&](const std::string &n, int &rows, int &cols) -> uint16_t * {
@@ -89,13 +97,15 @@ bool Vocoder::load(const std::string &path, hipStream_t s) {
     auto snake = [&](const std::string &pa, const std::string &pb, Snake &sn) -> bool {
         const GgufTensor *a = T(pa), *b = T(pb);
         if (!a || !b || a->type != GGML_TYPE_F32 || b->nelements() != a->nelements()) { set_error("bad snake " + pa); return false; }
-        std::vector<float> ea(a->nelements()), ib(a->nelements());
-        for (int64_t i = 0; i < a->nelements(); ++i) {
-            ea[i] = expf(((const float *)a->data)[i]);
-            ib[i] = expf(-((const float *)b->data)[i]);
-        }
-        sn.a = up32v(ea);
-        sn.ib = up32v(ib);
+        const size_t n = (size_t)a->nelements();
+        std::vector<float> ea(recv ? 0 : n), ib(recv ? 0 : n);
+        if (!recv)
+            for (size_t i = 0; i < n; ++i) {
+                ea[i] = expf(((const float *)a->data)[i]);
+                ib[i] = expf(-((const float *)b->data)[i]);
+            }
+        sn.a = up32n(ea.data(), n);
+        sn.ib = up32n(ib.data(), n);
         sn.n = (int)a->nelements();
         return sn.a && sn.ib;
     };
@@ -127,22 +137,26 @@ bool Vocoder::load(const std::string &path, hipStream_t s) {
         if (!g.find(p + "attn_q.weight")) break;
         Layer L;
         std::vector<uint16_t> qkv;
+        size_t n_qkv = 0;
         for (const char *nm : {"attn_q.weight", "attn_k.weight", "attn_v.weight"}) {
             const GgufTensor *t = T(p + nm);
             if (!t || t->ne[0] != hidden_ || t->ne[1] != latent_) { set_error("bad pre_tfm qkv"); return false; }
-            qkv.insert(qkv.end(), f16p(t), f16p(t) + t->nelements());
+            if (!recv) qkv.insert(qkv.end(), f16p(t), f16p(t) + t->nelements());
+            n_qkv += (size_t)t->nelements();
         }
-        L.qkv = up16(qkv.data(), qkv.size());
+        L.qkv = up16(qkv.data(), n_qkv);
         const GgufTensor *gt = T(p + "ffn_gate.weight"), *ut = T(p + "ffn_up.weight");
         if (!gt || !ut) return false;
         ffn_ = (int)gt->ne[1];
         if (ffn_ % 16) { set_error("pre_tfm ffn % 16"); return false; }
-        std::vector<uint16_t> gu((size_t)2 * ffn_ * hidden_);
-        for (int blk = 0; blk < ffn_ / 16; ++blk) {
-            std::memcpy(gu.data() + (size_t)(blk * 32) * hidden_, f16p(gt) + (size_t)(blk * 16) * hidden_, (size_t)16 * hidden_ * 2);
-            std::memcpy(gu.data() + (size_t)(blk * 32 + 16) * hidden_, f16p(ut) + (size_t)(blk * 16) * hidden_, (size_t)16 * hidden_ * 2);
-        }
-        L.gu = up16(gu.data(), gu.size());
+        const size_t n_gu = (size_t)2 * ffn_ * hidden_;
+        std::vector<uint16_t> gu(recv ? 0 : n_gu);
+        if (!recv)
+            for (int blk = 0; blk < ffn_ / 16; ++blk) {
+                std::memcpy(gu.data() + (size_t)(blk * 32) * hidden_, f16p(gt) + (size_t)(blk * 16) * hidden_, (size_t)16 * hidden_ * 2);
+                std::memcpy(gu.data() + (size_t)(blk * 32 + 16) * hidden_, f16p(ut) + (size_t)(blk * 16) * hidden_, (size_t)16 * hidden_ * 2);
+            }
+        L.gu = up16(gu.data(), n_gu);
         if (!(L.o = mat(p + "attn_output.weight", r, c))) return false;
         if (!(L.down = mat(p + "ffn_down.weight", r, c))) return false;
         if (!(L.attn_norm = vec(p + "attn_norm.weight", hidden_)) || !(L.ffn_norm = vec(p + "ffn_norm.weight", hidden_)) ||

@@ -4,6 +4,7 @@
 #include <string>
 #include <vector>
 
+#include "arena.h"
 #include "gguf.h"
 #include "kernels.h"
 
@@ -12,7 +13,8 @@ namespace q3t {
 class Vocoder {
 public:
     ~Vocoder();
-    bool load(const std::string &tok_gguf, hipStream_t s);
+    bool load(const std::string &tok_gguf, hipStream_t s, bool recv_weights = false);
+    WeightArena &weights() { return wa_; }
     // mode 0 = FULL (GGML decoder semantics), 1 = CHUNK40 (TRT streaming semantics)
     int64_t n_samples(int n_frames, int mode) const;
     bool decode(const int32_t *codes_host, int n_frames, int mode, float *pcm_host, int64_t *n_out);
@@ -47,6 +49,7 @@ private:
     bool loaded_ = false;
     hipStream_t stream_ = nullptr;
     std::vector<void *> allocs_, scratch_;
+    WeightArena wa_;   // every weight tensor (one blob)
     int cb_dim_ = 0, cb_size_ = 0, hidden_ = 0, latent_ = 0, n_heads_ = 16, head_dim_ = 64, ffn_ = 0;
     uint16_t *cb_first_ = nullptr, *cb_rest_[15] = {}, *vq_first_out_ = nullptr, *vq_rest_out_ = nullptr;
     uint16_t *in_proj_ = nullptr, *out_proj_ = nullptr;

@@ -49,6 +49,14 @@ _lib.q3t_ctx_destroy.argtypes = [_P]
 _lib.q3t_get_config.argtypes = [_P, C.POINTER(Config)]
 _lib.q3t_generate.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
                               C.POINTER(GenParams), _ip, _ip]
+FRAME_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_int32)
+_lib.q3t_generate_stream.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
+                                     C.POINTER(GenParams), _ip, _ip, FRAME_CB, C.c_void_p, C.c_int32]
+COMM_ID_BYTES = 128
+_lib.q3t_comm_unique_id.argtypes = [C.c_char_p]
+_lib.q3t_ctx_create_shared.argtypes = [C.c_char_p, C.c_char_p, _I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_P)]
+_lib.q3t_ctx_create_replica.argtypes = [_P, _I, _I, _I, C.POINTER(_P)]
+_lib.q3t_comm_allreduce_max.argtypes = [_P, np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"), _I]
 _lib.q3t_synchronize.argtypes = [_P]
 _lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
@@ -64,7 +72,8 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
-           "q3t_generate", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
+           "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -90,17 +99,47 @@ def _addr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
+def comm_unique_id():
+    """RCCL unique id (rank 0), Q3T_COMM_ID_BYTES bytes to hand to every rank of q3t_ctx_create_shared."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(_lib.q3t_comm_unique_id(buf))
+    return buf.raw
+
+
 class Engine:
     """One device context (TTSTransformer + code predictor + vocoder resident in HBM)."""
 
-    def __init__(self, tts_gguf, tokenizer_gguf=None, device=0, max_slots=1, max_ctx=4096 + 32):
-        h = _P()
-        _check(_lib.q3t_ctx_create(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
-                                   int(device), int(max_slots), int(max_ctx), C.byref(h)))
-        self.h = h
+    def __init__(self, tts_gguf=None, tokenizer_gguf=None, device=0, max_slots=1, max_ctx=4096 + 32, *, _handle=None):
+        if _handle is None:
+            h = _P()
+            _check(_lib.q3t_ctx_create(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
+                                       int(device), int(max_slots), int(max_ctx), C.byref(h)))
+            _handle = h
+        self.h = _handle
         c = Config()
         _check(_lib.q3t_get_config(self.h, C.byref(c)))
         self.cfg = {n: getattr(c, n) for n, _ in Config._fields_}
+
+    @classmethod
+    def shared(cls, tts_gguf, tokenizer_gguf, device, max_slots, max_ctx, rank, world, uid):
+        """One rank of a multi-GPU job: rank 0 reads the weights, RCCL broadcasts them to the others."""
+        assert len(uid) == COMM_ID_BYTES
+        h = _P()
+        _check(_lib.q3t_ctx_create_shared(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
+                                          int(device), int(max_slots), int(max_ctx), int(rank), int(world), uid,
+                                          C.byref(h)))
+        return cls(_handle=h)
+
+    def replica(self, device=0, max_slots=1, max_ctx=4096 + 32):
+        """A second context whose weights are copied device-to-device from this one (no file reads)."""
+        h = _P()
+        _check(_lib.q3t_ctx_create_replica(self.h, int(device), int(max_slots), int(max_ctx), C.byref(h)))
+        return Engine(_handle=h)
+
+    def allreduce_max(self, values):
+        v = np.ascontiguousarray(values, np.float64).copy()
+        _check(_lib.q3t_comm_allreduce_max(self.h, v, len(v)))
+        return v
 
     def close(self):
         if getattr(self, "h", None):
@@ -131,6 +170,38 @@ class Engine:
         nf = np.zeros(n, np.int32)
         _check(_lib.q3t_generate(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf))
         del keep
+        return [codes[i, :nf[i]].copy() for i in range(n)]
+
+    def generate_stream(self, prompts, on_frames, interval=40, speakers=None, **params):
+        """generate() with the reference's frame callback: on_frames(utt, codes [n][16]) -> bool, every `interval`
+        frames plus a final flush; returning False stops that utterance.  Returns the codes like generate()."""
+        p = default_params(**params)
+        n = len(prompts)
+        toks = [np.ascontiguousarray(t, np.int32) for t in prompts]
+        tarr = (C.POINTER(C.c_int32) * n)(*[t.ctypes.data_as(C.POINTER(C.c_int32)) for t in toks])
+        ntok = np.array([len(t) for t in toks], np.int32)
+        sarr = None
+        sp = []
+        if speakers is not None:
+            sp = [np.ascontiguousarray(s, np.float32) for s in speakers]
+            sarr = (C.POINTER(C.c_float) * n)(*[s.ctypes.data_as(C.POINTER(C.c_float)) for s in sp])
+        codes = np.zeros((n, p.max_len, 16), np.int32)
+        nf = np.zeros(n, np.int32)
+        errors = []
+
+        def _cb(_user, utt, ptr, nfr, ncb):
+            try:
+                arr = np.ctypeslib.as_array(ptr, shape=(nfr * ncb,)).reshape(nfr, ncb).copy()
+                return 1 if on_frames(int(utt), arr) is not False else 0
+            except Exception as e:  # never let an exception unwind through the C frames
+                errors.append(e)
+                return 0
+
+        cb = FRAME_CB(_cb)
+        _check(_lib.q3t_generate_stream(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf, cb, None, int(interval)))
+        del sp
+        if errors:
+            raise errors[0]
         return [codes[i, :nf[i]].copy() for i in range(n)]
 
     def synchronize(self):
