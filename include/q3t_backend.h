@@ -91,6 +91,10 @@ typedef int (*q3t_frame_cb)(void *user, int32_t utterance, const int32_t *codes,
 int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                         const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
                         q3t_frame_cb on_frames, void *user, int32_t interval);
+/* tuning knob (process-wide): batches of >= min_batch slots run the projections on the matrix cores (MFMA GEMM,
+ * gemm_mfma.hip) instead of the weight-streaming GEMV; 0 disables the matrix-core path.  Default 4 (env
+ * Q3T_MFMA_MIN_B).  Applies to graphs captured afterwards (create contexts after changing it). */
+int q3t_set_mfma_min_batch(int min_batch);
 /* wait until every operation queued on the context's device has finished (hipDeviceSynchronize) */
 int q3t_synchronize(q3t_ctx *ctx);
 /* device time (ms) of the last q3t_generate: prefill and frame loop */

@@ -119,6 +119,11 @@ int q3t_comm_allreduce_max(q3t_ctx *ctx, double *values, int n) {
 
 void q3t_ctx_destroy(q3t_ctx *ctx) { delete ctx; }
 
+int q3t_set_mfma_min_batch(int min_batch) {
+    q3t::gemm_mfma_set_min_batch(min_batch);
+    return Q3T_OK;
+}
+
 int q3t_get_config(const q3t_ctx *ctx, q3t_config *o) {
     CHECK_CTX(ctx);
     if (!o) { q3t::set_error("null argument"); return Q3T_ERR; }

@@ -285,13 +285,20 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
                           int max_splits, const int *pos, const float *rope, float *part, unsigned *ticket,
                           hipStream_t s, const StackInput *in0 = nullptr, bool fused_cp_attn = false) {
     const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
+    // batched (matrix-core) path: gathers become their own launch and the code predictor's attention runs unfused
+    const bool mm = S >= gemm_mfma_min_batch();
+    if (mm) fused_cp_attn = false;
     for (size_t il = 0; il < layers.size(); ++il) {
         const DevLayer &l = layers[il];
         GemvParams g;
         g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
         g.pro = PRO_RMS; g.x = x; g.ldx = H; g.nw = l.attn_norm; g.eps = c.eps;
         if (il == 0 && in0) {
-            g.pro = in0->pro; g.x = in0->x; g.gs = in0->gs; g.raw_out = x;
+            if (mm && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
+                if (!gather_sum(in0->gs, in0->pro == PRO_RMS_G16 ? 16 : 1, S, H, x, H, s)) return false;
+            } else {
+                g.pro = in0->pro; g.x = in0->x; g.gs = in0->gs; g.raw_out = x;
+            }
         }
         g.out_f32 = qkv; g.ldo = QKV;
         if (!gemv(g, s)) return false;
@@ -364,8 +371,11 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
     h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = S;
     h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_;
     h.out_f32 = logits_; h.ldo = c_.codec_vocab;
-    if (select_next) h.sel = select_spec(SEL_CB0, gp_, 1, 0);
-    return gemv(h, s);
+    const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
+    if (select_next && !mm) h.sel = select_spec(SEL_CB0, gp_, 1, 0);
+    if (!gemv(h, s)) return false;
+    if (select_next && mm) return select_tokens(select_spec(SEL_CB0, gp_, 1, 0), logits_, S, s);
+    return true;
 }
 
 // 16 passes of the 5-layer code predictor, token chosen on device each pass (trt_code_predictor.cpp:484-600).
@@ -394,7 +404,8 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
         h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
-        if (fused_select_) h.sel = select_spec(SEL_CP, gp_, 0, step);
+        const bool fsel = fused_select_ && S < gemm_mfma_min_batch();
+        if (fsel) h.sel = select_spec(SEL_CP, gp_, 0, step);
         if (!gemv(h, s)) return false;
         if (logits_host) {
             lg.resize((size_t)S * c_.cp_vocab);
@@ -403,7 +414,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
             for (int b = 0; b < S; ++b)
                 std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
         }
-        if (!fused_select_ && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
+        if (!fsel && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
     }
     return true;
 }

@@ -1,0 +1,391 @@
+// gemm_mfma.hip — batched decode projections on the gfx950 matrix cores (B >= Q3T_MFMA_MIN_B tokens).
+//
+// Y[b][n] = epilogue( W[n][:] . f16(prologue(X[b][:])) ) for up to 64 tokens per workgroup, W f16 [N][K] row-major
+// exactly as in the GGUF.  The same GemvParams as the weight-streaming GEMV (gemv.hip); gemv() routes here when the
+// batch is wide enough that the vector path's per-token FMAs and per-tile weight re-reads dominate (SURVEY §8(d):
+// B = 64 concurrent utterances, BASELINE configs[2]).
+//
+// Tiling (one workgroup per 32 weight rows x 64 tokens, 4 waves = 4 K-quarters):
+//   - v_mfma_f32_32x32x16_f16, A = the weight tile (32 rows), B = the activation tile (32 tokens), one or two token
+//     tiles sharing every A fragment.  f16 x f16 products are exact and accumulate in f32: the numerics of the
+//     vector path (and of ggml's f16 vec_dot) up to summation order.
+//   - K permutation: lane (r, h) loads 64 contiguous bytes (32 halves) of row r per 64-wide K chunk and feeds
+//     halves [8j, 8j+8) to k-step j.  A dot product may visit K in any order as long as both operands use the same
+//     bijection, so A and B fragments are both plain 64-B row segments: full 128-B lines per lane pair, no shuffles.
+//   - Every weight load of the lane (the HBM stream) is issued first, straight-line.
+//   - Prologues: PRO_F16 reads f16 activation rows (optional row gather x_idx) from global memory in the same
+//     fragment shape, issued a few chunks ahead; PRO_F32 / PRO_RMS / PRO_LN build the f16 activation tile in LDS
+//     (norm sums in double, like gemv.hip), row stride K + 8 halves so ds_read_b128 is conflict-free.
+//   - The 4 K-quarter partial tiles are summed through LDS; each wave then runs the epilogue of a quarter of the
+//     tile (bias, activation, scale, residual, aux, SwiGLU pairs, f16/f32 stores of 4 consecutive rows).
+#include "kernels.h"
+
+#include <cstdlib>
+
+namespace q3t {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_g __attribute__((ext_vector_type(4)));
+typedef float f32x4_g __attribute__((ext_vector_type(4)));
+
+namespace {
+template <class V>
+__device__ __forceinline__ V gld(const void *p) {
+    typedef const __attribute__((address_space(1))) V gV;
+    return *(gV *)(p);
+}
+__device__ __forceinline__ uint4 gld16(const void *p) {
+    const u32x4_g v = gld<u32x4_g>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 gldf4(const void *p) {
+    const f32x4_g v = gld<f32x4_g>(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ half8_t as_h8(const uint4 &u) { return __builtin_bit_cast(half8_t, u); }
+}  // namespace
+
+constexpr int MM_ROWS = 32, MM_TOK = 64, MM_XD = 3;   // weight rows / tokens per workgroup, F16 prefetch depth
+
+template <int PRO, int NCH, int TT, bool SWIGLU>
+__global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr bool kLds = PRO != PRO_F16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int K = NCH * 256, N = p.N;
+    const int row0 = blockIdx.x * MM_ROWS;
+    const int t0 = blockIdx.y * MM_TOK;
+    const int nt = min(MM_TOK, p.B - t0);
+    const int kw0 = wave * (NCH * 64);   // first K index of this wave's quarter
+
+    // ---------------- (1) every weight load of the lane: row row0 + r, k = kw0 + 64c + 32h .. +31
+    uint4 wr[NCH][4];
+    {
+        const uint16_t *wp = p.W + (size_t)(row0 + r) * K + kw0 + h * 32;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wr[c][j] = gld16(wp + c * 64 + j * 8);
+    }
+
+    f32x16_t acc[TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[tt][i] = 0.0f;
+
+    if constexpr (kLds) {
+        // ---------------- (2a) activation tile in LDS: 16 tokens per wave, f16 rows of K + 8 halves
+        constexpr int KP = NCH * 256 + 8;
+        uint16_t *xs = reinterpret_cast<uint16_t *>(smem);
+        const float *X = reinterpret_cast<const float *>(p.x);
+        float4 nwv[NCH], nbv[NCH];
+        if constexpr (PRO == PRO_RMS || PRO == PRO_LN) {
+#pragma unroll
+            for (int it = 0; it < NCH; ++it) {
+                nwv[it] = gldf4(p.nw + it * 256 + lane * 4);
+                nbv[it] = PRO == PRO_LN ? gldf4(p.nb + it * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float4 xv[4][NCH];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int tl = wave * 16 + g * 4 + q;
+                const int src = t0 + min(tl, nt - 1);
+                const float *row = X + (size_t)src * p.ldx;
+#pragma unroll
+                for (int it = 0; it < NCH; ++it) xv[q][it] = gldf4(row + it * 256 + lane * 4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int tl = wave * 16 + g * 4 + q;
+                const bool valid = tl < nt;
+                float scale = 1.0f, mean = 0.0f;
+                if constexpr (PRO == PRO_RMS) {
+                    double ss = 0.0;
+#pragma unroll
+                    for (int it = 0; it < NCH; ++it) {
+                        const float4 v = xv[q][it];
+                        ss += (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z) + (double)(v.w * v.w);
+                    }
+                    ss = wave_sum_d(ss);
+                    scale = 1.0f / sqrtf((float)(ss / K) + p.eps);
+                } else if constexpr (PRO == PRO_LN) {
+                    double s1 = 0.0;
+#pragma unroll
+                    for (int it = 0; it < NCH; ++it) {
+                        const float4 v = xv[q][it];
+                        s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+                    }
+                    s1 = wave_sum_d(s1);
+                    mean = (float)(s1 / K);
+                    double s2 = 0.0;
+#pragma unroll
+                    for (int it = 0; it < NCH; ++it) {
+                        const float4 v = xv[q][it];
+                        const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+                        s2 += (double)(dx * dx) + (double)(dy * dy) + (double)(dz * dz) + (double)(dw * dw);
+                    }
+                    s2 = wave_sum_d(s2);
+                    scale = 1.0f / sqrtf((float)(s2 / K) + p.eps);
+                }
+                const bool side = valid && blockIdx.x == 0;
+#pragma unroll
+                for (int it = 0; it < NCH; ++it) {
+                    const int k = it * 256 + lane * 4;
+                    const float4 v = xv[q][it];
+                    float y[4] = {v.x, v.y, v.z, v.w};
+                    if constexpr (PRO == PRO_RMS || PRO == PRO_LN) {
+                        const float w4[4] = {nwv[it].x, nwv[it].y, nwv[it].z, nwv[it].w};
+                        const float c4[4] = {nbv[it].x, nbv[it].y, nbv[it].z, nbv[it].w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            if constexpr (PRO == PRO_RMS) y[e] = (y[e] * scale) * w4[e];
+                            else y[e] = ((y[e] - mean) * scale) * w4[e] + c4[e];
+                        }
+                    }
+                    if (side && p.raw_out) *reinterpret_cast<float4 *>(p.raw_out + (size_t)(t0 + tl) * K + k) = v;
+                    if (side && p.side_out)
+                        *reinterpret_cast<float4 *>(p.side_out + (size_t)(t0 + tl) * K + k) = make_float4(y[0], y[1], y[2], y[3]);
+                    uint2 hv;
+                    hv.x = valid ? ((uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16)) : 0u;
+                    hv.y = valid ? ((uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16)) : 0u;
+                    *reinterpret_cast<uint2 *>(xs + (size_t)tl * KP + k) = hv;
+                }
+            }
+        }
+        __syncthreads();
+        // ---------------- (3a) MFMA over the wave's K quarter, B fragments from LDS
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const half8_t a = as_h8(wr[c][j]);
+#pragma unroll
+                for (int tt = 0; tt < TT; ++tt) {
+                    const half8_t b = *reinterpret_cast<const half8_t *>(xs + (size_t)(tt * 32 + r) * KP + kw0 + c * 64 + h * 32 + j * 8);
+                    acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[tt], 0, 0, 0);
+                }
+            }
+        __syncthreads();   // the reduction below reuses the LDS tile
+    } else {
+        // ---------------- (2b)+(3b) f16 activation rows from global memory in fragment shape, MM_XD chunks ahead
+        const uint16_t *xrow[TT];
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) {
+            const int tok = t0 + min(tt * 32 + r, nt - 1);
+            const int src = p.x_idx ? p.x_idx[tok] : tok;
+            xrow[tt] = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src * p.ldx + kw0 + h * 32;
+        }
+        uint4 xr[NCH][TT][4];
+#pragma unroll
+        for (int c = 0; c < NCH && c < MM_XD; ++c)
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) xr[c][tt][j] = gld16(xrow[tt] + c * 64 + j * 8);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c + MM_XD < NCH)
+#pragma unroll
+                for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) xr[c + MM_XD][tt][j] = gld16(xrow[tt] + (c + MM_XD) * 64 + j * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const half8_t a = as_h8(wr[c][j]);
+#pragma unroll
+                for (int tt = 0; tt < TT; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, as_h8(xr[c][tt][j]), acc[tt], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---------------- (4) sum the 4 K-quarters through LDS: red[wave][tt][reg][lane]
+    float *red = reinterpret_cast<float *>(smem);
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[((wave * TT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
+    __syncthreads();
+
+    // ---------------- (5) epilogue.  acc register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r.
+    auto sum4 = [&](int tt, int i) {
+        float v = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v += red[((w * TT + tt) * 16 + i) * 64 + lane];
+        return v;
+    };
+    const bool vec_ok = (p.ldo & 3) == 0;
+    if constexpr (SWIGLU) {
+        // combos (tt, q), q in {0, 1}: gate registers 4q..4q+3, up registers 4(q+2)..: unit = row0/2 + 8q + 4h + e
+        if (wave < TT * 2) {
+            const int tt = wave >> 1, q = wave & 1;
+            const int tl = tt * 32 + r;
+            if (tl < nt) {
+                const int tok = t0 + tl;
+                const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
+                const int unit = row0 / 2 + 8 * q + 4 * h;
+                float hv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4(tt, 4 * q + e)) * sum4(tt, 4 * (q + 2) + e);
+                if (p.out_f16) {
+                    if (vec_ok) {
+                        uint2 o;
+                        o.x = (uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16);
+                        o.y = (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16);
+                        *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + unit) = o;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + unit + e] = f2h(hv[e]);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + unit + e] = hv[e];
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const int combo = wave + 4 * cc;
+            if (combo >= TT * 4) break;
+            const int tt = combo >> 2, q = combo & 3;
+            const int tl = tt * 32 + r;
+            if (tl >= nt) continue;
+            const int tok = t0 + tl;
+            const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
+            const int n0 = row0 + 8 * q + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = sum4(tt, 4 * q + e);
+            // epilogue operands: 4 consecutive rows
+            float bb[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {1.f, 1.f, 1.f, 1.f}, rs[4] = {0.f, 0.f, 0.f, 0.f}, ax[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (p.bias) bb[e] = p.bias[n0 + e];
+                if (p.scale) sc[e] = p.scale[n0 + e];
+                if (p.resid) rs[e] = p.resid[(size_t)tok * p.ldr + n0 + e];
+                if (p.aux) ax[e] = p.aux[(size_t)tok * p.lda + n0 + e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = v[e];
+                if (p.bias) x += bb[e];
+                if (p.act == ACT_SILU) x = silu_f(x);
+                else if (p.act == ACT_GELU) x = gelu_ggml(x);
+                if (p.scale) x *= sc[e];
+                if (p.resid) x = rs[e] + x;
+                if (p.aux) x = ax[e] + x;
+                v[e] = x;
+            }
+            if (p.out_f16) {
+                if (vec_ok) {
+                    uint2 o;
+                    o.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
+                    o.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
+                    *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + n0) = o;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + n0 + e] = f2h(v[e]);
+                }
+            } else if (vec_ok) {
+                *reinterpret_cast<float4 *>(p.out_f32 + orow * p.ldo + n0) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + n0 + e] = v[e];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------ host dispatch
+static int g_mfma_min_b = [] {
+    const char *e = std::getenv("Q3T_MFMA_MIN_B");
+    return e ? std::atoi(e) : 4;
+}();
+int gemm_mfma_min_batch() { return g_mfma_min_b <= 0 ? (1 << 30) : g_mfma_min_b; }
+void gemm_mfma_set_min_batch(int b) { g_mfma_min_b = b; }
+
+static int nch_of(int K) {
+    switch (K) {
+        case 256: return 1;
+        case 512: return 2;
+        case 1024: return 4;
+        case 2048: return 8;
+        case 3072: return 12;
+        default: return 0;
+    }
+}
+
+bool gemm_mfma_supported(const GemvParams &p) {
+    if (p.B < gemm_mfma_min_batch() || p.sel.mode != SEL_NONE || p.N % MM_ROWS != 0) return false;
+    const int nch = nch_of(p.K);
+    if (!nch) return false;
+    const bool swiglu = p.act == ACT_SWIGLU;
+    if (swiglu && p.pro != PRO_RMS) return false;
+    const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x);
+    switch (p.pro) {
+        case PRO_F16: return (xa & 15) == 0 && p.ldx % 8 == 0;
+        case PRO_F32: case PRO_RMS: case PRO_LN:
+            return nch <= 4 && (xa & 15) == 0 && p.ldx % 4 == 0 && !p.x_idx;
+        default: return false;   // gather / fused-attention prologues stay on the vector path
+    }
+}
+
+template <int PRO, int NCH, int TT, bool SW>
+static bool launch_mm(const GemvParams &p, hipStream_t s) {
+    constexpr bool kLds = PRO != PRO_F16;
+    const size_t red = (size_t)4 * TT * 16 * 64 * 4;
+    const size_t xt = kLds ? (size_t)MM_TOK * (NCH * 256 + 8) * 2 : 0;
+    const size_t lds = xt > red ? xt : red;
+    static bool attr = false;
+    if (!attr) {
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_gemm_mfma<PRO, NCH, TT, SW>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK));
+    hipLaunchKernelGGL((k_gemm_mfma<PRO, NCH, TT, SW>), grid, dim3(256), lds, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+template <int PRO, int NCH, int TT>
+static bool launch_sw(const GemvParams &p, hipStream_t s) {
+    if constexpr (PRO == PRO_RMS) {
+        if (p.act == ACT_SWIGLU) return launch_mm<PRO, NCH, TT, true>(p, s);
+    }
+    return launch_mm<PRO, NCH, TT, false>(p, s);
+}
+template <int PRO, int NCH>
+static bool launch_tt(const GemvParams &p, hipStream_t s) {
+    return p.B > 32 ? launch_sw<PRO, NCH, 2>(p, s) : launch_sw<PRO, NCH, 1>(p, s);
+}
+template <int PRO>
+static bool launch_lds_nch(const GemvParams &p, hipStream_t s) {
+    switch (nch_of(p.K)) {
+        case 1: return launch_tt<PRO, 1>(p, s);
+        case 2: return launch_tt<PRO, 2>(p, s);
+        default: return launch_tt<PRO, 4>(p, s);
+    }
+}
+
+bool gemm_mfma(const GemvParams &p, hipStream_t s) {
+    switch (p.pro) {
+        case PRO_F16:
+            switch (nch_of(p.K)) {
+                case 1: return launch_tt<PRO_F16, 1>(p, s);
+                case 2: return launch_tt<PRO_F16, 2>(p, s);
+                case 4: return launch_tt<PRO_F16, 4>(p, s);
+                case 8: return launch_tt<PRO_F16, 8>(p, s);
+                default: return launch_tt<PRO_F16, 12>(p, s);
+            }
+        case PRO_F32: return launch_lds_nch<PRO_F32>(p, s);
+        case PRO_RMS: return launch_lds_nch<PRO_RMS>(p, s);
+        default: return launch_lds_nch<PRO_LN>(p, s);
+    }
+}
+
+}  // namespace q3t

@@ -57,6 +57,9 @@ struct GatherSum {
     const float *pad = nullptr;            // [B][K]
 };
 
+// the GatherSum rows as a plain f32 buffer out[b][0..K) (nt = 1 or 16 table rows; batched path)
+bool gather_sum(const GatherSum &gs, int nt, int S, int K, float *out, int ldo, hipStream_t s);
+
 // PRO_CPATT source: one new token per slot at position pos[b] (< 16) over a 16-position F16 cache
 // (scripts/export_code_predictor.py:132-231 step semantics; 16 q heads / 8 kv heads / D 128 only)
 struct CpAttnSrc {
@@ -95,7 +98,13 @@ struct GemvParams {
     int ldo = 0;
     int orow_mul = 1, orow_add = 0;  // output row of batch b = b*orow_mul + orow_add
 };
-bool gemv(const GemvParams &p, hipStream_t s);
+bool gemv(const GemvParams &p, hipStream_t s);   // routes wide batches to gemm_mfma (gemm_mfma.hip)
+// matrix-core path for B >= gemm_mfma_min_batch() tokens (Q3T_MFMA_MIN_B, default 4; 0 = off): F16 / F32 / RMS / LN
+// prologues, K in {256, 512, 1024, 2048, 3072} (norm prologues K <= 1024), N % 32 == 0, no fused selection
+bool gemm_mfma_supported(const GemvParams &p);
+bool gemm_mfma(const GemvParams &p, hipStream_t s);
+int gemm_mfma_min_batch();
+void gemm_mfma_set_min_batch(int b);
 void gemv_set_min_blocks(int n);   // tuning hook (tools/dev/kbench)
 
 // Qwen3 attention for one new token per slot (talker decode / unfused code-predictor pass), fused with q/k head

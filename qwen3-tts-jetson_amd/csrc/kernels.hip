@@ -23,6 +23,48 @@ bool select_tokens(const SelectSpec &sp, const float *logits, int S, hipStream_t
     return true;
 }
 
+// GatherSum rows materialised (batched path: the matrix-core GEMM has no gather prologue).  Same order of the f32
+// sums as gemv.hip's issue_x_gather, so both paths see bit-identical activation rows.
+template <int NT>
+__global__ void __launch_bounds__(256) k_gather_sum(const GatherSum gs, int K, float *out, int ldo) {
+    const int b = blockIdx.x, k = threadIdx.x * 4;
+    if (k >= K) return;
+    const uint16_t *row[NT];
+    const float *extra = nullptr;
+    if constexpr (NT == 1) {
+        row[0] = gs.tab0 + (size_t)gs.tok[(size_t)b * gs.tok_ld + gs.tok_col0] * K;
+    } else {
+        const int *tk = gs.tok + (size_t)b * gs.tok_ld;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) row[j] = gs.tabs[j] + (size_t)tk[j] * K;
+        const int fr = gs.frame[b];
+        extra = fr < gs.tr_len[b] ? gs.tr + (size_t)b * gs.tr_ld + (size_t)fr * K : gs.pad + (size_t)b * K;
+    }
+    float a[4];
+    {
+        const uint2 u = *reinterpret_cast<const uint2 *>(row[0] + k);
+        a[0] = h2f(u.x & 0xffff); a[1] = h2f(u.x >> 16); a[2] = h2f(u.y & 0xffff); a[3] = h2f(u.y >> 16);
+    }
+#pragma unroll
+    for (int j = 1; j < NT; ++j) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(row[j] + k);
+        a[0] += h2f(u.x & 0xffff); a[1] += h2f(u.x >> 16); a[2] += h2f(u.y & 0xffff); a[3] += h2f(u.y >> 16);
+    }
+    if constexpr (NT > 1) {
+        const float4 e = *reinterpret_cast<const float4 *>(extra + k);
+        a[0] += e.x; a[1] += e.y; a[2] += e.z; a[3] += e.w;
+    }
+    *reinterpret_cast<float4 *>(out + (size_t)b * ldo + k) = make_float4(a[0], a[1], a[2], a[3]);
+}
+bool gather_sum(const GatherSum &gs, int nt, int S, int K, float *out, int ldo, hipStream_t s) {
+    if (K > 1024 || K % 4 != 0 || (nt != 1 && nt != 16)) { set_error("gather_sum: unsupported shape"); return false; }
+    if (S <= 0) return true;
+    if (nt == 1) hipLaunchKernelGGL(k_gather_sum<1>, dim3(S), dim3(256), 0, s, gs, K, out, ldo);
+    else hipLaunchKernelGGL(k_gather_sum<16>, dim3(S), dim3(256), 0, s, gs, K, out, ldo);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 __global__ void k_advance(int *pos, int *frame, int S) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < S) { pos[s] += 1; frame[s] += 1; }

@@ -57,6 +57,7 @@ _lib.q3t_comm_unique_id.argtypes = [C.c_char_p]
 _lib.q3t_ctx_create_shared.argtypes = [C.c_char_p, C.c_char_p, _I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_P)]
 _lib.q3t_ctx_create_replica.argtypes = [_P, _I, _I, _I, C.POINTER(_P)]
 _lib.q3t_comm_allreduce_max.argtypes = [_P, np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"), _I]
+_lib.q3t_set_mfma_min_batch.argtypes = [_I]
 _lib.q3t_synchronize.argtypes = [_P]
 _lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
@@ -73,7 +74,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -97,6 +98,11 @@ def default_params(**kw):
 
 def _addr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def set_mfma_min_batch(b):
+    """Process-wide: batches of >= b slots use the matrix-core GEMM (0 = never).  Affects contexts created later."""
+    _check(_lib.q3t_set_mfma_min_batch(int(b)))
 
 
 def comm_unique_id():

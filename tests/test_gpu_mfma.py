@@ -1,0 +1,102 @@
+"""GPU parity of the batched matrix-core path (gemm_mfma.hip) against the CPU oracle and the vector path.
+
+q3t_set_mfma_min_batch(1) routes every projection with a supported shape (F16 / F32 / RMS / LN prologues, K in
+{256, 512, 1024, 2048, 3072}, N % 32 == 0) through v_mfma_f32_32x32x16_f16, even for one slot, so the same stage
+tests as tests/test_gpu_parity.py run on it.  The matrix cores multiply the same f16-rounded activations by the same
+f16 weights with f32 accumulation; only the summation order differs from the vector path and from ggml, so the
+tolerances are those of test_gpu_parity.py (see its header for why they are relative-max-abs and teacher-forced).
+Batched runs cover one and two 32-token tiles per workgroup (B <= 32, B = 64) and several token blocks per launch
+(the prefill text projection of 64 utterances: ~900 rows).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from q3t_testutil import REPO, check_decisions, check_token, prompt, rel_err, synth_dir
+
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+
+pytestmark = pytest.mark.gpu
+TOL = {"tiny": 3e-3, "full": 5e-3}
+LOGIT_TOL = {"tiny": 5e-2, "full": 8e-2}
+
+
+@pytest.fixture(scope="module", params=["tiny", "full"])
+def mm(request):
+    import q3t
+    cfg = request.param
+    tts, tok = synth_dir(cfg)
+    q3t.set_mfma_min_batch(1)
+    try:
+        eng = q3t.Engine(tts, tok, device=0, max_slots=64, max_ctx=96)
+    finally:
+        q3t.set_mfma_min_batch(4)
+    q3t.set_mfma_min_batch(0)
+    try:
+        vec = q3t.Engine(tts, None, device=0, max_slots=2, max_ctx=96)
+    finally:
+        q3t.set_mfma_min_batch(4)
+    orc = Oracle(tts, tok)
+    yield cfg, eng, vec, orc
+    eng.close()
+    vec.close()
+    orc.close()
+
+
+def test_mfma_talker_step_matches_oracle_and_vector_path(mm):
+    cfg, eng, vec, orc = mm
+    H = eng.cfg["hidden"]
+    rng = np.random.default_rng(31)
+    kv = orc.kv_new(96, 0)
+    for pos in range(12):
+        e = (rng.standard_normal(H) * 0.5).astype(np.float32)
+        hg, lg = eng.talker_forward(e[None], [pos])
+        hv, lv = vec.talker_forward(e[None], [pos])
+        ho, lo = orc.talker_step(kv, e, pos)
+        assert rel_err(hg[0], ho) < TOL[cfg], pos
+        assert rel_err(lg[0], lo) < TOL[cfg], pos
+        assert rel_err(hg[0], hv[0]) < TOL[cfg], pos
+    orc.kv_free(kv)
+
+
+def test_mfma_codepred_greedy_matches_oracle(mm):
+    cfg, eng, vec, orc = mm
+    H = eng.cfg["hidden"]
+    rng = np.random.default_rng(7)
+    hid = rng.standard_normal((5, H)).astype(np.float32)
+    cb0 = np.array([1, 77, 2047, 300, 5], np.int32)
+    codes, lg = eng.codepred_frame(hid, cb0, temperature=0.0, want_logits=True)
+    off = 0
+    for s in range(5):
+        ol = orc.cp_frame_forced(hid[s], int(cb0[s]), codes[s])
+        assert np.abs(lg[s] - ol).max() < LOGIT_TOL[cfg]
+        off += sum(check_token(ol[i], int(codes[s, i]), 0.0, 0, 0.0) for i in range(15))
+    assert off <= 3, off
+
+
+def test_mfma_project_text_matches_oracle(mm):
+    cfg, eng, vec, orc = mm
+    toks = prompt(cfg)
+    assert rel_err(eng.project_text(toks), orc.project_text(toks)) < TOL[cfg]
+
+
+@pytest.mark.parametrize("n_utt", [8, 64])
+def test_mfma_generate_batched_matches_oracle(mm, n_utt):
+    cfg, eng, vec, orc = mm
+    H = eng.cfg["hidden"]
+    base = prompt(cfg)
+    prompts = [base[:4] + [(t + 13 * i) % 900 + 20 for t in base[4:]] for i in range(n_utt)]
+    spk = [np.zeros(H, np.float32)] * n_utt
+    nf = 8
+    outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.0, force_frames=nf)
+    assert all(o.shape == (nf, 16) for o in outs)
+    for i in sorted({0, n_utt // 2, n_utt - 1}):
+        check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf)
+    # sampling: per-slot counter-based RNG, decisions teacher-forced against the oracle
+    outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.9, top_k=50, seed=99, force_frames=nf)
+    for i in sorted({1, n_utt - 2}):
+        check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf, temperature=0.9, top_k=50,
+                        seed=99, utt=i)
