@@ -46,7 +46,91 @@ __device__ __forceinline__ float4 gldf4(const void *p) {
 __device__ __forceinline__ half8_t as_h8(const uint4 &u) { return __builtin_bit_cast(half8_t, u); }
 }  // namespace
 
-constexpr int MM_ROWS = 32, MM_TOK = 64, MM_XD = 3;   // weight rows / tokens per workgroup, F16 prefetch depth
+constexpr int MM_ROWS = 32, MM_TOK = 64;   // weight rows / tokens per workgroup
+
+// epilogue shared by the kernels: acc register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r;
+// sumf(tt, i) returns the K-summed value of register i of token tile tt for this lane
+template <bool SWIGLU, int TT, class SumF>
+__device__ __forceinline__ void mm_epilogue(const GemvParams &p, int wave, int lane, int r, int h, int row0, int t0,
+                                            int nt, SumF sumf) {
+    const bool vec_ok = (p.ldo & 3) == 0;
+    if constexpr (SWIGLU) {
+        // combos (tt, q), q in {0, 1}: gate registers 4q..4q+3, up registers 4(q+2)..: unit = row0/2 + 8q + 4h + e
+        if (wave < TT * 2) {
+            const int tt = wave >> 1, q = wave & 1;
+            const int tl = tt * 32 + r;
+            if (tl < nt) {
+                const int tok = t0 + tl;
+                const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
+                const int unit = row0 / 2 + 8 * q + 4 * h;
+                float hv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[e] = silu_f(sumf(tt, 4 * q + e)) * sumf(tt, 4 * (q + 2) + e);
+                if (p.out_f16) {
+                    if (vec_ok) {
+                        uint2 o;
+                        o.x = (uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16);
+                        o.y = (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16);
+                        *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + unit) = o;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + unit + e] = f2h(hv[e]);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + unit + e] = hv[e];
+                }
+            }
+        }
+    } else {
+        for (int combo = wave; combo < TT * 4; combo += (int)(blockDim.x >> 6)) {
+            const int tt = combo >> 2, q = combo & 3;
+            const int tl = tt * 32 + r;
+            if (tl >= nt) continue;
+            const int tok = t0 + tl;
+            const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
+            const int n0 = row0 + 8 * q + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = sumf(tt, 4 * q + e);
+            float bb[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {1.f, 1.f, 1.f, 1.f}, rs[4] = {0.f, 0.f, 0.f, 0.f}, ax[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (p.bias) bb[e] = p.bias[n0 + e];
+                if (p.scale) sc[e] = p.scale[n0 + e];
+                if (p.resid) rs[e] = p.resid[(size_t)tok * p.ldr + n0 + e];
+                if (p.aux) ax[e] = p.aux[(size_t)tok * p.lda + n0 + e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = v[e];
+                if (p.bias) x += bb[e];
+                if (p.act == ACT_SILU) x = silu_f(x);
+                else if (p.act == ACT_GELU) x = gelu_ggml(x);
+                if (p.scale) x *= sc[e];
+                if (p.resid) x = rs[e] + x;
+                if (p.aux) x = ax[e] + x;
+                v[e] = x;
+            }
+            if (p.out_f16) {
+                if (vec_ok) {
+                    uint2 o;
+                    o.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
+                    o.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
+                    *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + n0) = o;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + n0 + e] = f2h(v[e]);
+                }
+            } else if (vec_ok) {
+                *reinterpret_cast<float4 *>(p.out_f32 + orow * p.ldo + n0) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + n0 + e] = v[e];
+            }
+        }
+    }
+}
 
 template <int PRO, int NCH, int TT, bool SWIGLU>
 __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
@@ -59,15 +143,17 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
     const int nt = min(MM_TOK, p.B - t0);
     const int kw0 = wave * (NCH * 64);   // first K index of this wave's quarter
 
-    // ---------------- (1) every weight load of the lane: row row0 + r, k = kw0 + 64c + 32h .. +31
+    // every weight load of the lane: row row0 + r, k = kw0 + 64c + 32h .. +31.  Issued right after the first
+    // activation loads (whose addresses must not wait behind them: vmcnt retires in issue order)
     uint4 wr[NCH][4];
-    {
-        const uint16_t *wp = p.W + (size_t)(row0 + r) * K + kw0 + h * 32;
+    const uint16_t *wp = p.W + (size_t)(row0 + r) * K + kw0 + h * 32;
+    const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
+    auto issue_w = [&]() {
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) wr[c][j] = gld16(wp + c * 64 + j * 8);
-    }
+            for (int j = 0; j < 4; ++j) wr[c][j] = dbg_now ? make_uint4(j, c, 0, 0) : gld16(wp + c * 64 + j * 8);
+    };
 
     f32x16_t acc[TT];
 #pragma unroll
@@ -88,27 +174,41 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
                 nbv[it] = PRO == PRO_LN ? gldf4(p.nb + it * 256 + lane * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            float4 xv[4][NCH];
+        // rows in groups of 4, two groups in flight (L2-served); the weight stream (HBM) is issued behind the first
+        // two groups so that their norms do not wait for it (vmcnt retires in issue order)
+        float4 xa[4][4][NCH];
+        auto issue_x = [&](int g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int tl = wave * 16 + g * 4 + q;
-                const int src = t0 + min(tl, nt - 1);
-                const float *row = X + (size_t)src * p.ldx;
+                const float *row = X + (size_t)(t0 + min(tl, nt - 1)) * p.ldx;
 #pragma unroll
-                for (int it = 0; it < NCH; ++it) xv[q][it] = gldf4(row + it * 256 + lane * 4);
+                for (int it = 0; it < NCH; ++it) xa[g][q][it] = dbg_nox ? make_float4(q, it, 1.f, 0.f) : gldf4(row + it * 256 + lane * 4);
+            }
+        };
+        issue_x(0);
+        issue_x(1);
+        __builtin_amdgcn_sched_barrier(0);
+        issue_w();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (g >= 1 && g + 1 < 4) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue_x(g + 1);
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int tl = wave * 16 + g * 4 + q;
+                float4 (&xvq)[NCH] = xa[g][q];
                 const bool valid = tl < nt;
                 float scale = 1.0f, mean = 0.0f;
                 if constexpr (PRO == PRO_RMS) {
                     double ss = 0.0;
 #pragma unroll
                     for (int it = 0; it < NCH; ++it) {
-                        const float4 v = xv[q][it];
+                        const float4 v = xvq[it];
                         ss += (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z) + (double)(v.w * v.w);
                     }
                     ss = wave_sum_d(ss);
@@ -117,7 +217,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
                     double s1 = 0.0;
 #pragma unroll
                     for (int it = 0; it < NCH; ++it) {
-                        const float4 v = xv[q][it];
+                        const float4 v = xvq[it];
                         s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
                     }
                     s1 = wave_sum_d(s1);
@@ -125,7 +225,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
                     double s2 = 0.0;
 #pragma unroll
                     for (int it = 0; it < NCH; ++it) {
-                        const float4 v = xv[q][it];
+                        const float4 v = xvq[it];
                         const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
                         s2 += (double)(dx * dx) + (double)(dy * dy) + (double)(dz * dz) + (double)(dw * dw);
                     }
@@ -136,7 +236,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
 #pragma unroll
                 for (int it = 0; it < NCH; ++it) {
                     const int k = it * 256 + lane * 4;
-                    const float4 v = xv[q][it];
+                    const float4 v = xvq[it];
                     float y[4] = {v.x, v.y, v.z, v.w};
                     if constexpr (PRO == PRO_RMS || PRO == PRO_LN) {
                         const float w4[4] = {nwv[it].x, nwv[it].y, nwv[it].z, nwv[it].w};
@@ -180,20 +280,26 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
             const int src = p.x_idx ? p.x_idx[tok] : tok;
             xrow[tt] = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src * p.ldx + kw0 + h * 32;
         }
+        // one ring for both operands: chunk c = 4 weight loads + 4 TT activation loads, XD chunks in flight
+        constexpr int XD = NCH < (TT == 2 ? 3 : 4) ? NCH : (TT == 2 ? 3 : 4);
         uint4 xr[NCH][TT][4];
+        auto issue_chunk = [&](int c) {
 #pragma unroll
-        for (int c = 0; c < NCH && c < MM_XD; ++c)
+            for (int j = 0; j < 4; ++j) wr[c][j] = dbg_now ? make_uint4(j, c, 0, 0) : gld16(wp + c * 64 + j * 8);
 #pragma unroll
             for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) xr[c][tt][j] = gld16(xrow[tt] + c * 64 + j * 8);
+                for (int j = 0; j < 4; ++j) xr[c][tt][j] = dbg_nox ? make_uint4(j, tt, c, 0) : gld16(xrow[tt] + c * 64 + j * 8);
+        };
+#pragma unroll
+        for (int c = 0; c < XD; ++c) issue_chunk(c);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-            if (c + MM_XD < NCH)
-#pragma unroll
-                for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) xr[c + MM_XD][tt][j] = gld16(xrow[tt] + (c + MM_XD) * 64 + j * 8);
+            // pinned schedule: chunk c + XD is issued, then chunk c's MFMAs run (left alone, the scheduler
+            // interleaves loads with MFMAs and keeps only ~2 in flight)
+            __builtin_amdgcn_sched_barrier(0);
+            if (c + XD < NCH) issue_chunk(c + XD);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const half8_t a = as_h8(wr[c][j]);
@@ -211,92 +317,208 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
         for (int i = 0; i < 16; ++i) red[((wave * TT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
     __syncthreads();
 
-    // ---------------- (5) epilogue.  acc register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r.
+    // ---------------- (5) epilogue
     auto sum4 = [&](int tt, int i) {
         float v = 0.0f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) v += red[((w * TT + tt) * 16 + i) * 64 + lane];
         return v;
     };
-    const bool vec_ok = (p.ldo & 3) == 0;
-    if constexpr (SWIGLU) {
-        // combos (tt, q), q in {0, 1}: gate registers 4q..4q+3, up registers 4(q+2)..: unit = row0/2 + 8q + 4h + e
-        if (wave < TT * 2) {
-            const int tt = wave >> 1, q = wave & 1;
-            const int tl = tt * 32 + r;
-            if (tl < nt) {
-                const int tok = t0 + tl;
-                const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
-                const int unit = row0 / 2 + 8 * q + 4 * h;
-                float hv[4];
+    mm_epilogue<SWIGLU, TT>(p, wave, lane, r, h, row0, t0, nt, sum4);
+}
+
+// ------------------------------------------------------------------------------------------ norm prologues, 16 waves
+// PRO_F32 / PRO_RMS / PRO_LN at K <= 1024: the per-token norm is a chain of dependent VALU work (double sums, wave
+// reductions) that one wave per SIMD cannot hide (measured: ~12 us of a 17 us launch at B = 64 with no loads at all).
+// 1024 threads spread it over 16 waves (4 tokens each, issued together); K splits into 64-wide chunks, one per wave
+// (K / 64 waves take part in the MFMA phase), summed through LDS.
+template <int PRO, int NCH, int TT, bool SWIGLU>
+__global__ void __launch_bounds__(1024, 1) k_gemm_mfma_norm(const GemvParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int K = NCH * 256, NCHK = K / 64, KP = K + 8;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int row0 = blockIdx.x * MM_ROWS;
+    const int t0 = blockIdx.y * MM_TOK;
+    const int nt = min(MM_TOK, p.B - t0);
+    const bool mma = wave < NCHK;
+    const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
+    uint16_t *xs = reinterpret_cast<uint16_t *>(smem);
+    const float *X = reinterpret_cast<const float *>(p.x);
+    // (1) the wave's 4 activation rows, all in flight; then its weight chunk
+    float4 xa[4][NCH];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4(tt, 4 * q + e)) * sum4(tt, 4 * (q + 2) + e);
-                if (p.out_f16) {
-                    if (vec_ok) {
-                        uint2 o;
-                        o.x = (uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16);
-                        o.y = (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16);
-                        *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + unit) = o;
-                    } else {
+    for (int q = 0; q < 4; ++q) {
+        const float *row = X + (size_t)(t0 + min(wave * 4 + q, nt - 1)) * p.ldx;
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + unit + e] = f2h(hv[e]);
-                    }
-                } else {
+        for (int it = 0; it < NCH; ++it) xa[q][it] = dbg_nox ? make_float4(q, it, 1.f, 0.f) : gldf4(row + it * 256 + lane * 4);
+    }
+    uint4 wr[4];
+    {
+        const uint16_t *wp = p.W + (size_t)(row0 + r) * K + (mma ? wave : 0) * 64 + h * 32;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + unit + e] = hv[e];
+        for (int j = 0; j < 4; ++j) wr[j] = dbg_now ? make_uint4(j, 1, 0, 0) : gld16(wp + j * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // (2) norms -> f16 rows in LDS
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int tl = wave * 4 + q;
+        const bool valid = tl < nt;
+        float scale = 1.0f, mean = 0.0f;
+        if constexpr (PRO == PRO_RMS) {
+            double ss = 0.0;
+#pragma unroll
+            for (int it = 0; it < NCH; ++it) {
+                const float4 v = xa[q][it];
+                ss += (double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z) + (double)(v.w * v.w);
+            }
+            ss = wave_sum_d(ss);
+            scale = 1.0f / sqrtf((float)(ss / K) + p.eps);
+        } else if constexpr (PRO == PRO_LN) {
+            double s1 = 0.0;
+#pragma unroll
+            for (int it = 0; it < NCH; ++it) {
+                const float4 v = xa[q][it];
+                s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+            }
+            s1 = wave_sum_d(s1);
+            mean = (float)(s1 / K);
+            double s2 = 0.0;
+#pragma unroll
+            for (int it = 0; it < NCH; ++it) {
+                const float4 v = xa[q][it];
+                const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+                s2 += (double)(dx * dx) + (double)(dy * dy) + (double)(dz * dz) + (double)(dw * dw);
+            }
+            s2 = wave_sum_d(s2);
+            scale = 1.0f / sqrtf((float)(s2 / K) + p.eps);
+        }
+        const bool side = valid && blockIdx.x == 0;
+#pragma unroll
+        for (int it = 0; it < NCH; ++it) {
+            const int k = it * 256 + lane * 4;
+            const float4 v = xa[q][it];
+            float y[4] = {v.x, v.y, v.z, v.w};
+            if constexpr (PRO == PRO_RMS || PRO == PRO_LN) {
+                const float4 w4 = gldf4(p.nw + k);
+                const float4 c4 = PRO == PRO_LN ? gldf4(p.nb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (PRO == PRO_RMS) y[e] = (y[e] * scale) * wv[e];
+                    else y[e] = ((y[e] - mean) * scale) * wv[e] + cv[e];
                 }
+            }
+            if (side && p.raw_out) *reinterpret_cast<float4 *>(p.raw_out + (size_t)(t0 + tl) * K + k) = v;
+            if (side && p.side_out)
+                *reinterpret_cast<float4 *>(p.side_out + (size_t)(t0 + tl) * K + k) = make_float4(y[0], y[1], y[2], y[3]);
+            uint2 hv;
+            hv.x = valid ? ((uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16)) : 0u;
+            hv.y = valid ? ((uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16)) : 0u;
+            *reinterpret_cast<uint2 *>(xs + (size_t)tl * KP + k) = hv;
+        }
+    }
+    __syncthreads();
+    // (3) MFMA over this wave's 64-wide K chunk
+    f32x16_t acc[TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[tt][i] = 0.0f;
+    if (mma) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const half8_t a = as_h8(wr[j]);
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) {
+                const half8_t b = *reinterpret_cast<const half8_t *>(xs + (size_t)(tt * 32 + r) * KP + wave * 64 + h * 32 + j * 8);
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[tt], 0, 0, 0);
             }
         }
-    } else {
+    }
+    __syncthreads();   // the reduction reuses the activation tile
+    float *red = reinterpret_cast<float *>(smem);
+    if (mma)
 #pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const int combo = wave + 4 * cc;
-            if (combo >= TT * 4) break;
-            const int tt = combo >> 2, q = combo & 3;
-            const int tl = tt * 32 + r;
-            if (tl >= nt) continue;
-            const int tok = t0 + tl;
-            const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
-            const int n0 = row0 + 8 * q + 4 * h;
-            float v[4];
+        for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = sum4(tt, 4 * q + e);
-            // epilogue operands: 4 consecutive rows
-            float bb[4] = {0.f, 0.f, 0.f, 0.f}, sc[4] = {1.f, 1.f, 1.f, 1.f}, rs[4] = {0.f, 0.f, 0.f, 0.f}, ax[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int i = 0; i < 16; ++i) red[((wave * TT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
+    __syncthreads();
+    auto sum_k = [&](int tt, int i) {
+        float v = 0.0f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (p.bias) bb[e] = p.bias[n0 + e];
-                if (p.scale) sc[e] = p.scale[n0 + e];
-                if (p.resid) rs[e] = p.resid[(size_t)tok * p.ldr + n0 + e];
-                if (p.aux) ax[e] = p.aux[(size_t)tok * p.lda + n0 + e];
-            }
+        for (int w = 0; w < NCHK; ++w) v += red[((w * TT + tt) * 16 + i) * 64 + lane];
+        return v;
+    };
+    mm_epilogue<SWIGLU, TT>(p, wave, lane, r, h, row0, t0, nt, sum_k);
+}
+
+// ------------------------------------------------------------------------------------------ split-K, f16 rows
+// PRO_F16 projections whose epilogue is linear and lands in place on the residual stream (O-proj, down-proj:
+// out = x + scale * (W.h + bias)): grid z splits K into 256-wide slices (one 64-wide chunk per wave), so N = 1024
+// projections fill 256-384 workgroups instead of 32; each slice adds its scaled partial with a no-return f32 atomic
+// (bias once, by slice 0).  The sum order of the slices is unspecified: the residual stream is reproducible to f32
+// rounding, not bitwise, on this path.
+template <int TT>
+__global__ void __launch_bounds__(256, 2) k_gemm_mfma_splitk(const GemvParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+    const int K = p.K;
+    const int row0 = blockIdx.x * MM_ROWS;
+    const int t0 = blockIdx.y * MM_TOK;
+    const int nt = min(MM_TOK, p.B - t0);
+    const int k0 = blockIdx.z * 256 + wave * 64 + h * 32;
+    const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
+    const uint16_t *xrow[TT];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                float x = v[e];
-                if (p.bias) x += bb[e];
-                if (p.act == ACT_SILU) x = silu_f(x);
-                else if (p.act == ACT_GELU) x = gelu_ggml(x);
-                if (p.scale) x *= sc[e];
-                if (p.resid) x = rs[e] + x;
-                if (p.aux) x = ax[e] + x;
-                v[e] = x;
-            }
-            if (p.out_f16) {
-                if (vec_ok) {
-                    uint2 o;
-                    o.x = (uint32_t)f2h(v[0]) | ((uint32_t)f2h(v[1]) << 16);
-                    o.y = (uint32_t)f2h(v[2]) | ((uint32_t)f2h(v[3]) << 16);
-                    *reinterpret_cast<uint2 *>(p.out_f16 + orow * p.ldo + n0) = o;
-                } else {
+    for (int tt = 0; tt < TT; ++tt) {
+        const int tok = t0 + min(tt * 32 + r, nt - 1);
+        const int src = p.x_idx ? p.x_idx[tok] : tok;
+        xrow[tt] = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src * p.ldx + k0;
+    }
+    uint4 wr[4], xr[TT][4];
+    const uint16_t *wp = p.W + (size_t)(row0 + r) * K + k0;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) p.out_f16[orow * p.ldo + n0 + e] = f2h(v[e]);
-                }
-            } else if (vec_ok) {
-                *reinterpret_cast<float4 *>(p.out_f32 + orow * p.ldo + n0) = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
+    for (int j = 0; j < 4; ++j) wr[j] = dbg_now ? make_uint4(j, 1, 0, 0) : gld16(wp + j * 8);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) p.out_f32[orow * p.ldo + n0 + e] = v[e];
-            }
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xr[tt][j] = dbg_nox ? make_uint4(j, tt, 1, 0) : gld16(xrow[tt] + j * 8);
+    f32x16_t acc[TT];
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[tt][i] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const half8_t a = as_h8(wr[j]);
+#pragma unroll
+        for (int tt = 0; tt < TT; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, as_h8(xr[tt][j]), acc[tt], 0, 0, 0);
+    }
+    float *red = reinterpret_cast<float *>(smem);
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[((wave * TT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+        const int combo = wave + 4 * cc;
+        if (combo >= TT * 4) break;
+        const int tt = combo >> 2, q = combo & 3;
+        const int tl = tt * 32 + r;
+        if (tl >= nt) continue;
+        const int tok = t0 + tl;
+        const size_t orow = (size_t)tok * p.orow_mul + p.orow_add;
+        const int n0 = row0 + 8 * q + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float v = 0.0f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) v += red[((w * TT + tt) * 16 + 4 * q + e) * 64 + lane];
+            if (p.bias && blockIdx.z == 0) v += p.bias[n0 + e];
+            if (p.scale) v *= p.scale[n0 + e];
+            unsafeAtomicAdd(p.out_f32 + orow * p.ldo + n0 + e, v);
         }
     }
 }
@@ -335,56 +557,89 @@ bool gemm_mfma_supported(const GemvParams &p) {
     }
 }
 
+static bool g_splitk = [] {
+    const char *e = std::getenv("Q3T_MFMA_SPLITK");
+    return e ? std::atoi(e) != 0 : true;
+}();
+
+static bool set_lds(const void *fn, size_t lds, bool &done) {
+    if (!done) {
+        Q3T_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        done = true;
+    }
+    return true;
+}
+
+// f16 rows, one workgroup per 32 rows x 64 tokens over all of K (4 waves = 4 K-quarters)
+template <int NCH, int TT>
+static bool launch_f16(const GemvParams &p, hipStream_t s) {
+    const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
+    static bool attr = false;
+    if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma<PRO_F16, NCH, TT, false>), lds, attr)) return false;
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK));
+    hipLaunchKernelGGL((k_gemm_mfma<PRO_F16, NCH, TT, false>), grid, dim3(256), lds, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+// f16 rows, split-K in 256-wide slices with atomic accumulation onto the residual stream
+template <int TT>
+static bool launch_splitk(const GemvParams &p, hipStream_t s) {
+    const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK), (unsigned)(p.K / 256));
+    hipLaunchKernelGGL((k_gemm_mfma_splitk<TT>), grid, dim3(256), lds, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+// f32 rows with a norm prologue (16 waves)
 template <int PRO, int NCH, int TT, bool SW>
-static bool launch_mm(const GemvParams &p, hipStream_t s) {
-    constexpr bool kLds = PRO != PRO_F16;
-    const size_t red = (size_t)4 * TT * 16 * 64 * 4;
-    const size_t xt = kLds ? (size_t)MM_TOK * (NCH * 256 + 8) * 2 : 0;
+static bool launch_norm(const GemvParams &p, hipStream_t s) {
+    const size_t xt = (size_t)MM_TOK * (NCH * 256 + 8) * 2, red = (size_t)(NCH * 4) * TT * 16 * 64 * 4;
     const size_t lds = xt > red ? xt : red;
     static bool attr = false;
-    if (!attr) {
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_gemm_mfma<PRO, NCH, TT, SW>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
-    }
+    if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma_norm<PRO, NCH, TT, SW>), lds, attr)) return false;
     const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK));
-    hipLaunchKernelGGL((k_gemm_mfma<PRO, NCH, TT, SW>), grid, dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_gemm_mfma_norm<PRO, NCH, TT, SW>), grid, dim3(1024), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
 }
 template <int PRO, int NCH, int TT>
-static bool launch_sw(const GemvParams &p, hipStream_t s) {
+static bool launch_norm_sw(const GemvParams &p, hipStream_t s) {
     if constexpr (PRO == PRO_RMS) {
-        if (p.act == ACT_SWIGLU) return launch_mm<PRO, NCH, TT, true>(p, s);
+        if (p.act == ACT_SWIGLU) return launch_norm<PRO, NCH, TT, true>(p, s);
     }
-    return launch_mm<PRO, NCH, TT, false>(p, s);
-}
-template <int PRO, int NCH>
-static bool launch_tt(const GemvParams &p, hipStream_t s) {
-    return p.B > 32 ? launch_sw<PRO, NCH, 2>(p, s) : launch_sw<PRO, NCH, 1>(p, s);
+    return launch_norm<PRO, NCH, TT, false>(p, s);
 }
 template <int PRO>
-static bool launch_lds_nch(const GemvParams &p, hipStream_t s) {
+static bool launch_norm_nch(const GemvParams &p, hipStream_t s) {
+    const bool two = p.B > 32;
     switch (nch_of(p.K)) {
-        case 1: return launch_tt<PRO, 1>(p, s);
-        case 2: return launch_tt<PRO, 2>(p, s);
-        default: return launch_tt<PRO, 4>(p, s);
+        case 1: return two ? launch_norm_sw<PRO, 1, 2>(p, s) : launch_norm_sw<PRO, 1, 1>(p, s);
+        case 2: return two ? launch_norm_sw<PRO, 2, 2>(p, s) : launch_norm_sw<PRO, 2, 1>(p, s);
+        default: return two ? launch_norm_sw<PRO, 4, 2>(p, s) : launch_norm_sw<PRO, 4, 1>(p, s);
     }
+}
+template <int NCH>
+static bool launch_f16_tt(const GemvParams &p, hipStream_t s) {
+    return p.B > 32 ? launch_f16<NCH, 2>(p, s) : launch_f16<NCH, 1>(p, s);
 }
 
 bool gemm_mfma(const GemvParams &p, hipStream_t s) {
     switch (p.pro) {
-        case PRO_F16:
+        case PRO_F16: {
+            const bool linear_inplace = p.act == ACT_NONE && !p.out_f16 && p.out_f32 && p.resid == p.out_f32 &&
+                                        p.ldr == p.ldo && !p.aux && p.K % 256 == 0;
+            if (g_splitk && linear_inplace) return p.B > 32 ? launch_splitk<2>(p, s) : launch_splitk<1>(p, s);
             switch (nch_of(p.K)) {
-                case 1: return launch_tt<PRO_F16, 1>(p, s);
-                case 2: return launch_tt<PRO_F16, 2>(p, s);
-                case 4: return launch_tt<PRO_F16, 4>(p, s);
-                case 8: return launch_tt<PRO_F16, 8>(p, s);
-                default: return launch_tt<PRO_F16, 12>(p, s);
+                case 1: return launch_f16_tt<1>(p, s);
+                case 2: return launch_f16_tt<2>(p, s);
+                case 4: return launch_f16_tt<4>(p, s);
+                case 8: return launch_f16_tt<8>(p, s);
+                default: return launch_f16_tt<12>(p, s);
             }
-        case PRO_F32: return launch_lds_nch<PRO_F32>(p, s);
-        case PRO_RMS: return launch_lds_nch<PRO_RMS>(p, s);
-        default: return launch_lds_nch<PRO_LN>(p, s);
+        }
+        case PRO_F32: return launch_norm_nch<PRO_F32>(p, s);
+        case PRO_RMS: return launch_norm_nch<PRO_RMS>(p, s);
+        default: return launch_norm_nch<PRO_LN>(p, s);
     }
 }
 

@@ -97,6 +97,7 @@ struct GemvParams {
     uint16_t *out_f16 = nullptr;
     int ldo = 0;
     int orow_mul = 1, orow_add = 0;  // output row of batch b = b*orow_mul + orow_add
+    int dbg = 0;                     // microbenchmark knobs (tools/dev/kbench_mm): 1 = no activation loads, 2 = no weight loads
 };
 bool gemv(const GemvParams &p, hipStream_t s);   // routes wide batches to gemm_mfma (gemm_mfma.hip)
 // matrix-core path for B >= gemm_mfma_min_batch() tokens (Q3T_MFMA_MIN_B, default 4; 0 = off): F16 / F32 / RMS / LN

@@ -91,6 +91,7 @@ def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperatu
     cb0, cp = orc.generate_forced(toks, forced, spk=spk, rep=rep, force_frames=force_frames)
     n_dec = n_off = 0
     worst = 0.0
+    offs = []
     for f in range(forced.shape[0]):
         last = stopped and f == F
         for c in range(1 if last else 16):
@@ -102,6 +103,7 @@ def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperatu
                 if gap > 0:
                     n_off += 1
                     worst = max(worst, gap)
+                    offs.append((f, c, round(gap, 6)))
                     assert gap <= tol_logit, (f, c, gap)
             else:
                 keep = eos_id if (c == 0 and not (force_frames and f < force_frames)) else -1
@@ -115,6 +117,7 @@ def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperatu
                     n_off += 1
                     err = max(lo - target, target - hi) / tot
                     worst = max(worst, err)
+                    offs.append((f, c, round(err, 6)))
                     assert err <= tol_cdf, (f, c, err)
-    assert n_off <= max(1, int(max_off_frac * n_dec)), (n_off, n_dec, worst)
+    assert n_off <= max(1, int(max_off_frac * n_dec)), (n_off, n_dec, worst, offs)
     return n_off, n_dec, worst

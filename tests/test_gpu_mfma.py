@@ -7,7 +7,14 @@ f16 weights with f32 accumulation; only the summation order differs from the vec
 tolerances are those of test_gpu_parity.py (see its header for why they are relative-max-abs and teacher-forced).
 Batched runs cover one and two 32-token tiles per workgroup (B <= 32, B = 64) and several token blocks per launch
 (the prefill text projection of 64 utterances: ~900 rows).
+
+The O / down projections add 256-wide K slices onto the residual stream with f32 atomics (split-K), so their sum
+order varies between runs.  Logit errors stay ~1e-3 (the worst near-tie gaps seen are ~1.2e-3), but the synthetic
+full model has many near-tied greedy decisions (~3 % of them fall within 1e-3 of the top logit), so the fraction of
+decisions allowed to take the near-tie branch is 6 % here instead of 3 %; every such decision must still be within
+the 5e-2 logit gap of the oracle's choice.
 """
+MAX_OFF = 0.06
 import os
 import sys
 
@@ -94,9 +101,9 @@ def test_mfma_generate_batched_matches_oracle(mm, n_utt):
     outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.0, force_frames=nf)
     assert all(o.shape == (nf, 16) for o in outs)
     for i in sorted({0, n_utt // 2, n_utt - 1}):
-        check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf)
+        check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf, max_off_frac=MAX_OFF)
     # sampling: per-slot counter-based RNG, decisions teacher-forced against the oracle
     outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.9, top_k=50, seed=99, force_frames=nf)
     for i in sorted({1, n_utt - 2}):
         check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf, temperature=0.9, top_k=50,
-                        seed=99, utt=i)
+                        seed=99, utt=i, max_off_frac=MAX_OFF)
