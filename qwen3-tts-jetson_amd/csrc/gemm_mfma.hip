@@ -139,8 +139,8 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int K = NCH * 256, N = p.N;
     const int row0 = blockIdx.x * MM_ROWS;
-    const int t0 = blockIdx.y * MM_TOK;
-    const int nt = min(MM_TOK, p.B - t0);
+    const int t0 = blockIdx.y * (TT * 32);
+    const int nt = min(TT * 32, p.B - t0);
     const int kw0 = wave * (NCH * 64);   // first K index of this wave's quarter
 
     // every weight load of the lane: row row0 + r, k = kw0 + 64c + 32h .. +31.  Issued right after the first
@@ -338,17 +338,18 @@ __global__ void __launch_bounds__(1024, 1) k_gemm_mfma_norm(const GemvParams p) 
     constexpr int K = NCH * 256, NCHK = K / 64, KP = K + 8;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int row0 = blockIdx.x * MM_ROWS;
-    const int t0 = blockIdx.y * MM_TOK;
-    const int nt = min(MM_TOK, p.B - t0);
+    const int t0 = blockIdx.y * (TT * 32);
+    const int nt = min(TT * 32, p.B - t0);
     const bool mma = wave < NCHK;
     const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
     uint16_t *xs = reinterpret_cast<uint16_t *>(smem);
     const float *X = reinterpret_cast<const float *>(p.x);
-    // (1) the wave's 4 activation rows, all in flight; then its weight chunk
-    float4 xa[4][NCH];
+    // (1) the wave's 2 TT activation rows, all in flight; then its weight chunk
+    constexpr int TPW = 2 * TT;   // tokens per wave (TT * 32 tokens over 16 waves)
+    float4 xa[TPW][NCH];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float *row = X + (size_t)(t0 + min(wave * 4 + q, nt - 1)) * p.ldx;
+    for (int q = 0; q < TPW; ++q) {
+        const float *row = X + (size_t)(t0 + min(wave * TPW + q, nt - 1)) * p.ldx;
 #pragma unroll
         for (int it = 0; it < NCH; ++it) xa[q][it] = dbg_nox ? make_float4(q, it, 1.f, 0.f) : gldf4(row + it * 256 + lane * 4);
     }
@@ -361,8 +362,8 @@ __global__ void __launch_bounds__(1024, 1) k_gemm_mfma_norm(const GemvParams p) 
     __builtin_amdgcn_sched_barrier(0);
     // (2) norms -> f16 rows in LDS
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int tl = wave * 4 + q;
+    for (int q = 0; q < TPW; ++q) {
+        const int tl = wave * TPW + q;
         const bool valid = tl < nt;
         float scale = 1.0f, mean = 0.0f;
         if constexpr (PRO == PRO_RMS) {
@@ -465,8 +466,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm_mfma_splitk(const GemvParams p)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int K = p.K;
     const int row0 = blockIdx.x * MM_ROWS;
-    const int t0 = blockIdx.y * MM_TOK;
-    const int nt = min(MM_TOK, p.B - t0);
+    const int t0 = blockIdx.y * (TT * 32);
+    const int nt = min(TT * 32, p.B - t0);
     const int k0 = blockIdx.z * 256 + wave * 64 + h * 32;
     const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
     const uint16_t *xrow[TT];
@@ -557,9 +558,17 @@ bool gemm_mfma_supported(const GemvParams &p) {
     }
 }
 
+// split-K with f32 atomics onto the residual: measured slower at B = 64 (the atomic traffic of 256-384 workgroups x
+// 2048 adds costs ~20 us), so off unless Q3T_MFMA_SPLITK=1
 static bool g_splitk = [] {
     const char *e = std::getenv("Q3T_MFMA_SPLITK");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) != 0 : false;
+}();
+// 32-token tiles per workgroup (TT) : 1 = 32 tokens (more workgroups, weights re-read from L2 per token block),
+// 2 = 64 tokens; Q3T_MFMA_TT
+static int g_tt = [] {
+    const char *e = std::getenv("Q3T_MFMA_TT");
+    return e && std::atoi(e) == 2 ? 2 : 1;
 }();
 
 static bool set_lds(const void *fn, size_t lds, bool &done) {
@@ -576,7 +585,7 @@ static bool launch_f16(const GemvParams &p, hipStream_t s) {
     const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
     static bool attr = false;
     if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma<PRO_F16, NCH, TT, false>), lds, attr)) return false;
-    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK));
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)));
     hipLaunchKernelGGL((k_gemm_mfma<PRO_F16, NCH, TT, false>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
@@ -585,7 +594,7 @@ static bool launch_f16(const GemvParams &p, hipStream_t s) {
 template <int TT>
 static bool launch_splitk(const GemvParams &p, hipStream_t s) {
     const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
-    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK), (unsigned)(p.K / 256));
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)), (unsigned)(p.K / 256));
     hipLaunchKernelGGL((k_gemm_mfma_splitk<TT>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
@@ -593,11 +602,11 @@ static bool launch_splitk(const GemvParams &p, hipStream_t s) {
 // f32 rows with a norm prologue (16 waves)
 template <int PRO, int NCH, int TT, bool SW>
 static bool launch_norm(const GemvParams &p, hipStream_t s) {
-    const size_t xt = (size_t)MM_TOK * (NCH * 256 + 8) * 2, red = (size_t)(NCH * 4) * TT * 16 * 64 * 4;
+    const size_t xt = (size_t)TT * 32 * (NCH * 256 + 8) * 2, red = (size_t)(NCH * 4) * TT * 16 * 64 * 4;
     const size_t lds = xt > red ? xt : red;
     static bool attr = false;
     if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma_norm<PRO, NCH, TT, SW>), lds, attr)) return false;
-    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + MM_TOK - 1) / MM_TOK));
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)));
     hipLaunchKernelGGL((k_gemm_mfma_norm<PRO, NCH, TT, SW>), grid, dim3(1024), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
@@ -611,7 +620,7 @@ static bool launch_norm_sw(const GemvParams &p, hipStream_t s) {
 }
 template <int PRO>
 static bool launch_norm_nch(const GemvParams &p, hipStream_t s) {
-    const bool two = p.B > 32;
+    const bool two = g_tt == 2 && p.B > 32;
     switch (nch_of(p.K)) {
         case 1: return two ? launch_norm_sw<PRO, 1, 2>(p, s) : launch_norm_sw<PRO, 1, 1>(p, s);
         case 2: return two ? launch_norm_sw<PRO, 2, 2>(p, s) : launch_norm_sw<PRO, 2, 1>(p, s);
@@ -620,7 +629,7 @@ static bool launch_norm_nch(const GemvParams &p, hipStream_t s) {
 }
 template <int NCH>
 static bool launch_f16_tt(const GemvParams &p, hipStream_t s) {
-    return p.B > 32 ? launch_f16<NCH, 2>(p, s) : launch_f16<NCH, 1>(p, s);
+    return g_tt == 2 && p.B > 32 ? launch_f16<NCH, 2>(p, s) : launch_f16<NCH, 1>(p, s);
 }
 
 bool gemm_mfma(const GemvParams &p, hipStream_t s) {
@@ -628,7 +637,7 @@ bool gemm_mfma(const GemvParams &p, hipStream_t s) {
         case PRO_F16: {
             const bool linear_inplace = p.act == ACT_NONE && !p.out_f16 && p.out_f32 && p.resid == p.out_f32 &&
                                         p.ldr == p.ldo && !p.aux && p.K % 256 == 0;
-            if (g_splitk && linear_inplace) return p.B > 32 ? launch_splitk<2>(p, s) : launch_splitk<1>(p, s);
+            if (g_splitk && linear_inplace) return g_tt == 2 && p.B > 32 ? launch_splitk<2>(p, s) : launch_splitk<1>(p, s);
             switch (nch_of(p.K)) {
                 case 1: return launch_f16_tt<1>(p, s);
                 case 2: return launch_f16_tt<2>(p, s);
