@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--roofline-pos", type=int, default=10 + 512 // 2,
                     help="KV position of the talker-step roofline measurement (mid-utterance of configs[1])")
     ap.add_argument("--stage-iters", type=int, default=20, help="graph replays timed for the roofline")
+    ap.add_argument("--batched", type=int, default=64,
+                    help="secondary measurement at N=1: this many concurrent utterances (BASELINE configs[2]); 0 = off")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -170,6 +172,8 @@ def main():
 
     voc_mode = {"full": q3t.VOCODER_FULL, "chunk40": q3t.VOCODER_CHUNK40, "none": None}[args.vocoder]
     max_ctx = max(args.frames, args.roofline_pos) + 32
+    batched = args.batched if world == 1 else 0
+    slots = max(args.batch, batched)
     weights = "local GGUF read"
     if world > 1:
         # rank 0 writes the synthetic GGUFs (node-local), then publishes the RCCL id; the others wait for it
@@ -178,7 +182,7 @@ def main():
         uid = exchange_uid(rank, q3t.comm_unique_id if rank == 0 else None)
         if rank != 0:
             tts, tok = synth_dir(args.cfg)
-        eng = q3t.Engine.shared(tts, tok if voc_mode is not None else None, local_rank, args.batch, max_ctx,
+        eng = q3t.Engine.shared(tts, tok if voc_mode is not None else None, local_rank, slots, max_ctx,
                                 rank, world, uid)
         if rank == 0:
             release_uid()
@@ -186,7 +190,7 @@ def main():
         ctrl = RcclCtrl(eng)
     else:
         tts, tok = synth_dir(args.cfg)
-        eng = q3t.Engine(tts, tok if voc_mode is not None else None, device=0, max_slots=args.batch, max_ctx=max_ctx)
+        eng = q3t.Engine(tts, tok if voc_mode is not None else None, device=0, max_slots=slots, max_ctx=max_ctx)
         ctrl = LocalCtrl()
     B = args.batch
     prompt = make_prompt(args.cfg)
@@ -195,7 +199,7 @@ def main():
     spks = [np.zeros(H, np.float32)] * B
     stats = {"prefill_ms": 0.0, "frames_ms": 0.0, "vocoder_ms": 0.0}
 
-    def step(k):
+    def step(k, prompts=prompts, spks=spks):
         codes = eng.generate(prompts, speakers=spks, max_len=args.frames, temperature=0.9, top_k=50,
                              repetition_penalty=1.05, seed=1000 * rank + k, force_frames=args.frames)
         pm, fm = eng.last_timing()
@@ -225,6 +229,32 @@ def main():
     t_cp = eng.time_stage(1, B, p_mid, max(1, args.stage_iters // 2))
     cp_bytes = 16 * CP_PASS_BYTES + 15 * CP_HEAD_BYTES
 
+    # ---- secondary: BASELINE configs[2], `batched` concurrent utterances through the matrix-core path
+    bres = None
+    if batched > 0:
+        bp = [prompt] * batched
+        bs = [np.zeros(H, np.float32)] * batched
+        for k in stats:
+            stats[k] = 0.0
+        step(-100, bp, bs)   # warm-up (graph capture for this slot count)
+        for k in stats:
+            stats[k] = 0.0
+        b_el = timed_steps(LocalCtrl(), eng.synchronize, lambda k: step(100 + k, bp, bs), 1)
+        bt = eng.time_stage(0, batched, p_mid, max(2, args.stage_iters // 4))
+        bc = eng.time_stage(1, batched, p_mid, 2)
+        b_bytes = TALKER_WEIGHT_BYTES + KV_BYTES_PER_POS * (p_mid + 2) * batched
+        bres = {"config": f"configs[2]: {batched} concurrent utterances x {args.frames} frames on one GPU, "
+                          f"vocoder({args.vocoder}) per utterance, temp 0.9 top-k 50",
+                "value": round(batched * args.frames / b_el, 1), "unit": "frames/s", "ms_per_step": round(b_el * 1e3, 1),
+                "x_realtime": round(args.frames * FRAME_SEC * batched / b_el, 1),
+                "breakdown_ms_per_step": {k: round(v, 1) for k, v in stats.items()},
+                "talker_step_ms": round(bt, 4), "cp_frame_ms": round(bc, 4),
+                "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots "
+                                                       "(MFMA projections + batched split-K attention)",
+                             "achieved": round(b_bytes / (bt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(b_bytes / (bt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "bytes_per_launch": b_bytes, "launch_ms": round(bt, 4)}}
+
     if rank == 0:
         res = {
             "metric": "audio frames/sec (12 Hz frames) + RTF, Qwen3-TTS-0.6B batch=1 and batch=8xN",
@@ -249,6 +279,7 @@ def main():
                             "bytes_per_frame": cp_bytes, "note": "157 MB of CP weights re-read 16x per frame "
                             "(Infinity-Cache resident), algorithmic bytes / time"},
         }
+        res["batched"] = bres
         if args.cpu_baseline == "on" and world == 1:
             try:
                 res["cpu_baseline"] = cpu_baseline(tts, tok if voc_mode is not None else None, prompt, args.frames,
