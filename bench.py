@@ -146,6 +146,19 @@ def release_uid():
         pass
 
 
+def pmc_traffic(slots):
+    """HBM bytes per talker-step replay from the newest committed rocprofv3 FETCH_SIZE pass
+    (profiles/rNN_pmc_fetch_talker_step[_b64].txt, tools/dev/gpu_bench.sh; x2 gfx950 correction applied there)."""
+    import glob
+    import re
+    suffix = "" if slots == 1 else f"_b{slots}"
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_fetch_talker_step{suffix}.txt")))
+    if not files:
+        return None, None
+    m = re.search(r"->\s*([0-9.]+) MB per replay", open(files[-1]).read())
+    return (round(float(m.group(1)) * 1e6), os.path.relpath(files[-1], REPO)) if m else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,6 +230,7 @@ def main():
     for k in stats:
         stats[k] = 0.0
     elapsed = timed_steps(ctrl, eng.synchronize, step, args.steps)
+    main_stats = dict(stats)
     ms_per_step = elapsed / args.steps * 1e3
     total_frames = world * B * args.frames * args.steps
     value = total_frames / elapsed
@@ -253,6 +267,7 @@ def main():
                                                        "(MFMA projections + batched split-K attention)",
                              "achieved": round(b_bytes / (bt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(b_bytes / (bt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "traffic": pmc_traffic(batched)[0], "traffic_source": pmc_traffic(batched)[1],
                              "bytes_per_launch": b_bytes, "launch_ms": round(bt, 4)}}
 
     if rank == 0:
@@ -268,12 +283,13 @@ def main():
                        "parallelism": f"utterance-sharded dp{world}", "weights": weights},
             "rtf": round(ms_per_step / 1e3 / (args.frames * FRAME_SEC), 5),
             "x_realtime": round(args.frames * FRAME_SEC * B / (ms_per_step / 1e3), 1),
-            "breakdown_ms_per_step": {k: round(v / args.steps, 2) for k, v in stats.items()},
+            "breakdown_ms_per_step": {k: round(v / args.steps, 2) for k, v in main_stats.items()},
             "talker_step_ms": round(t_talker, 4), "cp_frame_ms": round(t_cp, 4),
             "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid} (28 layers + codec head: "
                                                   "141 kernels, one hipGraph replay)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(B)[0],
+                         "traffic_source": pmc_traffic(B)[1],
                          "bytes_per_launch": talker_bytes, "launch_ms": round(t_talker, 4)},
             "cp_roofline": {"achieved": round(cp_bytes / (t_cp * 1e-3) / 1e9, 1), "unit": "GB/s",
                             "bytes_per_frame": cp_bytes, "note": "157 MB of CP weights re-read 16x per frame "
