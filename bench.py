@@ -173,7 +173,8 @@ def main():
                     help="KV position of the talker-step roofline measurement (mid-utterance of configs[1])")
     ap.add_argument("--stage-iters", type=int, default=20, help="graph replays timed for the roofline")
     ap.add_argument("--batched", type=int, default=64,
-                    help="secondary measurement at N=1: this many concurrent utterances (BASELINE configs[2]); 0 = off")
+                    help="secondary measurement: this many concurrent utterances per GPU (BASELINE configs[2] at N=1, "
+                         "configs[3] at N>1: weak scaling, value over all ranks); 0 = off")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -185,7 +186,7 @@ def main():
 
     voc_mode = {"full": q3t.VOCODER_FULL, "chunk40": q3t.VOCODER_CHUNK40, "none": None}[args.vocoder]
     max_ctx = max(args.frames, args.roofline_pos) + 32
-    batched = args.batched if world == 1 else 0
+    batched = args.batched
     slots = max(args.batch, batched)
     weights = "local GGUF read"
     if world > 1:
@@ -253,14 +254,17 @@ def main():
         step(-100, bp, bs)   # warm-up (graph capture for this slot count)
         for k in stats:
             stats[k] = 0.0
-        b_el = timed_steps(LocalCtrl(), eng.synchronize, lambda k: step(100 + k, bp, bs), 1)
+        b_el = timed_steps(ctrl, eng.synchronize, lambda k: step(100 + k, bp, bs), 1)
         bt = eng.time_stage(0, batched, p_mid, max(2, args.stage_iters // 4))
         bc = eng.time_stage(1, batched, p_mid, 2)
         b_bytes = TALKER_WEIGHT_BYTES + KV_BYTES_PER_POS * (p_mid + 2) * batched
-        bres = {"config": f"configs[2]: {batched} concurrent utterances x {args.frames} frames on one GPU, "
-                          f"vocoder({args.vocoder}) per utterance, temp 0.9 top-k 50",
-                "value": round(batched * args.frames / b_el, 1), "unit": "frames/s", "ms_per_step": round(b_el * 1e3, 1),
-                "x_realtime": round(args.frames * FRAME_SEC * batched / b_el, 1),
+        bres = {"config": (f"configs[2]: {batched} concurrent utterances x {args.frames} frames on one GPU"
+                           if world == 1 else f"configs[3]: {world} x {batched} utterances x {args.frames} frames, "
+                           f"utterance-sharded over {world} GPUs") +
+                          f", vocoder({args.vocoder}) per utterance, temp 0.9 top-k 50",
+                "value": round(world * batched * args.frames / b_el, 1), "unit": "frames/s",
+                "ms_per_step": round(b_el * 1e3, 1), "n_gpus": world, "scaling": "weak",
+                "x_realtime": round(args.frames * FRAME_SEC * batched * world / b_el, 1),
                 "breakdown_ms_per_step": {k: round(v, 1) for k, v in stats.items()},
                 "talker_step_ms": round(bt, 4), "cp_frame_ms": round(bc, 4),
                 "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots "

@@ -58,7 +58,9 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
     uint4 kr[NP], vr[NP];
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
-        const int j = min(j0 + pi * PPP + pg, p.n_ctx - 1);
+        // rows past pos (masked below) re-read row pos: no HBM bytes beyond the live context (the last chunk of a
+        // context at p = 266 would otherwise fetch 53 dead rows of 64)
+        const int j = min(j0 + pi * PPP + pg, pos);
         kr[pi] = ldg16(p.kc + head_off + (size_t)j * D + li * 8);
         vr[pi] = ldg16(p.vc + head_off + (size_t)j * D + li * 8);
     }

@@ -55,6 +55,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     tok_path_ = tok_gguf;
     wa_.recv = recv_weights;
     cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
+    defer_cp_select_ = env_flag("Q3T_CP_DEFER_SELECT", true);
     fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
     if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
     max_slots_ = std::max(1, max_slots);
@@ -279,6 +280,8 @@ struct StackInput {
     int pro = PRO_RMS;
     const float *x = nullptr;
     GatherSum gs;
+    SelectSpec sel;                      // PRO_SEL_G1: selection of the gathered token
+    const float *sel_logits = nullptr;
 };
 static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, float *qkv,
                           uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc, size_t kv_layer, int n_ctx,
@@ -298,6 +301,7 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
                 if (!gather_sum(in0->gs, in0->pro == PRO_RMS_G16 ? 16 : 1, S, H, x, H, s)) return false;
             } else {
                 g.pro = in0->pro; g.x = in0->x; g.gs = in0->gs; g.raw_out = x;
+                g.sel = in0->sel; g.sel_logits = in0->sel_logits;
             }
         }
         g.out_f32 = qkv; g.ldo = QKV;
@@ -386,6 +390,11 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
     std::vector<float> lg;
+    // vector path with fused selection: heads 0..13 only produce logits; the next pass's QKV launch selects the token
+    // in every workgroup while its weights stream (PRO_SEL_G1), so the head's 256 -> 1 arrival chain and the serial
+    // selection leave the critical path.  Head 14 (its token feeds the next talker step) keeps the fused selection.
+    const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
+    const bool defer = fsel_all && defer_cp_select_;
     for (int p = 0; p < 16; ++p) {
         StackInput in0;
         if (p == 0) {
@@ -394,6 +403,11 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
             in0.pro = PRO_RMS_G1;
             in0.gs.tok = tokens_; in0.gs.tok_ld = 16; in0.gs.tok_col0 = p - 1;
             in0.gs.tab0 = p == 1 ? codec_embd_ : cp_embd_[p - 2];
+            if (defer && p >= 2) {
+                in0.pro = PRO_SEL_G1;
+                in0.sel = select_spec(SEL_CP, gp_, 0, p - 2);
+                in0.sel_logits = cp_logits_;
+            }
         }
         if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_,
                            rope_, part_, ticket_, s, &in0, cp_fused_attn_))
@@ -404,7 +418,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
         h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
-        const bool fsel = fused_select_ && S < gemm_mfma_min_batch();
+        const bool fsel = fsel_all && (!defer || step == 14);
         if (fsel) h.sel = select_spec(SEL_CP, gp_, 0, step);
         if (!gemv(h, s)) return false;
         if (logits_host) {
@@ -414,7 +428,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
             for (int b = 0; b < S; ++b)
                 std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
         }
-        if (!fsel && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
+        if (!fsel && !(defer && step < 14) && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
     }
     return true;
 }

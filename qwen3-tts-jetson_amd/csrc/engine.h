@@ -142,6 +142,7 @@ private:
     int poll_every_ = 16;        // frames between done-flag polls (Q3T_POLL_EVERY)
     bool fused_select_ = true;    // Q3T_FUSED_SELECT=0: separate selection launches
     bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
+    bool defer_cp_select_ = true; // Q3T_CP_DEFER_SELECT=0: code-predictor tokens selected in the head launch
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
     std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;

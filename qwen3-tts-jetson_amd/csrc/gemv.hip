@@ -78,13 +78,13 @@ __device__ __forceinline__ void mask_x(int K, bool valid, float4 (&r)[4]) {
 // embedding, tts_transformer.cpp:2529-2553), summed left to right in f32.  Tokens and table pointers are uniform
 // scalar loads; every row load is issued before any sum.
 template <int NT>
-__device__ __forceinline__ void issue_x_gather(const GemvParams &p, int b, float4 (&r)[4]) {
+__device__ __forceinline__ void issue_x_gather(const GemvParams &p, int b, float4 (&r)[4], int tok_sel = -1) {
     const GatherSum &gs = p.gs;
     const int tid = threadIdx.x, K = p.K;
     const uint16_t *row[NT];
     const float *extra = nullptr;
     if constexpr (NT == 1) {
-        row[0] = gs.tab0 + (size_t)gs.tok[(size_t)b * gs.tok_ld + gs.tok_col0] * K;
+        row[0] = gs.tab0 + (size_t)(tok_sel >= 0 ? tok_sel : gs.tok[(size_t)b * gs.tok_ld + gs.tok_col0]) * K;
     } else {
         const int *tk = gs.tok + (size_t)b * gs.tok_ld;   // the 16 codes of the frame, [S][16]
 #pragma unroll
@@ -284,7 +284,8 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int GPB = 16 / KS;   // row-groups per block
     constexpr int WPS = 4 / KS;    // waves per K slice
-    constexpr bool kGather = PRO == PRO_RMS_G1 || PRO == PRO_RMS_G16;
+    constexpr bool kSelG = PRO == PRO_SEL_G1;
+    constexpr bool kGather = PRO == PRO_RMS_G1 || PRO == PRO_RMS_G16 || kSelG;
     constexpr bool kRms = PRO == PRO_RMS || kGather;
     constexpr bool kAtt = PRO == PRO_CPATT;
     constexpr bool kF32 = PRO != PRO_F16 && !kAtt;
@@ -332,6 +333,9 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
     }
     CpAttRegs ar;
     if constexpr (kAtt) cpatt_issue(p, b0, ar);
+    // PRO_SEL_G1: the first slot's logits row, ahead of the weight stream (vmcnt retires in issue order)
+    float selv[kSelG ? SEL_VPT_MAX : 1];
+    if constexpr (kSelG) sel_load_exact<8>(p.sel_logits + (size_t)b0 * p.sel.V, selv);   // V = 2048 (gemv() checks)
     if constexpr (kXh) {
 #pragma unroll
         for (int b = 0; b < BT; ++b) {
@@ -390,9 +394,24 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
             for (int i = 0; i < RPG; ++i) wv[t][i] = ld_w(wrow[i] + (ok ? k : 0));
         }
     }
+    // PRO_SEL_G1: every workgroup selects the tokens of its slots while its weights stream (uniform per workgroup,
+    // identical in every workgroup: same inputs, same code); workgroup x = 0 records them
+    int *sel_tok = reinterpret_cast<int *>(att_lds + (kSelG ? sizeof(SelLds) : 0));
+    if constexpr (kSelG) {
+        __builtin_amdgcn_sched_barrier(0);
+        SelLds &SL = *reinterpret_cast<SelLds *>(att_lds);
+        for (int b = 0; b < nb; ++b) {
+            const int s = b0 + b;
+            if (b > 0) sel_load_exact<8>(p.sel_logits + (size_t)s * p.sel.V, selv);
+            const int tok = select_token_regs<SEL_CP>(p.sel, selv, s, SL);
+            if (tok >= 0 && blockIdx.x == 0 && tid == 0) select_commit(p.sel, s, tok);
+            if (tid == 0) sel_tok[b] = tok;
+            __syncthreads();
+        }
+    }
     if constexpr (kGather) {
 #pragma unroll
-        for (int q = 0; q < XB; ++q) issue_x_gather<NT>(p, b0 + min(q, nb - 1), r[q]);
+        for (int q = 0; q < XB; ++q) issue_x_gather<NT>(p, b0 + min(q, nb - 1), r[q], kSelG ? sel_tok[min(q, nb - 1)] : -1);
     }
 
     __builtin_amdgcn_sched_barrier(0);
@@ -429,7 +448,7 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
             if (bb > 0)
 #pragma unroll
                 for (int q = 0; q < XB; ++q) {
-                    if constexpr (kGather) issue_x_gather<NT>(p, b0 + min(bb + q, nb - 1), r[q]);
+                    if constexpr (kGather) issue_x_gather<NT>(p, b0 + min(bb + q, nb - 1), r[q], kSelG ? sel_tok[min(bb + q, nb - 1)] : -1);
                     else issue_x_plain(p, b0 + min(bb + q, nb - 1), r[q]);
                 }
 #pragma unroll
@@ -657,6 +676,7 @@ static void launch_pro(const GemvParams &p, int nl, dim3 grid, size_t lds, hipSt
             case PRO_RMS: launch_nl<1, BT, KS, PRO_RMS>(p, nl, grid, lds, s); break;
             case PRO_RMS_G1: launch_nl<1, BT, KS, PRO_RMS_G1>(p, nl, grid, lds, s); break;
             case PRO_RMS_G16: launch_nl<1, BT, KS, PRO_RMS_G16>(p, nl, grid, lds, s); break;
+            case PRO_SEL_G1: launch_nl<1, BT, KS, PRO_SEL_G1>(p, nl, grid, lds, s); break;
             case PRO_CPATT: launch_nl<1, BT, KS, PRO_CPATT>(p, nl, grid, lds, s); break;
             default: launch_nl<1, BT, KS, PRO_LN>(p, nl, grid, lds, s); break;
         }
@@ -691,13 +711,19 @@ bool gemv(const GemvParams &p, hipStream_t s) {
         return false;
     }
     if (swiglu && p.pro != PRO_RMS) { set_error("gemv: SwiGLU needs the RMSNorm prologue"); return false; }
-    if (p.sel.mode != SEL_NONE &&
+    const bool selg = p.pro == PRO_SEL_G1;
+    if (selg && (p.sel.mode != SEL_CP || !p.sel_logits || !p.sel.tokens || p.sel.V != 2048 ||
+                 (reinterpret_cast<uintptr_t>(p.sel_logits) & 15) != 0)) {
+        set_error("gemv: PRO_SEL_G1 needs a code-predictor SelectSpec and the previous head's logits");
+        return false;
+    }
+    if (!selg && p.sel.mode != SEL_NONE &&
         (p.pro != PRO_RMS || swiglu || !p.out_f32 || p.out_f16 || p.orow_mul != 1 || p.orow_add != 0 || p.ldo != p.N ||
          p.sel.V != p.N || p.N > 256 * SEL_VPT_MAX || !p.sel.ticket)) {
         set_error("gemv: fused selection needs an RMS-prologue head writing f32 logits [B][N] and a ticket buffer");
         return false;
     }
-    const bool g1 = p.pro == PRO_RMS_G1, g16 = p.pro == PRO_RMS_G16;
+    const bool g1 = p.pro == PRO_RMS_G1 || selg, g16 = p.pro == PRO_RMS_G16;
     if (p.pro == PRO_CPATT) {
         const CpAttnSrc &A = p.att;
         if (p.K != CPA_NH * CPA_D || !A.qkv || !A.qn || !A.kn || !A.rope || !A.pos || !A.kc || !A.vc || A.ld % 4 != 0) {
@@ -741,7 +767,8 @@ bool gemv(const GemvParams &p, hipStream_t s) {
     if (bt > 2 || Kp > 4096) nl = 0;
     const dim3 grid((unsigned)((units + (16 / ks) - 1) / (16 / ks)), (unsigned)gy);
     const size_t lds = (size_t)bt * Kp * 2 + 16 * rpg * bt * 4 + 8 * sizeof(double) +
-                       (p.pro == PRO_CPATT ? CPA_LDS : 0) + (p.sel.mode != SEL_NONE ? sizeof(SelLds) : 0);
+                       (p.pro == PRO_CPATT ? CPA_LDS : 0) + (p.sel.mode != SEL_NONE ? sizeof(SelLds) : 0) +
+                       (selg ? 8 * sizeof(int) : 0);
     if (bt == 1) launch_bt<1>(p, rpg, ks, nl, grid, lds, s);
     else if (bt == 2) launch_bt<2>(p, rpg, ks, nl, grid, lds, s);
     else if (bt == 4) launch_bt<4>(p, rpg, ks, nl, grid, lds, s);

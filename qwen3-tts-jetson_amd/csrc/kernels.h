@@ -7,7 +7,11 @@ namespace q3t {
 // PRO_RMS_G1 / PRO_RMS_G16: RMSNorm over a GatherSum source (1 table row / 16 table rows + trailing-or-pad row)
 // PRO_CPATT: the code predictor's whole attention (head RMSNorm + RoPE + KV append + softmax(QK^T)V over <= 16
 // positions) computed in the O-projection's prologue from the raw QKV rows (GemvParams::att)
-enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3, PRO_RMS_G1 = 4, PRO_RMS_G16 = 5, PRO_CPATT = 6 };
+// PRO_SEL_G1: PRO_RMS_G1 whose token is first SELECTED by every workgroup from the previous head's logits
+// (sel_logits, SelectSpec sel; workgroup x = 0 records it): the code predictor's selection moved off the head's
+// last-arriver chain into the next pass's weight-streaming window
+enum Prologue { PRO_F16 = 0, PRO_F32 = 1, PRO_RMS = 2, PRO_LN = 3, PRO_RMS_G1 = 4, PRO_RMS_G16 = 5, PRO_CPATT = 6,
+                PRO_SEL_G1 = 7 };
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_SWIGLU = 3 };
 
 // Token selection (select.h): SEL_CB0 = CB0 logit processing + selection (src/tts_transformer.cpp:2416-2499),
@@ -84,7 +88,8 @@ struct GemvParams {
     float eps = 1e-6f;
     GatherSum gs;                 // PRO_RMS_G1 / PRO_RMS_G16 source
     CpAttnSrc att;                // PRO_CPATT source
-    SelectSpec sel;               // PRO_RMS heads: select in the last workgroup (logits -> out_f32)
+    SelectSpec sel;               // PRO_RMS heads: select in the last workgroup (logits -> out_f32); PRO_SEL_G1 source
+    const float *sel_logits = nullptr;  // PRO_SEL_G1: [B][sel.V] logits of the previous head
     float *side_out = nullptr;    // normalized prologue rows (f32 [B][K]) written by x-block 0
     float *raw_out = nullptr;     // raw (pre-norm) f32 prologue rows [B][K] written by x-block 0
     int act = ACT_NONE;           // ACT_SWIGLU: rows interleaved in 16-row blocks [gate16 | up16]

@@ -145,7 +145,7 @@ __device__ __forceinline__ uint32_t sel_radix_pass(const uint32_t (&keys)[SEL_VP
 // k-th largest value (1-based k) of v[0..n): one 12-bit MSB histogram pass (4096 bins: sign, exponent, 3 mantissa
 // bits), then an exact rank among the few keys of the boundary bin (LDS candidate list); a boundary bin with more
 // than SEL_CAND keys (degenerate inputs) falls back to two more 10-bit radix passes.
-__device__ float sel_kth_largest(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, SelLds &S) {
+__device__ __forceinline__ float sel_kth_largest(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, SelLds &S) {
     const int t = threadIdx.x;
     uint32_t keys[SEL_VPT_MAX];
 #pragma unroll
@@ -201,8 +201,98 @@ __device__ float sel_kth_largest(const float (&v)[SEL_VPT_MAX], int n, int vpt, 
     return sel_keyf(prefix | d2);
 }
 
+// k-th largest value (1-based k < n) through ONE 256-bin histogram of the value range [min, max] of the finite
+// values (bin = floor((v - min) * 256 / (max - min)), monotonic in v, so the boundary bin holds the k-th largest),
+// scanned by a single wave; then the exact rank among the boundary bin's keys (LDS candidate list, as above).
+// Degenerate rows (max == min, non-finite range, > SEL_CAND keys in the boundary bin) take sel_kth_largest.
+// *vmax = the row maximum (exact, so the caller's softmax needs no second block reduction).
+__device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, float *vmax, SelLds &S) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    float mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (e < vpt && t * vpt + e < n) {
+            mx = fmaxf(mx, v[e]);
+            if (v[e] > -INFINITY) mn = fminf(mn, v[e]);
+        }
+    S.hist[t] = 0u;   // 256 bins, one per thread
+    mx = wave_max(mx);
+    mn = -wave_max(-mn);
+    __syncthreads();
+    if (lane == 0) { S.fred[wave] = mx; S.wsum[wave] = mn; }
+    __syncthreads();
+    mx = fmaxf(fmaxf(S.fred[0], S.fred[1]), fmaxf(S.fred[2], S.fred[3]));
+    mn = fminf(fminf(S.wsum[0], S.wsum[1]), fminf(S.wsum[2], S.wsum[3]));
+    *vmax = mx;
+    const float range = mx - mn;
+    if (!(range > 0.0f) || !(range < INFINITY)) return sel_kth_largest(v, n, vpt, k, S);   // uniform
+    const float scale = 256.0f / range;
+    int dig[SEL_VPT_MAX];
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        dig[e] = -1;
+        if (e < vpt && t * vpt + e < n && v[e] > -INFINITY) {
+            dig[e] = min(255, (int)((v[e] - mn) * scale));
+            atomicAdd(&S.hist[dig[e]], 1u);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // lane l owns bins 255-4l .. 252-4l (descending), so the inclusive lane scan counts keys from the top
+        const uint4 h4 = *reinterpret_cast<const uint4 *>(&S.hist[252 - 4 * lane]);
+        const unsigned c[4] = {h4.w, h4.z, h4.y, h4.x};
+        const unsigned loc = c[0] + c[1] + c[2] + c[3];
+        const unsigned incl = wave_scan_incl_u(loc);
+        const unsigned total = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
+        unsigned cum = incl - loc;
+        if (lane == 0) { S.ncand = 0; S.sres[0] = 0xFFFFFFFFu; }
+        if (total >= (unsigned)k) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (cum < (unsigned)k && (unsigned)k <= cum + c[q]) { S.sres[0] = 255 - 4 * lane - q; S.sres[1] = cum; }
+                cum += c[q];
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned bstar = S.sres[0];
+    if (bstar == 0xFFFFFFFFu) return -INFINITY;   // fewer than k finite values: the k-th largest is -inf
+    const int kk = k - (int)S.sres[1];
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e)
+        if (dig[e] == (int)bstar) {
+            const unsigned i = atomicAdd(&S.ncand, 1u);
+            if (i < SEL_CAND) S.cand[i] = sel_fkey(v[e]);
+        }
+    __syncthreads();
+    const unsigned nc = S.ncand;
+    if (nc > SEL_CAND) return sel_kth_largest(v, n, vpt, k, S);   // uniform
+    if (nc <= 64) {
+        if (t < 64) {
+            const uint32_t me = t < (int)nc ? S.cand[t] : 0u;
+            unsigned gt = 0, eq = 0;
+            for (unsigned j = 0; j < nc; ++j) {
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)me, (int)j);
+                gt += o > me;
+                eq += o == me;
+            }
+            if (t < (int)nc && gt < (unsigned)kk && (unsigned)kk <= gt + eq) S.sres[0] = me;
+        }
+    } else if (t < (int)nc) {
+        const uint32_t me = S.cand[t];
+        unsigned gt = 0, eq = 0;
+#pragma unroll 8
+        for (unsigned j = 0; j < nc; ++j) { const uint32_t o = S.cand[j]; gt += o > me; eq += o == me; }
+        if (gt < (unsigned)kk && (unsigned)kk <= gt + eq) S.sres[0] = me;
+    }
+    __syncthreads();
+    const uint32_t r = S.sres[0];
+    __syncthreads();
+    return sel_keyf(r);
+}
+
 // temperature -> top-k -> keep_id restored -> exp -> inverse CDF with u (v is modified)
-__device__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float temperature, int top_k, float u, int keep_id,
+__device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float temperature, int top_k, float u, int keep_id,
                           SelLds &S) {
     const int t = threadIdx.x;
 #pragma unroll
@@ -214,8 +304,11 @@ __device__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float tempera
 #pragma unroll
     for (int e = 0; e < SEL_VPT_MAX; ++e)
         if (t == keep_owner && t * vpt + e == keep_id) keep_v = v[e];
-    if (top_k > 0 && top_k < n) {
-        const float thr = sel_kth_largest(v, n, vpt, top_k, S);
+    float m = -INFINITY;
+    const bool topk = top_k > 0 && top_k < n;
+    if (topk) {
+        // the row max survives the threshold and bounds the restored kept logit: it is the softmax max as well
+        const float thr = sel_kth_largest_range(v, n, vpt, top_k, &m, S);
 #pragma unroll
         for (int e = 0; e < SEL_VPT_MAX; ++e)
             if (v[e] < thr) v[e] = -INFINITY;
@@ -223,11 +316,12 @@ __device__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float tempera
 #pragma unroll
     for (int e = 0; e < SEL_VPT_MAX; ++e)
         if (t == keep_owner && t * vpt + e == keep_id) v[e] = keep_v;
-    float m = -INFINITY;
+    if (!topk) {
 #pragma unroll
-    for (int e = 0; e < SEL_VPT_MAX; ++e)
-        if (e < vpt && t * vpt + e < n) m = fmaxf(m, v[e]);
-    m = sel_block_max(m, S);
+        for (int e = 0; e < SEL_VPT_MAX; ++e)
+            if (e < vpt && t * vpt + e < n) m = fmaxf(m, v[e]);
+        m = sel_block_max(m, S);
+    }
     float loc = 0.0f;
 #pragma unroll
     for (int e = 0; e < SEL_VPT_MAX; ++e) {
@@ -272,18 +366,36 @@ __device__ __forceinline__ void sel_load(const float *row, int n, int vpt, float
         else v[e] = in ? row[i] : -INFINITY;
     }
 }
+// the same for the vocabularies of the decode path (V = 2048: vpt 8, V = 3072: vpt 12, n == 256 vpt): 16-byte
+// loads, all issued before any is consumed
+template <int VPT>
+__device__ __forceinline__ void sel_load_exact(const float *row, float (&v)[SEL_VPT_MAX]) {
+    static_assert(VPT % 4 == 0 && VPT <= SEL_VPT_MAX, "vpt");
+    const float4 *r4 = reinterpret_cast<const float4 *>(row + threadIdx.x * VPT);
+    float4 q[VPT / 4];
+#pragma unroll
+    for (int i = 0; i < VPT / 4; ++i) q[i] = r4[i];
+#pragma unroll
+    for (int i = 0; i < VPT / 4; ++i) { v[4 * i] = q[i].x; v[4 * i + 1] = q[i].y; v[4 * i + 2] = q[i].z; v[4 * i + 3] = q[i].w; }
+#pragma unroll
+    for (int e = VPT; e < SEL_VPT_MAX; ++e) v[e] = -INFINITY;
+}
 
-// select the token of slot s from its logits row and record it (SelectSpec semantics, kernels.h)
-template <bool SC1>
-__device__ void select_slot(const SelectSpec &sp, const float *row, int s, SelLds &S) {
-    if (sp.done[s] >= 0) return;   // uniform over the workgroup
+// the token of slot s (uniform over the workgroup), or -1 if the slot is done; no side effects
+// select_token on a row already loaded into the owner registers (sel_load): lets a kernel issue the logits loads
+// ahead of its weight stream
+// MODE: SEL_CB0 / SEL_CP at compile time (the code-predictor path carries none of the CB0 rules), or SEL_NONE to
+// dispatch on sp.mode
+template <int MODE = SEL_NONE>
+__device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v)[SEL_VPT_MAX], int s, SelLds &S) {
+    if constexpr (MODE == SEL_NONE)
+        return sp.mode == SEL_CB0 ? select_token_regs<SEL_CB0>(sp, v, s, S) : select_token_regs<SEL_CP>(sp, v, s, S);
+    if (sp.done[s] >= 0) return -1;   // uniform over the workgroup
     const int t = threadIdx.x, V = sp.V, vpt = (V + 255) / 256;
     const int frame = sp.frame[s] + sp.frame_offset;
-    float v[SEL_VPT_MAX];
-    sel_load<SC1>(row, V, vpt, v);
     int keep = -1;
     float u;
-    if (sp.mode == SEL_CB0) {
+    if constexpr (MODE == SEL_CB0) {
         const int EOS = sp.eos;
         const uint8_t *seen = sp.seen + (size_t)s * V;
         float m = -INFINITY;
@@ -314,18 +426,53 @@ __device__ void select_slot(const SelectSpec &sp, const float *row, int s, SelLd
     } else {
         u = uniform24(sp.seed, sp.utt[s], (uint64_t)frame, (uint64_t)sp.step + 1);
     }
-    const int tok = sp.temperature <= 0.0f ? sel_argmax(v, V, vpt, S)
-                                           : sel_sample(v, V, vpt, sp.temperature, sp.top_k, u, keep, S);
-    if (t != 0) return;
+    return sp.temperature <= 0.0f ? sel_argmax(v, V, vpt, S) : sel_sample(v, V, vpt, sp.temperature, sp.top_k, u, keep, S);
+}
+
+// agent-scope (sc1) loads of a row published in this launch, exact widths: unconditional, all issued first
+template <int VPT>
+__device__ __forceinline__ void sel_load_exact_sc1(const float *row, float (&v)[SEL_VPT_MAX]) {
+    const float *r = row + threadIdx.x * VPT;
+#pragma unroll
+    for (int e = 0; e < VPT; ++e) v[e] = __hip_atomic_load(r + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int e = VPT; e < SEL_VPT_MAX; ++e) v[e] = -INFINITY;
+}
+
+template <bool SC1>
+__device__ __forceinline__ int select_token(const SelectSpec &sp, const float *row, int s, SelLds &S) {
+    float v[SEL_VPT_MAX];
+    if (sp.V == 2048) {
+        if constexpr (SC1) sel_load_exact_sc1<8>(row, v);
+        else sel_load_exact<8>(row, v);
+    } else if (sp.V == 3072) {
+        if constexpr (SC1) sel_load_exact_sc1<12>(row, v);
+        else sel_load_exact<12>(row, v);
+    } else {
+        sel_load<SC1>(row, sp.V, (sp.V + 255) / 256, v);
+    }
+    return select_token_regs(sp, v, s, S);
+}
+
+// the side effects of a selected token (thread 0 of ONE workgroup per slot): frame codes, EOS, seen set
+__device__ __forceinline__ void select_commit(const SelectSpec &sp, int s, int tok) {
+    const int frame = sp.frame[s] + sp.frame_offset;
     if (sp.mode == SEL_CB0) {
         sp.tokens[s * 16] = tok;
         if (tok == sp.eos) { sp.done[s] = frame; return; }
-        sp.seen[(size_t)s * V + tok] = 1;
+        sp.seen[(size_t)s * sp.V + tok] = 1;
         if (frame < sp.max_len) sp.codes[((size_t)s * sp.max_len + frame) * sp.ncb] = tok;
     } else {
         sp.tokens[s * 16 + sp.step + 1] = tok;
         if (frame < sp.max_len) sp.codes[((size_t)s * sp.max_len + frame) * sp.ncb + sp.step + 1] = tok;
     }
+}
+
+// select the token of slot s from its logits row and record it (SelectSpec semantics, kernels.h)
+template <bool SC1>
+__device__ __forceinline__ void select_slot(const SelectSpec &sp, const float *row, int s, SelLds &S) {
+    const int tok = select_token<SC1>(sp, row, s, S);
+    if (tok >= 0 && threadIdx.x == 0) select_commit(sp, s, tok);
 }
 
 }  // namespace q3t

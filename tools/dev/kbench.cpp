@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) k_sel_prof(const float *lg, int n, float 
     for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = v[e] / T;
     ts[2] = __builtin_amdgcn_s_memtime();
     float thr = -INFINITY;
-    if (topk > 0) thr = sel_kth_largest(v, n, vpt, topk, S);
+    float vmx; if (topk > 0) thr = sel_kth_largest_range(v, n, vpt, topk, &vmx, S);
     ts[3] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int e = 0; e < SEL_VPT_MAX; ++e) if (v[e] < thr) v[e] = -INFINITY;
