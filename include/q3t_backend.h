@@ -61,6 +61,8 @@ typedef struct q3t_gen_params {
 const char *q3t_last_error(void);
 void q3t_default_params(q3t_gen_params *p);
 
+/* tts_gguf may be NULL: a vocoder-only context (AudioTokenizerDecoder::load_model / TRTVocoderDecoder::load_engine
+ * without a talker); the talker entry points then fail with an error.  tokenizer_gguf may be NULL: no vocoder. */
 int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf /* may be NULL: no vocoder */, int device,
                    int max_slots, int max_ctx, q3t_ctx **out);
 void q3t_ctx_destroy(q3t_ctx *ctx);
@@ -108,6 +110,11 @@ int q3t_time_stage(q3t_ctx *ctx, int stage, int n_slots, int pos, int iters, dou
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);
 int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, int32_t n_frames, int mode,
                        float *pcm /* [q3t_vocoder_num_samples] */, int64_t *n_samples);
+
+/* TRTVocoderDecoder::decode (src/trt_vocoder.h:33-34) with the engine's fixed_frames: independent chunk_frames-long
+ * chunks, n_frames * 1920 samples (pcm capacity); n_codebooks must be 16 */
+int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes /* [n_frames][n_codebooks] */, int32_t n_frames,
+                               int32_t n_codebooks, int32_t chunk_frames, float *pcm, int64_t *n_samples);
 
 /* ---- stage entry points (used by the parity tests; each syncs the context stream) */
 int q3t_talker_forward(q3t_ctx *ctx, int n_slots, const float *embd /* [n][H] */, const int32_t *pos /* [n] */,

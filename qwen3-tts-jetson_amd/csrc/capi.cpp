@@ -39,6 +39,13 @@ q3t::GenParams to_gp(const q3t_gen_params *p) {
     }
 #define CHECK_CTX(c) if (!(c)) { q3t::set_error("null context"); return Q3T_ERR; }
 }  // namespace
+#define CHECK_TALKER(c)                                                                                   \
+    do {                                                                                                   \
+        if (!(c)->engine.has_talker()) {                                                                   \
+            q3t::set_error("vocoder-only context (created without a TTS GGUF)");                            \
+            return Q3T_ERR;                                                                                \
+        }                                                                                                  \
+    } while (0)
 
 extern "C" {
 
@@ -57,10 +64,10 @@ void q3t_default_params(q3t_gen_params *p) {
 
 int q3t_ctx_create(const char *tts_gguf, const char *tokenizer_gguf, int device, int max_slots, int max_ctx, q3t_ctx **out) {
     GUARD_BEGIN
-    if (!out || !tts_gguf) { q3t::set_error("null argument"); return Q3T_ERR; }
+    if (!out || (!tts_gguf && !tokenizer_gguf)) { q3t::set_error("null argument"); return Q3T_ERR; }
     *out = nullptr;
     q3t_ctx *c = new q3t_ctx();
-    if (!c->engine.load(tts_gguf, tokenizer_gguf ? tokenizer_gguf : "", device, max_slots, max_ctx)) {
+    if (!c->engine.load(tts_gguf ? tts_gguf : "", tokenizer_gguf ? tokenizer_gguf : "", device, max_slots, max_ctx)) {
         delete c;
         return Q3T_ERR;
     }
@@ -144,6 +151,7 @@ int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const in
                  const q3t_gen_params *p, int32_t *codes, int32_t *n_frames) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.generate(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -154,6 +162,7 @@ int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, c
                         q3t_frame_cb on_frames, void *user, int32_t interval) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.generate(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames, on_frames, user, interval)
                ? Q3T_OK : Q3T_ERR;
@@ -181,6 +190,7 @@ int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms) {
 int q3t_time_stage(q3t_ctx *ctx, int stage, int n, int pos, int iters, double *ms) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (!ms) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.time_stage(stage, n, pos, iters, ms) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -204,9 +214,23 @@ int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes, int32_t n_frames, int
     GUARD_END
 }
 
+int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes, int32_t n_frames, int32_t n_codebooks,
+                               int32_t chunk_frames, float *pcm, int64_t *n_samples) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::Vocoder *v = ctx->engine.vocoder();
+    if (!v || !v->loaded()) { q3t::set_error("vocoder not loaded (no tokenizer GGUF given)"); return Q3T_ERR; }
+    if (n_codebooks != 16) { q3t::set_error("n_codebooks must be 16"); return Q3T_ERR; }
+    if (chunk_frames <= 0) { q3t::set_error("chunk_frames must be > 0"); return Q3T_ERR; }
+    if (n_frames > 0 && (!codes || !pcm)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return v->decode(codes, n_frames, Q3T_VOCODER_CHUNK40, pcm, n_samples, chunk_frames) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
 int q3t_talker_forward(q3t_ctx *ctx, int n, const float *embd, const int32_t *pos, float *hidden, float *logits) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (!embd || !pos) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.talker_forward(n, embd, pos, hidden, logits) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -216,6 +240,7 @@ int q3t_codepred_frame(q3t_ctx *ctx, int n, const float *hidden, const int32_t *
                        uint64_t seed, int32_t frame, int32_t *codes15, float *logits) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (!hidden || !cb0 || !codes15) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.codepred_frame(n, hidden, cb0, temperature, top_k, seed, frame, codes15, logits) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -225,6 +250,7 @@ int q3t_cb0_select(q3t_ctx *ctx, int n, const float *logits, const uint8_t *seen
                    const int32_t *n_tokens, const q3t_gen_params *p, int32_t *tokens) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (!logits || !seen || !frame || !n_tokens || !tokens) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.cb0_select_host(n, logits, seen, frame, n_tokens, to_gp(p), tokens) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -233,6 +259,7 @@ int q3t_cb0_select(q3t_ctx *ctx, int n, const float *logits, const uint8_t *seen
 int q3t_project_text(q3t_ctx *ctx, int n, const int32_t *tokens, float *out) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (n > 0 && (!tokens || !out)) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.project_text(n, tokens, out) ? Q3T_OK : Q3T_ERR;
     GUARD_END
@@ -242,6 +269,7 @@ int q3t_prefill_embd(q3t_ctx *ctx, const int32_t *tokens, int n, const float *sp
                      int32_t *prefill_len, float *trailing, int32_t *trailing_len, float *tts_pad) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
     if (!tokens || !prefill || !prefill_len || !trailing || !trailing_len || !tts_pad) { q3t::set_error("null argument"); return Q3T_ERR; }
     return ctx->engine.prefill_embd(tokens, n, speaker, language_id, prefill, prefill_len, trailing, trailing_len, tts_pad)
                ? Q3T_OK : Q3T_ERR;

@@ -63,6 +63,15 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
     Q3T_HIP(hipSetDevice(device));
     Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (tts_gguf.empty()) {
+        // vocoder-only context (AudioTokenizerDecoder / TRTVocoderDecoder load without a talker model)
+        if (tok_gguf.empty()) { set_error("no model file given"); return false; }
+        talker_ = false;
+        voc_.reset(new Vocoder());
+        if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        return true;
+    }
     Gguf g;
     if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
     // parse_config key aliases / defaults: src/tts_transformer.cpp:288-442
@@ -573,7 +582,7 @@ bool Engine::copy_weights_from(Engine &src) {
     if (a.size() != b.size()) { set_error("copy_weights_from: contexts differ in vocoder presence"); return false; }
     for (size_t i = 0; i < a.size(); ++i) {
         if (a[i]->used != b[i]->used) { set_error("copy_weights_from: weight blobs differ in size"); return false; }
-        Q3T_HIP(hipMemcpyPeerAsync(a[i]->base, device_, b[i]->base, src.device_, a[i]->used, stream_));
+        if (a[i]->used) Q3T_HIP(hipMemcpyPeerAsync(a[i]->base, device_, b[i]->base, src.device_, a[i]->used, stream_));
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
     return true;

@@ -55,6 +55,7 @@ public:
     int max_slots() const { return max_slots_; }
     int device() const { return device_; }
     const std::string &tts_path() const { return tts_path_; }
+    bool has_talker() const { return talker_; }
     const std::string &tok_path() const { return tok_path_; }
     int max_ctx() const { return max_ctx_; }
     hipStream_t stream() const { return stream_; }
@@ -102,6 +103,7 @@ private:
 
     Config c_;
     std::string tts_path_, tok_path_;
+    bool talker_ = true;   // false: vocoder-only context
     int device_ = 0, max_slots_ = 0, max_ctx_ = 0, max_trailing_ = 0;
     hipStream_t stream_ = nullptr;
     std::vector<void *> allocs_;

@@ -406,7 +406,7 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     return true;
 }
 
-bool Vocoder::decode(const int32_t *codes, int F, int mode, float *pcm, int64_t *n_out) {
+bool Vocoder::decode(const int32_t *codes, int F, int mode, float *pcm, int64_t *n_out, int chunk_frames) {
     *n_out = n_samples(F, mode);
     if (F <= 0) return true;
     if (mode == 0) {
@@ -419,8 +419,10 @@ bool Vocoder::decode(const int32_t *codes, int F, int mode, float *pcm, int64_t 
         *n_out = n;
         return true;
     }
-    // CHUNK40 (trt_vocoder.cpp:98-170): independent 40-frame chunks, zero-padded codes, chunk_frames*1920 kept
-    const int FIX = 40;
+    // CHUNK40 (trt_vocoder.cpp:98-170): independent fixed-length chunks (40 frames unless the caller names the
+    // engine's fixed_frames), zero-padded codes, chunk_frames*1920 kept
+    if (chunk_frames <= 0) { set_error("vocoder: chunk_frames must be > 0"); return false; }
+    const int FIX = chunk_frames;
     if (!ensure(FIX)) return false;
     std::vector<int32_t> cc((size_t)FIX * 16);
     const int64_t full = full_len(FIX);

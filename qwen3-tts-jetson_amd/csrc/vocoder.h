@@ -17,7 +17,8 @@ public:
     WeightArena &weights() { return wa_; }
     // mode 0 = FULL (GGML decoder semantics), 1 = CHUNK40 (TRT streaming semantics)
     int64_t n_samples(int n_frames, int mode) const;
-    bool decode(const int32_t *codes_host, int n_frames, int mode, float *pcm_host, int64_t *n_out);
+    // chunk_frames: the fixed chunk length of the chunked mode (TRTVocoderDecoder::load_engine's fixed_frames)
+    bool decode(const int32_t *codes_host, int n_frames, int mode, float *pcm_host, int64_t *n_out, int chunk_frames = 40);
     // FULL decode of device-resident codes [F][16] into pcm_dev (capacity >= n_samples(F, 0)); ensure(F) first
     bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s);
     bool ensure(int n_frames);

@@ -64,6 +64,7 @@ _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
 _lib.q3t_vocoder_num_samples.restype = C.c_int64
 _lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
+_lib.q3t_vocoder_decode_chunked.argtypes = [_P, _ip, C.c_int32, C.c_int32, C.c_int32, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_talker_forward.argtypes = [_P, _I, _fp, _ip, _P, _P]
 _lib.q3t_codepred_frame.argtypes = [_P, _I, _fp, _ip, _F, C.c_int32, C.c_uint64, C.c_int32, _ip, _P]
 _lib.q3t_cb0_select.argtypes = [_P, _I, _fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _ip, _ip,
@@ -74,7 +75,8 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode", "q3t_talker_forward",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
+           "q3t_vocoder_decode_chunked", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -118,7 +120,8 @@ class Engine:
     def __init__(self, tts_gguf=None, tokenizer_gguf=None, device=0, max_slots=1, max_ctx=4096 + 32, *, _handle=None):
         if _handle is None:
             h = _P()
-            _check(_lib.q3t_ctx_create(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
+            _check(_lib.q3t_ctx_create(tts_gguf.encode() if tts_gguf else None,
+                                       tokenizer_gguf.encode() if tokenizer_gguf else None,
                                        int(device), int(max_slots), int(max_ctx), C.byref(h)))
             _handle = h
         self.h = _handle
@@ -235,6 +238,14 @@ class Engine:
         pcm = np.zeros(max(n, 1), np.float32)
         ns = C.c_int64(0)
         _check(_lib.q3t_vocoder_decode(self.h, codes, codes.shape[0], int(mode), pcm, C.byref(ns)))
+        return pcm[:ns.value]
+
+    def vocoder_chunked(self, codes, chunk_frames):
+        """TRTVocoderDecoder::decode with the engine's fixed_frames (src/trt_vocoder.cpp:98-170)."""
+        codes = np.ascontiguousarray(codes, np.int32).reshape(-1, 16)
+        pcm = np.zeros(max(codes.shape[0] * 1920, 1), np.float32)
+        ns = C.c_int64(0)
+        _check(_lib.q3t_vocoder_decode_chunked(self.h, codes, codes.shape[0], 16, int(chunk_frames), pcm, C.byref(ns)))
         return pcm[:ns.value]
 
     # ---- stages

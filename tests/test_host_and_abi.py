@@ -68,6 +68,47 @@ def test_ctx_create_without_gpu_fails_loudly():
     assert str(ei.value)
 
 
+CPP_LIB = os.path.join(PKG, "cpp", "libqwen3_tts_hip.so")
+CPP_TEST = os.path.join(REPO, "tests", "cpp", "_build", "test_host_api")
+
+
+def test_cpp_mirror_exports_the_reference_runtime_classes():
+    """qwen3_tts_hip.h keeps the reference's C++ surface (SURVEY §8(b) layer 2): qwen3_tts::TTSTransformer
+    (src/tts_transformer.h:164-245), AudioTokenizerDecoder (src/audio_tokenizer_decoder.h:158-180) and
+    TRTVocoderDecoder (src/trt_vocoder.h:18-42), same method names, built over libq3t.so (build() makes it)."""
+    assert os.path.exists(CPP_LIB), "libqwen3_tts_hip.so missing: run __graft_entry__.build()"
+    out = subprocess.run(["nm", "-D", "-C", "--defined-only", CPP_LIB], capture_output=True, text=True,
+                         check=True).stdout
+    for m in ("TTSTransformer::load_model(", "TTSTransformer::unload_model(", "TTSTransformer::init_kv_cache(",
+              "TTSTransformer::clear_kv_cache(", "TTSTransformer::forward_text(", "TTSTransformer::forward_prefill(",
+              "TTSTransformer::forward_step(", "TTSTransformer::get_hidden_states(",
+              "TTSTransformer::predict_codes_autoregressive(", "TTSTransformer::generate(",
+              "AudioTokenizerDecoder::load_model(", "AudioTokenizerDecoder::decode(",
+              "TRTVocoderDecoder::load_engine(", "TRTVocoderDecoder::decode(", "TRTVocoderDecoder::unload("):
+        assert "qwen3_tts::" + m in out, m
+    # the mirror calls only the C ABI: every libq3t symbol it needs is one the header declares
+    und = subprocess.run(["nm", "-D", "--undefined-only", CPP_LIB], capture_output=True, text=True, check=True).stdout
+    used = {ln.split()[-1] for ln in und.splitlines() if ln.split() and ln.split()[-1].startswith(("q3t_", "gpu_"))}
+    assert used and used <= set(header_functions()), used - set(header_functions())
+
+
+def test_cpp_mirror_error_paths_without_gpu():
+    """The C++ driver's first block (errors before/without load, bool + get_error(), nothing thrown) runs on a
+    GPU-less host; load_model then fails loudly instead of falling back to the CPU."""
+    import hip_py
+    if hip_py.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    assert os.path.exists(CPP_TEST), "tests/cpp/_build/test_host_api missing: run __graft_entry__.build()"
+    import tempfile
+    tts, tok = synth_dir("tiny")
+    with tempfile.TemporaryDirectory() as d:
+        np.asarray(prompt("tiny"), np.int32).tofile(os.path.join(d, "prompt.bin"))
+        r = subprocess.run([CPP_TEST, tts, tok, d], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, (r.returncode, r.stdout, r.stderr)
+    assert "FAIL" not in r.stderr, r.stderr
+    assert "load_model:" in r.stderr and "device" in r.stderr, r.stderr
+
+
 def test_default_params_match_reference_tts_params():
     sys.path.insert(0, PKG)
     import q3t
