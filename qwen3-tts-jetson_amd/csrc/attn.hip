@@ -10,6 +10,8 @@
 // add; the last adder loads the partials with sc1 loads) -- no combine launch, no release/acquire cache flushes.
 #include "kernels.h"
 
+#pragma clang fp contract(off)   // every rounding as written (persist.hip reproduces this kernel bit for bit)
+
 namespace q3t {
 
 template <class V>
@@ -82,7 +84,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float x[E];
         double ss = 0.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { x[e] = src[lane + 64 * e]; ss += (double)(x[e] * x[e]); }
+        for (int e = 0; e < E; ++e) { x[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(x[e], x[e]); }
         ss = wave_sum_d(ss);
         const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
 #pragma unroll
@@ -90,8 +92,9 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float y[E];
         if constexpr (D == 128) {
             const float c = rope[2 * lane], s = rope[2 * lane + 1];
-            y[0] = x[0] * c - x[1] * s;
-            y[1] = x[0] * s + x[1] * c;
+            // every rounding explicit (no fma / fma_mix fusion): the persistent step (persist.hip) reproduces it bit for bit
+            y[0] = opaque(opaque(x[0] * c) - opaque(x[1] * s));
+            y[1] = opaque(opaque(x[0] * s) + opaque(x[1] * c));
         } else {
             const int i = lane & 31;
             const float c = rope[2 * i], s = rope[2 * i + 1];
@@ -133,9 +136,9 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         for (int h = 0; h < RMAX; ++h) {
             float s = 0.0f;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s += k8[e] * q8[h][e];
+            for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);   // explicit fma: identical in k_attn and persist.hip
             s = group_sum<LPP>(s);
-            sc[pi][h] = ok[pi] ? s * kq_scale : -INFINITY;
+            sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
         }
     }
     // ---- (4) chunk max / exp / sum per head (xor over the position bits of the wave, then LDS over waves)
@@ -161,7 +164,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float l = 0.0f;
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
-            pr[pi][h] = ok[pi] ? expf(sc[pi][h] - M[h]) : 0.0f;
+            pr[pi][h] = ok[pi] ? expf(__fsub_rn(sc[pi][h], M[h])) : 0.0f;
             l += pr[pi][h];
         }
         if constexpr (LPP == 16) l = rows_sum(l);
@@ -189,7 +192,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 #pragma unroll
         for (int h = 0; h < RMAX; ++h)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[h][e] += pr[pi][h] * (ok[pi] ? v8[e] : 0.0f);
+            for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr[pi][h], ok[pi] ? v8[e] : 0.0f, acc[h][e]);
     }
 #pragma unroll
     for (int h = 0; h < RMAX; ++h)
@@ -212,6 +215,11 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
             const int h = o / D, d = o % D;
             const float a = (ared[0][h][d] + ared[1][h][d]) + (ared[2][h][d] + ared[3][h][d]);
             p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(a / L[h]);
+            if (p.dbg && slot == 0 && g == 5 && R == 2) p.dbg[516 + o] = a / L[h];
+        }
+        if (p.dbg && slot == 0 && g == 5 && R == 2 && t < D) {
+            p.dbg[t] = q_s[0][t]; p.dbg[128 + t] = q_s[1 % R][t]; p.dbg[256 + t] = kn_s[t]; p.dbg[384 + t] = vn_s[t];
+            if (t == 0) { p.dbg[512] = M[0]; p.dbg[513] = M[1 % R]; p.dbg[514] = L[0]; p.dbg[515] = L[1 % R]; }
         }
         return;
     }
@@ -243,7 +251,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float mx = -INFINITY;
         for (int s = 0; s < nsplit; ++s) mx = fmaxf(mx, sm[s][t]);
         float lt = 0.0f;
-        for (int s = 0; s < nsplit; ++s) lt += sl[s][t] * expf(sm[s][t] - mx);
+        for (int s = 0; s < nsplit; ++s) lt = __fmaf_rn(sl[s][t], expf(sm[s][t] - mx), lt);
         cm[t] = mx;
         cl[t] = lt;
     }
@@ -263,7 +271,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
                 v[u] = s0 + u < nsplit ? ld_sc1(part + ((size_t)(s0 + u) * R + h) * (D + 2) + d) : 0.0f;
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (s0 + u < nsplit) a += v[u] * sw[s0 + u][h];
+                if (s0 + u < nsplit) a = __fmaf_rn(v[u], sw[s0 + u][h], a);
         }
         p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(a / cl[h]);
     }

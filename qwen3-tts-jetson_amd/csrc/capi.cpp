@@ -196,6 +196,19 @@ int q3t_time_stage(q3t_ctx *ctx, int stage, int n, int pos, int iters, double *m
     GUARD_END
 }
 
+int q3t_debug_read(q3t_ctx *ctx, int which, void *dst, size_t bytes) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
+    return ctx->engine.debug_read(which, dst, bytes) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_persist_status(q3t_ctx *ctx) {
+    if (!ctx || !ctx->engine.has_talker() || !ctx->engine.persist_enabled()) return -1;
+    return ctx->engine.persist_error() ? 1 : 0;
+}
+
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode) {
     if (!ctx) return -1;
     q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();

@@ -1,5 +1,6 @@
 // engine.cpp — see engine.h.
 #include "engine.h"
+#include "persist.h"
 
 #include <cmath>
 #include <cstdio>
@@ -57,6 +58,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
     defer_cp_select_ = env_flag("Q3T_CP_DEFER_SELECT", true);
     fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
+    persist_ = env_flag("Q3T_PERSIST", true);
     if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
@@ -109,6 +111,11 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     cp_fused_attn_ = cp_fused_attn_ && c_.n_heads == 16 && c_.n_kv == 8 && c_.head_dim == 128;
     if (!upload_weights(g)) return false;
     if (!alloc_state()) return false;
+    if (const char *e = std::getenv("Q3T_TALKER_LAYERS")) {   // dev knob: truncated talker stack (debugging only)
+        const int n = std::atoi(e);
+        if (n > 0 && n < c_.n_layers) { c_.n_layers = n; L_.resize(n); }
+    }
+    if (!setup_persist()) return false;
     if (!tok_gguf.empty()) {
         voc_.reset(new Vocoder());
         if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
@@ -280,6 +287,63 @@ bool Engine::alloc_state() {
     return true;
 }
 
+// the persistent single-slot talker step (persist.hip): layer pointer table + zeroed hand-off state; off when the
+// shapes or the device do not match what the kernel is built for (the launch-per-phase graph is used then)
+bool Engine::setup_persist() {
+    int n_cu = 0;
+    Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
+    persist_ = persist_ && fused_select_ &&
+               persist_supported(c_.hidden, c_.n_heads, c_.n_kv, c_.head_dim, c_.inter, c_.codec_vocab, max_ctx_, n_cu);
+    if (!persist_) return true;
+    std::vector<PLayerW> pl(L_.size());
+    for (size_t i = 0; i < L_.size(); ++i)
+        pl[i] = PLayerW{L_[i].qkv, L_[i].o, L_[i].gu, L_[i].down, L_[i].attn_norm, L_[i].ffn_norm, L_[i].qn, L_[i].kn};
+    pl_dev_ = dalloc<PLayerW>(pl.size());
+    pstate_ = dalloc<uint8_t>(persist_state_bytes());
+    if (!pl_dev_ || !pstate_) { set_error("device allocation failed"); return false; }
+    Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
+    if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
+    return true;
+}
+
+bool Engine::debug_read(int which, void *dst, size_t bytes) {
+    if (which == 5 && pprof_) {   // persistent-step timeline (dev)
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        Q3T_HIP(hipMemcpy(dst, pprof_, std::min<size_t>(bytes, (size_t)256 * PROF_PH * 4 * 8), hipMemcpyDeviceToHost));
+        return true;
+    }
+    if (which == 4 && !pstate_) {   // launch-per-phase attention partial buffer (dev dumps)
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        Q3T_HIP(hipMemcpy(dst, part_, std::min<size_t>(bytes, (size_t)max_slots_ * c_.n_heads * ((max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK) * (c_.head_dim + 2) * 4), hipMemcpyDeviceToHost));
+        return true;
+    }
+    if (which == 4 && pstate_) {   // persistent-step partial buffer (dev dumps)
+        PersistParams pp;
+        persist_carve(pstate_, pp);
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        Q3T_HIP(hipMemcpy(dst, pp.part, std::min<size_t>(bytes, 8 * 32 * 2 * 130 * 4), hipMemcpyDeviceToHost));
+        return true;
+    }
+    const void *src = which == 0 ? (const void *)kc_ : which == 1 ? (const void *)vc_ : which == 2 ? (const void *)qkv_ : (const void *)attn_;
+    const size_t kvb = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim * c_.n_layers * 2;
+    const size_t cap = which <= 1 ? kvb : which == 2 ? (size_t)max_slots_ * (c_.n_heads + 2 * c_.n_kv) * c_.head_dim * 4
+                                                     : (size_t)max_slots_ * c_.n_heads * c_.head_dim * 2;
+    if (which < 0 || which > 3 || bytes > cap) { set_error("debug_read: bad buffer or size"); return false; }
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    Q3T_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return true;
+}
+
+bool Engine::persist_error() {
+    if (!persist_ || !pstate_) return false;
+    PersistParams p;
+    persist_carve(pstate_, p);
+    unsigned e = 0;
+    if (hipMemcpy(&e, p.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return true;
+    return e != 0;
+}
+
 // ------------------------------------------------------------------------------------------ one decoder stack
 // 5 launches per layer: [RMSNorm+QKV GEMV] [head-norm+RoPE+KV-append+attention] [O GEMV + residual]
 // [RMSNorm+gate/up GEMV+SwiGLU] [down GEMV + residual]   (tts_transformer.cpp:1410-1494)
@@ -328,6 +392,7 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
             a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
             a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
             a.max_splits = max_splits; a.part = part; a.ticket = ticket; a.out = attn;
+            if (il == 0 && std::getenv("Q3T_PERSIST_DBG")) a.dbg = part;
             if (!attn_decode(a, s)) return false;
             o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
         }
@@ -369,6 +434,22 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
+    if (S == 1 && persist_) {
+        PersistParams p;
+        persist_carve(pstate_, p);
+        p.L = pl_dev_; p.n_layers = c_.n_layers; p.eps = c_.eps;
+        p.gather = gather_input ? 1 : 0;
+        p.x_in = x_;
+        p.gs.tok = tokens_; p.gs.tok_ld = 16; p.gs.tabs = tabs16_dev_;
+        p.gs.tr = trailing_; p.gs.tr_len = trailing_len_; p.gs.frame = frame_;
+        p.gs.tr_ld = max_trailing_ * H; p.gs.pad = tts_pad_;
+        p.rope = rope_; p.pos = pos_; p.kc = kc_; p.vc = vc_; p.kv_layer = kv_layer; p.n_ctx = max_ctx_;
+        p.head = codec_head_; p.out_norm = out_norm_; p.hidden = hidden_; p.logits = logits_;
+        if (select_next) p.sel = select_spec(SEL_CB0, gp_, 1, 0);
+        if (std::getenv("Q3T_PERSIST_DBG")) { p.dbg_qkv = qkv_; p.dbg_attn = attn_; }   // layer-0 intermediates (dev)
+        p.prof = pprof_;
+        return persist_talker_step(p, s);
+    }
     StackInput in0;
     if (gather_input) {
         in0.pro = PRO_RMS_G16;
@@ -739,6 +820,7 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
                                (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
     if (dbg) { fprintf(stderr, "[q3t] frame loop done\n"); fflush(stderr); }
+    if (persist_error()) { hipHostFree(done_h); set_error("persistent talker step: an in-launch hand-off timed out"); return false; }
     for (int s = 0; s < S; ++s) n_frames[s] = done_h[s] >= 0 ? std::min(done_h[s], gp.max_len) : gp.max_len;
     hipHostFree(done_h);
     if (stream_cb) {
@@ -797,6 +879,7 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (hidden) Q3T_HIP(hipMemcpyAsync(hidden, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToHost, stream_));
     if (logits) Q3T_HIP(hipMemcpyAsync(logits, logits_, (size_t)S * c_.codec_vocab * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
+    if (persist_error()) { set_error("persistent talker step: an in-launch hand-off timed out"); return false; }
     return true;
 }
 

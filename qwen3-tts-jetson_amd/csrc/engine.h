@@ -40,6 +40,7 @@ struct DevLayer {
 };
 
 class Vocoder;
+struct PLayerW;
 
 class Engine {
 public:
@@ -86,12 +87,19 @@ public:
     // report the mean device time per replay (HIP events on the context stream)
     bool time_stage(int stage, int S, int pos, int iters, double *ms);
 
+    // true if a persistent launch gave up waiting on a hand-off (never expected: a protocol fault)
+    bool persist_error();
+    bool persist_enabled() const { return persist_; }
+    // development hook: copy a device state buffer to the host (0 K cache, 1 V cache, 2 qkv, 3 attention output)
+    bool debug_read(int which, void *dst, size_t bytes);
+
     // profiling hooks for bench.py: last generate() timings
     double last_prefill_ms = 0, last_frames_ms = 0;
 
 private:
     bool upload_weights(const Gguf &g);
     bool alloc_state();
+    bool setup_persist();
     bool enqueue_talker_step(int S, hipStream_t s);
     bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next);
     SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;
@@ -145,6 +153,10 @@ private:
     bool fused_select_ = true;    // Q3T_FUSED_SELECT=0: separate selection launches
     bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
     bool defer_cp_select_ = true; // Q3T_CP_DEFER_SELECT=0: code-predictor tokens selected in the head launch
+    bool persist_ = true;         // Q3T_PERSIST=0: launch-per-phase talker step at one slot (no persistent kernel)
+    PLayerW *pl_dev_ = nullptr;
+    uint8_t *pstate_ = nullptr;
+    uint64_t *pprof_ = nullptr;   // Q3T_PERSIST_PROF: persistent-step timeline (dev)
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
     std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;

@@ -128,6 +128,7 @@ struct AttnParams {
     float *part = nullptr;        // [S][nKV][max_splits][R][D + 2] split partials (m, l, acc)
     unsigned *ticket = nullptr;   // [S][nKV] arrival counters, zero between launches
     uint16_t *out = nullptr;      // [S][nH*D] f16 (rounded attention output, the O-proj input)
+    float *dbg = nullptr;         // development dump (slot 0, kv group 5, split 0)
 };
 bool attn_decode(const AttnParams &p, hipStream_t s);
 constexpr int ATTN_CHUNK = 64;

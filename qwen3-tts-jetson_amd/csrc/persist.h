@@ -1,0 +1,62 @@
+// persist.h — the persistent talker decode step (persist.hip): the whole 28-layer Talker step plus the codec head and
+// the fused CB0 selection of ONE slot as a single launch of one workgroup per CU, replacing the 141-launch graph of
+// enqueue_talker at batch 1 (src/tts_transformer.cpp:1376-1512 build_step_graph + :2416-2499 CB0 processing).
+//
+// Inside the launch, every dependency edge (x -> QKV -> attention -> O -> x' -> gate/up -> h -> down -> x) is a
+// vector of data-tagged granules: {32-bit payload, 32-bit tag} written by ONE 8-byte agent-scope (sc1) store and
+// polled by the consumers with sc1 loads until every tag matches (MI355X_MICROARCH.md, handoff-1to1 / allgather rows;
+// no flags, no fences, no grid barrier).  Tags are ((seq * 1024 + phase) << 1) | 1 with `seq` a device word bumped
+// by the last workgroup of every launch, so a granule of an earlier launch or layer can never match.  Weights and
+// K/V rows do not depend on the edge: each phase's weight loads are issued as soon as the previous phase's input has
+// arrived, so they stream while the chain waits.
+#pragma once
+#include "kernels.h"
+
+namespace q3t {
+
+constexpr int PROF_PH = 160;   // timeline phases recorded per workgroup (5 per layer + head)
+
+struct PLayerW {
+    const uint16_t *qkv, *o, *gu, *down;
+    const float *attn_norm, *ffn_norm, *qn, *kn;
+};
+
+struct PersistParams {
+    const PLayerW *L = nullptr;   // device array [n_layers]
+    int n_layers = 0;
+    float eps = 1e-6f;
+    // layer-0 input: x_in (f32 [1024], written before the launch) or the step-embedding gather (GatherSum, NT = 16)
+    int gather = 0;
+    const float *x_in = nullptr;
+    GatherSum gs;
+    // attention (talker KV layout [layer][slot][kv][n_ctx][128], slot 0)
+    const float *rope = nullptr;
+    const int *pos = nullptr;
+    uint16_t *kc = nullptr, *vc = nullptr;
+    size_t kv_layer = 0;
+    int n_ctx = 0;
+    float *part = nullptr;        // [8][32][2][130] split partials
+    unsigned *ticket = nullptr;   // [8] split arrival counters (zero between layers)
+    // head: hidden = rms(x) * out_norm (f32, side output), logits = head . f16(hidden) (f32 [V], sc1 stores)
+    const uint16_t *head = nullptr;
+    const float *out_norm = nullptr;
+    float *hidden = nullptr, *logits = nullptr;
+    SelectSpec sel;               // SEL_CB0 of the next frame, or SEL_NONE
+    // hand-off state (persist_alloc)
+    uint64_t *gx = nullptr, *gx2 = nullptr, *gqkv = nullptr, *gattn = nullptr, *gh = nullptr;
+    uint64_t *gpart = nullptr;     // [8][32][264] attention split partials (granules)
+    float *dbg_qkv = nullptr;      // development: layer 0's QKV rows / attention output copied out (null = off)
+    uint16_t *dbg_attn = nullptr;
+    uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
+    unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
+};
+
+// shapes the persistent step supports: H 1024, 16 q / 8 kv heads of 128, I 3072, V 3072, one workgroup per CU on a
+// 256-CU device, n_ctx <= 32 * 256 (split chunk of 64..256 positions)
+bool persist_supported(int hidden, int n_heads, int n_kv, int head_dim, int inter, int vocab, int n_ctx, int n_cu);
+size_t persist_state_bytes();                    // granule buffers + counters (zeroed once at allocation)
+void persist_carve(uint8_t *base, PersistParams &p);   // point the hand-off buffers into a zeroed state block
+bool persist_talker_step(const PersistParams &p, hipStream_t s);
+int persist_chunk(int n_ctx);                    // positions per attention split workgroup
+
+}  // namespace q3t

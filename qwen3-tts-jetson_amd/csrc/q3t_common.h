@@ -28,6 +28,13 @@ __device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_
 __device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
 __device__ __forceinline__ float f16r(float f) { return __half2float(__float2half_rn(f)); }
 
+// an f32 value the compiler must materialise as rounded: blocks fusing the producing op with its consumer (e.g. a
+// mul-sub followed by an f16 conversion becoming ONE v_fma_mixlo_f16, which rounds once instead of three times)
+__device__ __forceinline__ float opaque(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // 8 f16 (one uint4) dot 8 f16 -> f32 accumulate (v_dot2_f32_f16: exact f16 products, f32 sums)
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float dot8(const uint4 &a, const uint4 &b, float acc) {
