@@ -32,18 +32,18 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
     for (int e = 0; e < 4; ++e) { f[2 * e] = h2f(w[e] & 0xffff); f[2 * e + 1] = h2f(w[e] >> 16); }
 }
 
-template <int D, int RMAX>
+template <int D, int RMAX, int CHUNK>
 __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
     constexpr int LPP = D / 8;               // lanes per position
     constexpr int PPP = 256 / LPP;           // positions per pass
-    constexpr int NP = ATTN_CHUNK / PPP;     // passes per chunk
+    constexpr int NP = CHUNK / PPP;          // passes per chunk
     constexpr int E = D / 64;                // elements per lane in the one-wave-per-vector prologue
     const int slot = blockIdx.x, g = blockIdx.y, split = blockIdx.z;
     constexpr int R = RMAX;   // q heads per kv head
     const int pos = p.pos[slot];
-    const int j0 = split * ATTN_CHUNK;
+    const int j0 = split * CHUNK;
     if (j0 > pos) return;
-    const int nsplit = pos / ATTN_CHUNK + 1;
+    const int nsplit = pos / CHUNK + 1;
     const bool has_pos = split == nsplit - 1;   // this chunk contains the new token
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
 
@@ -283,13 +283,17 @@ bool attn_decode(const AttnParams &p, hipStream_t s) {
         set_error("attn_decode: unsupported head layout");
         return false;
     }
-    if (p.max_splits * ATTN_CHUNK < p.n_ctx || p.max_splits > ATTN_MAX_SPLITS || !p.part || !p.ticket) {
+    if ((p.chunk != 64 && p.chunk != 128) || p.max_splits * p.chunk < p.n_ctx || p.max_splits > ATTN_MAX_SPLITS || !p.part || !p.ticket) {
         set_error("attn_decode: split buffers too small");
         return false;
     }
     const dim3 grid(p.S, p.nKV, p.max_splits);
     const int R = p.nH / p.nKV;
-#define Q3T_ATTN_LAUNCH(DD, RR) hipLaunchKernelGGL((k_attn<DD, RR>), grid, dim3(256), 0, s, p)
+#define Q3T_ATTN_LAUNCH(DD, RR)                                                                      \
+    do {                                                                                             \
+        if (p.chunk == 128) hipLaunchKernelGGL((k_attn<DD, RR, 128>), grid, dim3(256), 0, s, p);     \
+        else hipLaunchKernelGGL((k_attn<DD, RR, 64>), grid, dim3(256), 0, s, p);                     \
+    } while (0)
     if (p.D == 128) {
         if (R == 1) Q3T_ATTN_LAUNCH(128, 1);
         else if (R == 2) Q3T_ATTN_LAUNCH(128, 2);

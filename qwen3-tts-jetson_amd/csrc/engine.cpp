@@ -249,6 +249,8 @@ bool Engine::alloc_state() {
     sel_ticket_ = dalloc<unsigned>((size_t)S);
     attn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
     hmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
+    xn_ = dalloc<uint16_t>((size_t)S * H);
+    parts_ = dalloc<float>((size_t)4 * S * H);
     const size_t kv_layer = (size_t)S * c_.n_kv * max_ctx_ * D;
     kc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
     vc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
@@ -344,11 +346,6 @@ bool Engine::persist_error() {
     return e != 0;
 }
 
-// ------------------------------------------------------------------------------------------ one decoder stack
-// 5 launches per layer: [RMSNorm+QKV GEMV] [head-norm+RoPE+KV-append+attention] [O GEMV + residual]
-// [RMSNorm+gate/up GEMV+SwiGLU] [down GEMV + residual]   (tts_transformer.cpp:1410-1494)
-// `in0` (optional) replaces layer 0's activation source: a gather prologue or another f32 buffer, with the raw
-// rows written to x (the residual stream) by the QKV kernel itself.
 struct StackInput {
     int pro = PRO_RMS;
     const float *x = nullptr;
@@ -356,6 +353,84 @@ struct StackInput {
     SelectSpec sel;                      // PRO_SEL_G1: selection of the gathered token
     const float *sel_logits = nullptr;
 };
+
+// ------------------------------------------------------------------------------------------ batched decoder stack
+// matrix-core path (S >= gemm_mfma_min_batch()): 7 launches per layer so that every projection fills the chip:
+//   [QKV GEMM on xn] [attention] [O GEMM, split-K slabs] [resid + RMSNorm(ffn) -> xn] [gate/up GEMM + SwiGLU]
+//   [down GEMM, split-K slabs] [resid + RMSNorm(next attn_norm | final norm) -> xn]
+// The norms are hoisted out of the GEMM prologues (each projection workgroup used to recompute the norm of its
+// tokens: ~12 us of chained double math per launch at 64 slots) and the N = 1024 projections split K four ways
+// (32 row tiles x 2 token tiles would leave 192 of 256 CUs idle).  final_norm null: no normalisation after the last
+// layer (code-predictor pass 0 has no head).
+static int splitk_for(int N, int S, int K) {
+    const int tiles = (N / 32) * ((S + 31) / 32), nch = K / 256;
+    for (int ks : {1, 2, 3, 4})
+        if (nch % ks == 0 && tiles * ks >= 256) return ks;
+    return nch % 4 == 0 ? 4 : nch % 3 == 0 ? 3 : nch % 2 == 0 ? 2 : 1;
+}
+static bool decoder_stack_mm(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
+                             float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
+                             size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
+                             unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
+                             float *final_side) {
+    const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
+    ResidNorm rn;
+    rn.S = S; rn.H = H; rn.eps = c.eps; rn.x = x; rn.xn = xn;
+    if (in0 && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
+        if (!gather_sum(in0->gs, in0->pro == PRO_RMS_G16 ? 16 : 1, S, H, x, H, s)) return false;
+    } else if (in0 && in0->x) {
+        rn.xin = in0->x;   // copied into the residual stream by the norm
+    }
+    rn.nw = layers[0].attn_norm;
+    if (!resid_norm(rn, s)) return false;
+    rn.xin = nullptr;
+    for (size_t il = 0; il < layers.size(); ++il) {
+        const DevLayer &l = layers[il];
+        GemvParams g;
+        g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
+        g.pro = PRO_F16; g.x = xn; g.ldx = H;
+        g.out_f32 = qkv; g.ldo = QKV;
+        if (!gemv(g, s)) return false;
+        AttnParams a;
+        a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
+        a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
+        a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
+        a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
+        a.part = part; a.ticket = ticket; a.out = attn;
+        if (!attn_decode(a, s)) return false;
+        GemvParams o;
+        o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
+        o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
+        o.parts = parts; o.ksplit = splitk_for(H, S, o.K);
+        if (!gemv(o, s)) return false;
+        rn.parts = parts; rn.ksplit = o.ksplit; rn.nw = l.ffn_norm; rn.side = nullptr;
+        if (!resid_norm(rn, s)) return false;
+        GemvParams gu;
+        gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
+        gu.pro = PRO_F16; gu.x = xn; gu.ldx = H;
+        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter;
+        if (!gemv(gu, s)) return false;
+        GemvParams dn;
+        dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;
+        dn.pro = PRO_F16; dn.x = hmlp; dn.ldx = c.inter;
+        dn.parts = parts; dn.ksplit = splitk_for(H, S, dn.K);
+        if (!gemv(dn, s)) return false;
+        const bool last = il + 1 == layers.size();
+        if (last && !final_norm) break;   // code-predictor pass 0: only its K/V caches are read afterwards
+        rn.parts = parts; rn.ksplit = dn.ksplit;
+        rn.nw = last ? (final_norm ? final_norm : l.ffn_norm) : layers[il + 1].attn_norm;
+        rn.side = last ? final_side : nullptr;
+        if (!resid_norm(rn, s)) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ one decoder stack
+// 5 launches per layer: [RMSNorm+QKV GEMV] [head-norm+RoPE+KV-append+attention] [O GEMV + residual]
+// [RMSNorm+gate/up GEMV+SwiGLU] [down GEMV + residual]   (tts_transformer.cpp:1410-1494)
+// `in0` (optional) replaces layer 0's activation source: a gather prologue or another f32 buffer, with the raw
+// rows written to x (the residual stream) by the QKV kernel itself.
+
 static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, float *qkv,
                           uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc, size_t kv_layer, int n_ctx,
                           int max_splits, const int *pos, const float *rope, float *part, unsigned *ticket,
@@ -457,15 +532,22 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         in0.gs.tr = trailing_; in0.gs.tr_len = trailing_len_; in0.gs.frame = frame_;
         in0.gs.tr_ld = max_trailing_ * H; in0.gs.pad = tts_pad_;
     }
-    if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_, ticket_, s,
-                       gather_input ? &in0 : nullptr))
+    const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
+    if (mm) {
+        if (!decoder_stack_mm(c_, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
+                              rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_))
+            return false;
+    } else if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_,
+                              ticket_, s, gather_input ? &in0 : nullptr)) {
         return false;
-    // final RMSNorm (hidden_states, side output) + codec_head -> logits  (:1496-1505)
+    }
+    // final RMSNorm (hidden_states, side output) + codec_head -> logits  (:1496-1505); batched: the stack's last
+    // resid_norm already normalised x into xn (and wrote hidden_)
     GemvParams h;
     h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = S;
     h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_;
+    if (mm) { h.pro = PRO_F16; h.x = xn_; h.nw = nullptr; h.side_out = nullptr; }
     h.out_f32 = logits_; h.ldo = c_.codec_vocab;
-    const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
     if (select_next && !mm) h.sel = select_spec(SEL_CB0, gp_, 1, 0);
     if (!gemv(h, s)) return false;
     if (select_next && mm) return select_tokens(select_spec(SEL_CB0, gp_, 1, 0), logits_, S, s);
@@ -499,14 +581,22 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
                 in0.sel_logits = cp_logits_;
             }
         }
-        if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1, cp_pos_ + (size_t)p * max_slots_,
-                           rope_, part_, ticket_, s, &in0, cp_fused_attn_))
+        const bool mm = S >= gemm_mfma_min_batch();
+        if (mm) {
+            if (!decoder_stack_mm(c_, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
+                                  cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
+                                  p == 0 ? nullptr : cp_out_norm_, nullptr))
+                return false;
+        } else if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
+                                  cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0, cp_fused_attn_)) {
             return false;
+        }
         if (p == 0) continue;
         const int step = p - 1;
         GemvParams h;
         h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
         h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
+        if (mm) { h.pro = PRO_F16; h.x = xn_; h.nw = nullptr; }
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
         const bool fsel = fsel_all && (!defer || step == 14);
         if (fsel) h.sel = select_spec(SEL_CP, gp_, 0, step);

@@ -133,6 +133,8 @@ private:
     unsigned *ticket_ = nullptr;   // split-attention arrival counters [S][n_kv]
     unsigned *sel_ticket_ = nullptr;   // fused head+select arrival counters [S]
     uint16_t *attn_ = nullptr, *hmlp_ = nullptr;
+    uint16_t *xn_ = nullptr;      // batched path: normalised f16 activations (resid_norm output)
+    float *parts_ = nullptr;      // batched path: split-K partial slabs [4][S][H]
     uint16_t *kc_ = nullptr, *vc_ = nullptr, *cpkc_ = nullptr, *cpvc_ = nullptr;
     int *pos_ = nullptr, *frame_ = nullptr, *done_ = nullptr, *token_ = nullptr, *tokens_ = nullptr;
     int *n_tokens_ = nullptr, *force_ = nullptr, *trailing_len_ = nullptr, *cp_pos_ = nullptr;

@@ -82,6 +82,18 @@ __device__ __forceinline__ void mm_epilogue(const GemvParams &p, int wave, int l
                 }
             }
         }
+    } else if (p.parts) {   // split-K slab: raw partial sums of this K slice, [z][token][n]
+        for (int combo = wave; combo < TT * 4; combo += (int)(blockDim.x >> 6)) {
+            const int tt = combo >> 2, q = combo & 3;
+            const int tl = tt * 32 + r;
+            if (tl >= nt) continue;
+            const int tok = t0 + tl;
+            const int n0 = row0 + 8 * q + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = sumf(tt, 4 * q + e);
+            *reinterpret_cast<float4 *>(p.parts + ((size_t)blockIdx.z * p.B + tok) * p.N + n0) = make_float4(v[0], v[1], v[2], v[3]);
+        }
     } else {
         for (int combo = wave; combo < TT * 4; combo += (int)(blockDim.x >> 6)) {
             const int tt = combo >> 2, q = combo & 3;
@@ -146,7 +158,9 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
     // every weight load of the lane: row row0 + r, k = kw0 + 64c + 32h .. +31.  Issued right after the first
     // activation loads (whose addresses must not wait behind them: vmcnt retires in issue order)
     uint4 wr[NCH][4];
-    const uint16_t *wp = p.W + (size_t)(row0 + r) * K + kw0 + h * 32;
+    // f16 rows may be one K slice of a split-K launch (grid z): the weight row stride is the full K
+    const int kz = PRO == PRO_F16 ? (int)blockIdx.z * K : 0;
+    const uint16_t *wp = p.W + (size_t)(row0 + r) * (PRO == PRO_F16 ? p.K : K) + kz + kw0 + h * 32;
     const bool dbg_now = p.dbg & 2, dbg_nox = p.dbg & 1;
     auto issue_w = [&]() {
 #pragma unroll
@@ -278,7 +292,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
         for (int tt = 0; tt < TT; ++tt) {
             const int tok = t0 + min(tt * 32 + r, nt - 1);
             const int src = p.x_idx ? p.x_idx[tok] : tok;
-            xrow[tt] = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src * p.ldx + kw0 + h * 32;
+            xrow[tt] = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src * p.ldx + kz + kw0 + h * 32;
         }
         // one ring for both operands: chunk c = 4 weight loads + 4 TT activation loads, XD chunks in flight
         constexpr int XD = NCH < (TT == 2 ? 3 : 4) ? NCH : (TT == 2 ? 3 : 4);
@@ -548,7 +562,13 @@ bool gemm_mfma_supported(const GemvParams &p) {
     const int nch = nch_of(p.K);
     if (!nch) return false;
     const bool swiglu = p.act == ACT_SWIGLU;
-    if (swiglu && p.pro != PRO_RMS) return false;
+    if (swiglu && p.pro != PRO_RMS && !(p.pro == PRO_F16 && nch <= 4 && !p.x_idx)) return false;
+    if (p.parts) {   // split-K slabs: f16 rows, no epilogue, K slices of 256-multiples
+        const int nk = p.ksplit > 0 && nch % p.ksplit == 0 ? nch / p.ksplit : 0;
+        if (p.pro != PRO_F16 || swiglu || !(nk == 1 || nk == 2 || nk == 3 || nk == 4 || nk == 8 || nk == 12) ||
+            p.N % 4 != 0)
+            return false;
+    }
     const uintptr_t xa = reinterpret_cast<uintptr_t>(p.x);
     switch (p.pro) {
         case PRO_F16: return (xa & 15) == 0 && p.ldx % 8 == 0;
@@ -580,15 +600,22 @@ static bool set_lds(const void *fn, size_t lds, bool &done) {
 }
 
 // f16 rows, one workgroup per 32 rows x 64 tokens over all of K (4 waves = 4 K-quarters)
-template <int NCH, int TT>
-static bool launch_f16(const GemvParams &p, hipStream_t s) {
+template <int NCH, int TT, bool SW>
+static bool launch_f16_sw(const GemvParams &p, hipStream_t s) {
     const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
     static bool attr = false;
-    if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma<PRO_F16, NCH, TT, false>), lds, attr)) return false;
-    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)));
-    hipLaunchKernelGGL((k_gemm_mfma<PRO_F16, NCH, TT, false>), grid, dim3(256), lds, s, p);
+    if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma<PRO_F16, NCH, TT, SW>), lds, attr)) return false;
+    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)), (unsigned)(p.parts ? p.ksplit : 1));
+    hipLaunchKernelGGL((k_gemm_mfma<PRO_F16, NCH, TT, SW>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
+}
+template <int NCH, int TT>
+static bool launch_f16(const GemvParams &p, hipStream_t s) {
+    if constexpr (NCH <= 4) {
+        if (p.act == ACT_SWIGLU) return launch_f16_sw<NCH, TT, true>(p, s);
+    }
+    return launch_f16_sw<NCH, TT, false>(p, s);
 }
 // f16 rows, split-K in 256-wide slices with atomic accumulation onto the residual stream
 template <int TT>
@@ -637,10 +664,12 @@ bool gemm_mfma(const GemvParams &p, hipStream_t s) {
         case PRO_F16: {
             const bool linear_inplace = p.act == ACT_NONE && !p.out_f16 && p.out_f32 && p.resid == p.out_f32 &&
                                         p.ldr == p.ldo && !p.aux && p.K % 256 == 0;
-            if (g_splitk && linear_inplace) return g_tt == 2 && p.B > 32 ? launch_splitk<2>(p, s) : launch_splitk<1>(p, s);
-            switch (nch_of(p.K)) {
+            if (g_splitk && linear_inplace && !p.parts) return g_tt == 2 && p.B > 32 ? launch_splitk<2>(p, s) : launch_splitk<1>(p, s);
+            const int nch = nch_of(p.K) / (p.parts ? p.ksplit : 1);
+            switch (nch) {
                 case 1: return launch_f16_tt<1>(p, s);
                 case 2: return launch_f16_tt<2>(p, s);
+                case 3: return launch_f16_tt<3>(p, s);
                 case 4: return launch_f16_tt<4>(p, s);
                 case 8: return launch_f16_tt<8>(p, s);
                 default: return launch_f16_tt<12>(p, s);

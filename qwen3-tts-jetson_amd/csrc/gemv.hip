@@ -705,6 +705,7 @@ void gemv_set_min_blocks(int n) { g_min_blocks = n > 0 ? n : 256; }
 bool gemv(const GemvParams &p, hipStream_t s) {
     if (p.B <= 0 || p.N <= 0) return true;
     if (gemm_mfma_supported(p)) return gemm_mfma(p, s);
+    if (p.parts) { set_error("gemv: split-K slabs need the matrix-core path"); return false; }
     const bool swiglu = p.act == ACT_SWIGLU;
     if (p.K % 8 != 0 || (swiglu && p.N % 32 != 0)) {
         set_error("gemv: unsupported shape N=" + std::to_string(p.N) + " K=" + std::to_string(p.K));

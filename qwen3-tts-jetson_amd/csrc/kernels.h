@@ -103,6 +103,10 @@ struct GemvParams {
     int ldo = 0;
     int orow_mul = 1, orow_add = 0;  // output row of batch b = b*orow_mul + orow_add
     int dbg = 0;                     // microbenchmark knobs (tools/dev/kbench_mm): 1 = no activation loads, 2 = no weight loads
+    // split-K partial slabs (matrix-core path, PRO_F16): grid z = ksplit K slices, slice z writes its raw partial sums
+    // to parts[z][b][n] (no epilogue); resid_norm() folds them into the residual stream
+    float *parts = nullptr;
+    int ksplit = 1;
 };
 bool gemv(const GemvParams &p, hipStream_t s);   // routes wide batches to gemm_mfma (gemm_mfma.hip)
 // matrix-core path for B >= gemm_mfma_min_batch() tokens (Q3T_MFMA_MIN_B, default 4; 0 = off): F16 / F32 / RMS / LN
@@ -124,7 +128,8 @@ struct AttnParams {
     const int *pos = nullptr;     // [S] position of the new token
     uint16_t *kc = nullptr, *vc = nullptr;  // cache base of this layer: [S][nKV][n_ctx][D] f16
     int n_ctx = 0, S = 0, nH = 0, nKV = 0, D = 0;
-    int max_splits = 1;           // grid z = ceil(n_ctx / ATTN_CHUNK)
+    int chunk = 64;               // positions per split workgroup: 64 or 128 (batched decode: fewer, fuller splits)
+    int max_splits = 1;           // grid z = ceil(n_ctx / chunk)
     float *part = nullptr;        // [S][nKV][max_splits][R][D + 2] split partials (m, l, acc)
     unsigned *ticket = nullptr;   // [S][nKV] arrival counters, zero between launches
     uint16_t *out = nullptr;      // [S][nH*D] f16 (rounded attention output, the O-proj input)
@@ -143,6 +148,23 @@ bool advance(int *pos, int *frame, int S, hipStream_t s);
 struct RowTerm { const void *ptr; int is_f16; };
 struct RowRecipe { float *out; RowTerm t[3]; };
 bool rows_recipe(const RowRecipe *recipe_dev, int n_rows, int H, hipStream_t s);
+
+// batched residual + RMSNorm between the matrix-core projections (one workgroup per token, H <= 1024):
+//   x[b] = xin[b] + parts[0][b] + ... + parts[ksplit-1][b]   (written to x when parts or xin != x)
+//   xn[b] = f16((x[b] * rsqrt(mean(x[b]^2) + eps)) * nw)       (double sums, as the GEMV prologues)
+//   side[b] = the same normalised row in f32 (optional: hidden_states side output)
+struct ResidNorm {
+    const float *xin = nullptr;
+    float *x = nullptr;
+    const float *parts = nullptr;
+    int ksplit = 0;
+    const float *nw = nullptr;
+    float eps = 1e-6f;
+    uint16_t *xn = nullptr;
+    float *side = nullptr;
+    int S = 0, H = 0;
+};
+bool resid_norm(const ResidNorm &r, hipStream_t s);
 
 // src/trt_cuda_kernels.cu drop-ins (C ABI wrappers in capi.cpp)
 void launch_f32_to_f16(const float *in, uint16_t *out, int n, hipStream_t s);

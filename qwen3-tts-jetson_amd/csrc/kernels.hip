@@ -160,4 +160,49 @@ void launch_sample_topk_f32(const float *logits, const float *rand_val, int32_t 
     hipLaunchKernelGGL(k_sample_topk_f32, dim3(1), dim3(256), 0, s, logits, rand_val, out, temperature, top_k, n);
 }
 
+// ------------------------------------------------------------------------------------------ batched residual + norm
+// one workgroup per token; thread t owns elements 4t .. 4t+3 (H <= 1024).  Partial slabs are added in slice order;
+// the RMS sum runs in double over the block (gemv.hip / gemm_mfma.hip prologue numerics).
+__global__ void __launch_bounds__(256) k_resid_norm(const ResidNorm r) {
+    __shared__ double scr[4];
+    const int b = blockIdx.x, t = threadIdx.x, k = 4 * t;
+    const bool ok = k < r.H;
+    const size_t o = (size_t)b * r.H + (ok ? k : 0);
+    float4 x = *reinterpret_cast<const float4 *>((r.xin ? r.xin : r.x) + o);
+    float4 pz[8];
+    const int ks = r.parts ? r.ksplit : 0;
+#pragma unroll
+    for (int z = 0; z < 8; ++z)
+        if (z < ks) pz[z] = *reinterpret_cast<const float4 *>(r.parts + (size_t)z * r.S * r.H + o);
+#pragma unroll
+    for (int z = 0; z < 8; ++z)
+        if (z < ks) x = make_float4(x.x + pz[z].x, x.y + pz[z].y, x.z + pz[z].z, x.w + pz[z].w);
+    if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok && (ks > 0 || (r.xin && r.xin != r.x))) *reinterpret_cast<float4 *>(r.x + o) = x;
+    double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);
+    ss = wave_sum_d(ss);
+    if ((t & 63) == 0) scr[t >> 6] = ss;
+    __syncthreads();
+    ss = (scr[0] + scr[1]) + (scr[2] + scr[3]);
+    if (!ok) return;
+    const float scale = 1.0f / sqrtf((float)(ss / r.H) + r.eps);
+    const float4 w = *reinterpret_cast<const float4 *>(r.nw + k);
+    const float y0 = (x.x * scale) * w.x, y1 = (x.y * scale) * w.y, y2 = (x.z * scale) * w.z, y3 = (x.w * scale) * w.w;
+    if (r.side) *reinterpret_cast<float4 *>(r.side + o) = make_float4(y0, y1, y2, y3);
+    uint2 h;
+    h.x = (uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16);
+    h.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
+    *reinterpret_cast<uint2 *>(r.xn + o) = h;
+}
+bool resid_norm(const ResidNorm &r, hipStream_t s) {
+    if (r.S <= 0) return true;
+    if (r.H > 1024 || r.H % 4 != 0 || !r.x || !r.nw || !r.xn || (r.parts && (r.ksplit < 1 || r.ksplit > 8))) {
+        set_error("resid_norm: unsupported shape");
+        return false;
+    }
+    hipLaunchKernelGGL(k_resid_norm, dim3(r.S), dim3(256), 0, s, r);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 }  // namespace q3t
