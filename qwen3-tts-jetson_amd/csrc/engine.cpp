@@ -59,6 +59,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     defer_cp_select_ = env_flag("Q3T_CP_DEFER_SELECT", true);
     fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
     persist_ = env_flag("Q3T_PERSIST", true);
+    persist_cp_env_ = env_flag("Q3T_PERSIST_CP", true);
     if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
@@ -304,6 +305,19 @@ bool Engine::setup_persist() {
     pstate_ = dalloc<uint8_t>(persist_state_bytes());
     if (!pl_dev_ || !pstate_) { set_error("device allocation failed"); return false; }
     Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+    // the code-predictor frame (persist_cp_frame): its 5 layers and 15 lm_heads
+    persist_cp_ = persist_cp_env_ && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15;
+    if (persist_cp_) {
+        std::vector<PLayerW> cpl(CP_.size());
+        for (size_t i = 0; i < CP_.size(); ++i)
+            cpl[i] = PLayerW{CP_[i].qkv, CP_[i].o, CP_[i].gu, CP_[i].down, CP_[i].attn_norm, CP_[i].ffn_norm, CP_[i].qn, CP_[i].kn};
+        pl_cp_dev_ = dalloc<PLayerW>(cpl.size());
+        heads_dev_ = dalloc<const uint16_t *>(16);
+        if (!pl_cp_dev_ || !heads_dev_) { set_error("device allocation failed"); return false; }
+        Q3T_HIP(hipMemcpy(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+        std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
+        Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
+    }
     Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
     return true;
@@ -565,6 +579,18 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
     // vector path with fused selection: heads 0..13 only produce logits; the next pass's QKV launch selects the token
     // in every workgroup while its weights stream (PRO_SEL_G1), so the head's 256 -> 1 arrival chain and the serial
     // selection leave the critical path.  Head 14 (its token feeds the next talker step) keeps the fused selection.
+    if (S == 1 && persist_ && persist_cp_ && !logits_host) {   // the whole frame as one persistent launch
+        PersistParams p;
+        persist_carve(pstate_, p);
+        p.L = pl_cp_dev_; p.n_layers = c_.cp_layers; p.eps = c_.eps;
+        p.x_in = hidden_;
+        p.gs.tok = tokens_; p.gs.tok_ld = 16; p.gs.tabs = tabs16_dev_;
+        p.rope = rope_; p.kc = cpkc_; p.vc = cpvc_; p.kv_layer = kv_layer; p.n_ctx = 16;
+        p.heads = heads_dev_; p.out_norm = cp_out_norm_; p.logits = cp_logits_;
+        p.sel = select_spec(SEL_CP, gp_, 0, 0);
+        p.prof = pprof_;
+        return persist_cp_frame(p, s);
+    }
     const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
     const bool defer = fsel_all && defer_cp_select_;
     for (int p = 0; p < 16; ++p) {

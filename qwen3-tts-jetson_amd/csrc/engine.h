@@ -156,7 +156,9 @@ private:
     bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
     bool defer_cp_select_ = true; // Q3T_CP_DEFER_SELECT=0: code-predictor tokens selected in the head launch
     bool persist_ = true;         // Q3T_PERSIST=0: launch-per-phase talker step at one slot (no persistent kernel)
-    PLayerW *pl_dev_ = nullptr;
+    PLayerW *pl_dev_ = nullptr, *pl_cp_dev_ = nullptr;
+    const uint16_t **heads_dev_ = nullptr;
+    bool persist_cp_ = false, persist_cp_env_ = true;     // Q3T_PERSIST_CP=0: code-predictor frame as per-op launches
     uint8_t *pstate_ = nullptr;
     uint64_t *pprof_ = nullptr;   // Q3T_PERSIST_PROF: persistent-step timeline (dev)
 

@@ -14,7 +14,7 @@
 
 namespace q3t {
 
-constexpr int PROF_PH = 160;   // timeline phases recorded per workgroup (5 per layer + head)
+constexpr int PROF_PH = 448;   // timeline phases recorded per workgroup (5 per layer + head)
 
 struct PLayerW {
     const uint16_t *qkv, *o, *gu, *down;
@@ -45,6 +45,8 @@ struct PersistParams {
     // hand-off state (persist_alloc)
     uint64_t *gx = nullptr, *gx2 = nullptr, *gqkv = nullptr, *gattn = nullptr, *gh = nullptr;
     uint64_t *gpart = nullptr;     // [8][32][264] attention split partials (granules)
+    uint64_t *gtok = nullptr;      // [16] code-predictor tokens of the launch (granules)
+    const uint16_t *const *heads = nullptr;   // code-predictor frame: device array of the 15 lm_heads
     float *dbg_qkv = nullptr;      // development: layer 0's QKV rows / attention output copied out (null = off)
     uint16_t *dbg_attn = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
@@ -57,6 +59,11 @@ bool persist_supported(int hidden, int n_heads, int n_kv, int head_dim, int inte
 size_t persist_state_bytes();                    // granule buffers + counters (zeroed once at allocation)
 void persist_carve(uint8_t *base, PersistParams &p);   // point the hand-off buffers into a zeroed state block
 bool persist_talker_step(const PersistParams &p, hipStream_t s);
+// the 16-pass code-predictor frame of one slot as one launch (same hand-off protocol): p.L = the 5 code-predictor
+// layers, x_in = the talker hidden state, gs.tok = the frame's codes (CB0 in column 0), gs.tabs = the 16 embedding
+// tables, kc/vc = the 16-position code-predictor caches, heads = lm_head[0..14], out_norm, logits [2048],
+// sel = SEL_CP (step set per pass)
+bool persist_cp_frame(const PersistParams &p, hipStream_t s);
 int persist_chunk(int n_ctx);                    // positions per attention split workgroup
 
 }  // namespace q3t

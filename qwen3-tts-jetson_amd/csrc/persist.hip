@@ -56,7 +56,12 @@ __device__ __forceinline__ uint64_t g_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_sc1f(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ float ld_sc1f(const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two agent-scope (L1-bypassing) 8-B loads
+    uint64_t *q = reinterpret_cast<uint64_t *>(const_cast<uint16_t *>(p));
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
 
 struct Ctl {
     unsigned *err;
@@ -112,7 +117,8 @@ struct Lds {
     unsigned last;
     SelLds sel;
     float pl[MAXSPLIT * 264];    // split-0 combiner: every split's partial, split order
-    PLayerW layers[MAXL];        // the layer pointer table, copied once: a pointer fetched from global memory inside
+    PLayerW layers[MAXL];
+    const uint16_t *heads[16];   // code-predictor lm_heads (MODE 1)        // the layer pointer table, copied once: a pointer fetched from global memory inside
                                  // the chain would make the next wait cover every weight stream in flight (vmcnt order)
 };
 
@@ -156,8 +162,13 @@ __device__ __forceinline__ void issue_rows_ks4(const uint16_t *W, int K, int row
     for (int tt = 0; tt < NC; ++tt) w[tt] = ld16(r + tt * 128);
 }
 
-template <int CH>
-__global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
+// MODE 0: the talker step (one pass of n_layers at p.pos[0], codec head, CB0 selection).
+// MODE 1: the whole code-predictor frame (trt_code_predictor.cpp:484-600): 16 passes of the 5 layers, pass q at KV
+// position q (16-position cache, always one split), pass q >= 1 ends with lm_head[q-1] + token selection by the last
+// workgroup, whose token (a granule) feeds the next pass's embedding gather.  K/V rows written by an earlier pass of
+// the same launch are read back by the same workgroup with sc1 loads (no stale L1 line).
+template <int MODE, int CH>
+__global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Lds &S = *reinterpret_cast<Lds *>(smem);
     constexpr int NP = CH / 16;   // positions per lane group pass (16 lanes per position, 16 positions per pass)
@@ -166,8 +177,10 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
     Ctl c{p.err, false};
     const unsigned seq = __hip_atomic_load(p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     auto TAG = [&](int ph) -> uint32_t { return ((seq * 1024u + (unsigned)ph) << 1) | 1u; };
-    const int pos = p.pos[0];
-    const int nsplit = pos / CH + 1;
+    int pos = MODE == 0 ? p.pos[0] : 0;
+    const int nsplit = MODE == 0 ? pos / CH + 1 : 1;
+    const int nl = p.n_layers, npass = MODE == 0 ? 1 : 16, PPH = 5 * nl + 1;   // phases per pass
+    constexpr int RPW = MODE == 0 ? 12 : 8;                                    // head rows per workgroup
     const int ag = w & (NKV - 1), as = w >> 3;   // attention role: kv group, split
     const bool att = as < nsplit;
     const bool has_pos = as == nsplit - 1;
@@ -184,30 +197,39 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
     //   wq(l+1) after D(l)'s input, K/V(l+1) after E(l)'s, wo(l) after A(l)'s, gate/up(l) after B(l)'s, wd(l) after C(l)'s
     const int gu_unit = w * 12 + min(grp, 11);
     const int gu_row = (gu_unit >> 4) * 32 + (gu_unit & 15);
-    auto issue_kv = [&](int layer) {   // this split's cached K/V rows (clamped rows re-read row pos, masked later)
+    auto issue_kv = [&](int layer, int kpos) {   // this split's cached K/V rows (clamped rows re-read row kpos)
         const size_t o = (size_t)layer * p.kv_layer + (size_t)ag * p.n_ctx * D;
         const int j0 = as * CH;
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
-            const int j = min(j0 + pi * 16 + pg, pos);
-            kr[pi] = ld16(p.kc + o + (size_t)j * D + li * 8);
-            vr[pi] = ld16(p.vc + o + (size_t)j * D + li * 8);
+            const int j = min(j0 + pi * 16 + pg, kpos);
+            if constexpr (MODE == 1) {
+                kr[pi] = ld16_sc1(p.kc + o + (size_t)j * D + li * 8);
+                vr[pi] = ld16_sc1(p.vc + o + (size_t)j * D + li * 8);
+            } else {
+                kr[pi] = ld16(p.kc + o + (size_t)j * D + li * 8);
+                vr[pi] = ld16(p.vc + o + (size_t)j * D + li * 8);
+            }
         }
     };
     if (t < p.n_layers) S.layers[t] = p.L[t];
+    if (MODE == 1 && t < 15) S.heads[t] = p.heads[t];
     issue_rows_k1024(p.L[0].qkv, w * 16 + grp, wq);
-    if (att) issue_kv(0);
+    if (att) issue_kv(0, pos);
     float4 nwA = ldf4(p.L[0].attn_norm + 4 * t), nwD;   // attn_norm(l) / ffn_norm(l) for this thread's 4 elements
     float hn[2], rp[2];                                  // attention: head-norm weights and RoPE (cos, sin) of this lane
 
-    for (int l = 0; l < p.n_layers; ++l) {
-        if (l == 0) __syncthreads();   // layer table visible
+    __syncthreads();   // layer / head tables visible
+    for (int pass = 0, ph0 = 0; pass < npass; ++pass, ph0 += PPH) {
+    const bool head_here = MODE == 0 || pass > 0;
+    if (MODE == 1) pos = pass;
+    for (int l = 0; l < nl; ++l) {
         const PLayerW Lw = S.layers[l];
         const size_t kvo = (size_t)l * p.kv_layer + (size_t)ag * p.n_ctx * D;
         // ================= A: x -> RMSNorm -> QKV rows
         float4 x;
         if (l == 0) {
-            if (p.gather) {
+            if (MODE == 0 && p.gather) {
                 const GatherSum &gs = p.gs;
                 const int *tk = gs.tok;
                 uint2 hv[16];
@@ -221,14 +243,23 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
 #pragma unroll
                 for (int j = 1; j < 16; ++j) { const float4 b = h4(hv[j]); x = make_float4(x.x + b.x, x.y + b.y, x.z + b.z, x.w + b.w); }
                 x = make_float4(x.x + ex.x, x.y + ex.y, x.z + ex.z, x.w + ex.w);
-            } else {
+            } else if (MODE == 0 || pass == 0) {
                 x = ldf4(p.x_in + 4 * t);
+            } else {   // code-predictor pass input: table row of the previous pass's token (pass 1: CB0)
+                int tok = p.gs.tok[0];
+                if (pass >= 2) {
+                    uint32_t u1[1];
+                    g_wait<1>(p.gtok + pass - 1, TAG(ph0 - 1), u1, c);
+                    tok = (int)u1[0];
+                }
+                const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
+                x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
             }
         } else {
             uint32_t u[4];
-            PROF(5 * l + 0, 0);
-            g_wait<4>(p.gx + 4 * t, TAG(5 * (l - 1) + 4), u, c);
-            PROF(5 * l + 0, 1);
+            PROF(ph0 + 5 * l + 0, 0);
+            g_wait<4>(p.gx + 4 * t, TAG(ph0 + 5 * (l - 1) + 4), u, c);
+            PROF(ph0 + 5 * l + 0, 1);
             x = f4_of(u);
         }
         if (att) {
@@ -243,14 +274,14 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
         *reinterpret_cast<float4 *>(S.xr + 4 * t) = x;
         rms_to_lds(x, nwA, p.eps, S, nullptr);
         __syncthreads();
-        if (l > 0) PROF(5 * l + 0, 3);
+        if (l > 0) PROF(ph0 + 5 * l + 0, 3);
         {
             float acc = 0.0f;
 #pragma unroll
             for (int tt = 0; tt < 8; ++tt) acc = dot8(wq[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), acc);
             acc = group_sum<16>(acc);
-            if (l16 == 0) g_put(p.gqkv + w * 16 + grp, __float_as_uint(acc), TAG(5 * l + 0));
-            PROF(5 * l + 0, 2);
+            if (l16 == 0) g_put(p.gqkv + w * 16 + grp, __float_as_uint(acc), TAG(ph0 + 5 * l + 0));
+            PROF(ph0 + 5 * l + 0, 2);
         }
         // ================= B: attention (kv group ag, split as)
         if (!att) {
@@ -261,9 +292,9 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
             {
                 uint32_t u[2];
                 const int gi = t < 128 ? ag * 256 + 2 * t : t < 192 ? NH * D + ag * D + 2 * (t - 128) : (NH + NKV) * D + ag * D + 2 * (t - 192);
-                PROF(5 * l + 1, 0);
-                g_wait<2>(p.gqkv + gi, TAG(5 * l + 0), u, c);
-                PROF(5 * l + 1, 1);
+                PROF(ph0 + 5 * l + 1, 0);
+                g_wait<2>(p.gqkv + gi, TAG(ph0 + 5 * l + 0), u, c);
+                PROF(ph0 + 5 * l + 1, 1);
                 nwD = ldf4(Lw.ffn_norm + 4 * t);
                 issue_rows_k1024(Lw.gu, gu_row, wg);
                 issue_rows_k1024(Lw.gu, gu_row + 16, wu);
@@ -397,7 +428,7 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
                     const int h = t / (D / 2), d = 2 * (t % (D / 2));
                     const float a0 = (S.ared[0][h][d] + S.ared[1][h][d]) + (S.ared[2][h][d] + S.ared[3][h][d]);
                     const float a1 = (S.ared[0][h][d + 1] + S.ared[1][h][d + 1]) + (S.ared[2][h][d + 1] + S.ared[3][h][d + 1]);
-                    g_put(gout + t, (uint32_t)f2h(a0 / Lsum[h]) | ((uint32_t)f2h(a1 / Lsum[h]) << 16), TAG(5 * l + 1));
+                    g_put(gout + t, (uint32_t)f2h(a0 / Lsum[h]) | ((uint32_t)f2h(a1 / Lsum[h]) << 16), TAG(ph0 + 5 * l + 1));
                     if (p.dbg_attn && l == 0) {
                         p.dbg_attn[(ag * R + h) * D + d] = f2h(a0 / Lsum[h]);
                         p.dbg_attn[(ag * R + h) * D + d + 1] = f2h(a1 / Lsum[h]);
@@ -421,11 +452,11 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
                     {
                         const int h = t / D, d = t % D;
                         const float a = (S.ared[0][h][d] + S.ared[1][h][d]) + (S.ared[2][h][d] + S.ared[3][h][d]);
-                        g_put(mine + t, __float_as_uint(a), TAG(5 * l + 1));
+                        g_put(mine + t, __float_as_uint(a), TAG(ph0 + 5 * l + 1));
                     }
                     if (t < PSLOT - R * D) {
                         const float v = t < R ? M[t] : t < 2 * R ? Lsum[t - R] : 0.0f;
-                        g_put(mine + R * D + t, __float_as_uint(v), TAG(5 * l + 1));
+                        g_put(mine + R * D + t, __float_as_uint(v), TAG(ph0 + 5 * l + 1));
                     }
                 } else {
                     {
@@ -436,7 +467,7 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
                     const int n = (nsplit - 1) * PSLOT;
                     for (int i0 = 4 * t; i0 < n; i0 += 1024) {
                         uint32_t u4[4];
-                        g_wait<4>(gp + PSLOT + i0, TAG(5 * l + 1), u4, c);
+                        g_wait<4>(gp + PSLOT + i0, TAG(ph0 + 5 * l + 1), u4, c);
 #pragma unroll
                         for (int q = 0; q < 4; ++q) pl[PSLOT + i0 + q] = __uint_as_float(u4[q]);
                     }
@@ -465,18 +496,18 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
                             for (int s2 = 0; s2 < nsplit; ++s2) a = __fmaf_rn(pl[s2 * PSLOT + h * D + d + q], S.sw[s2][h], a);
                             a2[q] = a;
                         }
-                        g_put(gout + t, (uint32_t)f2h(a2[0] / S.cl[h]) | ((uint32_t)f2h(a2[1] / S.cl[h]) << 16), TAG(5 * l + 1));
+                        g_put(gout + t, (uint32_t)f2h(a2[0] / S.cl[h]) | ((uint32_t)f2h(a2[1] / S.cl[h]) << 16), TAG(ph0 + 5 * l + 1));
                     }
                 }
             }
         }
-        PROF(5 * l + 1, 2);
+        PROF(ph0 + 5 * l + 1, 2);
         // ================= C: O-proj + residual -> x'
         {
             uint32_t u[4];
-            PROF(5 * l + 2, 0);
-            g_wait<4>(p.gattn + 4 * t, TAG(5 * l + 1), u, c);
-            PROF(5 * l + 2, 1);
+            PROF(ph0 + 5 * l + 2, 0);
+            g_wait<4>(p.gattn + 4 * t, TAG(ph0 + 5 * l + 1), u, c);
+            PROF(ph0 + 5 * l + 2, 1);
             issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
             __syncthreads();
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
@@ -491,25 +522,32 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
             if (t < 4) {
                 const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
                 const int row = w * 4 + t;
-                g_put(p.gx2 + row, __float_as_uint(S.xr[row] + s), TAG(5 * l + 2));
+                g_put(p.gx2 + row, __float_as_uint(S.xr[row] + s), TAG(ph0 + 5 * l + 2));
             }
-            PROF(5 * l + 2, 2);
+            PROF(ph0 + 5 * l + 2, 2);
         }
         // ================= D: RMSNorm(ffn_norm) + gate/up + SwiGLU -> h
         {
             uint32_t u[4];
-            PROF(5 * l + 3, 0);
-            g_wait<4>(p.gx2 + 4 * t, TAG(5 * l + 2), u, c);
-            PROF(5 * l + 3, 1);
-            nwA = ldf4((l + 1 < p.n_layers ? S.layers[l + 1].attn_norm : p.out_norm) + 4 * t);
-            if (l + 1 < p.n_layers) issue_rows_k1024(S.layers[l + 1].qkv, w * 16 + grp, wq);
-            else issue_rows_k1024(p.head, w * 12 + min(grp, 11), wq);
+            PROF(ph0 + 5 * l + 3, 0);
+            g_wait<4>(p.gx2 + 4 * t, TAG(ph0 + 5 * l + 2), u, c);
+            PROF(ph0 + 5 * l + 3, 1);
+            if (l + 1 < nl) {
+                nwA = ldf4(S.layers[l + 1].attn_norm + 4 * t);
+                issue_rows_k1024(S.layers[l + 1].qkv, w * 16 + grp, wq);
+            } else if (head_here) {
+                nwA = ldf4(p.out_norm + 4 * t);
+                issue_rows_k1024(MODE == 0 ? p.head : S.heads[pass - 1], w * RPW + min(grp, RPW - 1), wq);
+            } else {   // code-predictor pass 0 (no head): the next pass's layer 0
+                nwA = ldf4(S.layers[0].attn_norm + 4 * t);
+                issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
+            }
             const float4 x2 = f4_of(u);
             __syncthreads();
             *reinterpret_cast<float4 *>(S.xr2 + 4 * t) = x2;
             rms_to_lds(x2, nwD, p.eps, S, nullptr);
             __syncthreads();
-            PROF(5 * l + 3, 3);
+            PROF(ph0 + 5 * l + 3, 3);
             float a0 = 0.0f, a1 = 0.0f, b0 = 0.0f, b1 = 0.0f;   // gate / up, K halves 0 and 1
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt) {
@@ -527,16 +565,17 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
             b0 = group_sum<16>(b0); b1 = group_sum<16>(b1);
             if (l16 == 0 && grp < 12) S.hs[grp] = silu_f(a0 + a1) * (b0 + b1);
             __syncthreads();
-            if (t < 6) g_put(p.gh + w * 6 + t, (uint32_t)f2h(S.hs[2 * t]) | ((uint32_t)f2h(S.hs[2 * t + 1]) << 16), TAG(5 * l + 3));
-            PROF(5 * l + 3, 2);
+            if (t < 6) g_put(p.gh + w * 6 + t, (uint32_t)f2h(S.hs[2 * t]) | ((uint32_t)f2h(S.hs[2 * t + 1]) << 16), TAG(ph0 + 5 * l + 3));
+            PROF(ph0 + 5 * l + 3, 2);
         }
         // ================= E: down + residual -> x (next layer input)
         {
             uint32_t u[6];
-            PROF(5 * l + 4, 0);
-            g_wait<6>(p.gh + 6 * t, TAG(5 * l + 3), u, c);
-            PROF(5 * l + 4, 1);
-            if (att && l + 1 < p.n_layers) issue_kv(l + 1);
+            PROF(ph0 + 5 * l + 4, 0);
+            g_wait<6>(p.gh + 6 * t, TAG(ph0 + 5 * l + 3), u, c);
+            PROF(ph0 + 5 * l + 4, 1);
+            if (att && l + 1 < nl) issue_kv(l + 1, pos);
+            else if (att && !head_here && pass + 1 < npass) issue_kv(0, pos + 1);
             __syncthreads();
             *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
@@ -552,46 +591,65 @@ __global__ void __launch_bounds__(256) k_talker_persist(const PersistParams p) {
             if (t < 4) {
                 const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
                 const int row = w * 4 + t;
-                g_put(p.gx + row, __float_as_uint(S.xr2[row] + s), TAG(5 * l + 4));
+                g_put(p.gx + row, __float_as_uint(S.xr2[row] + s), TAG(ph0 + 5 * l + 4));
             }
-            PROF(5 * l + 4, 2);
+            PROF(ph0 + 5 * l + 4, 2);
         }
     }
-    // ================= head: RMSNorm(output_norm) -> hidden (side output) -> codec head logits -> CB0 selection
-    {
+    // ================= head: RMSNorm(output_norm) -> hidden (side output) -> codec head / lm_head logits -> selection
+    if (head_here) {
         uint32_t u[4];
-        PROF(5 * p.n_layers, 0);
-        g_wait<4>(p.gx + 4 * t, TAG(5 * (p.n_layers - 1) + 4), u, c);
-        PROF(5 * p.n_layers, 1);
+        const int hph = ph0 + 5 * nl;
+        PROF(hph, 0);
+        g_wait<4>(p.gx + 4 * t, TAG(ph0 + 5 * (nl - 1) + 4), u, c);
+        PROF(hph, 1);
         const float4 x = f4_of(u);
         __syncthreads();
         rms_to_lds(x, nwA, p.eps, S, w == 0 ? p.hidden : nullptr);
         __syncthreads();
+        // head rows are in registers now: the next pass's layer-0 streams can follow
+        uint4 wh[8];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) wh[tt] = wq[tt];
+        if (MODE == 1 && pass + 1 < npass) {
+            nwA = ldf4(S.layers[0].attn_norm + 4 * t);
+            issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
+            if (att) issue_kv(0, pos + 1);
+        }
         float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll
-        for (int tt = 0; tt < 4; ++tt) a0 = dot8(wq[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a0);
+        for (int tt = 0; tt < 4; ++tt) a0 = dot8(wh[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a0);
 #pragma unroll
-        for (int tt = 4; tt < 8; ++tt) a1 = dot8(wq[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a1);
+        for (int tt = 4; tt < 8; ++tt) a1 = dot8(wh[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a1);
         a0 = group_sum<16>(a0);
         a1 = group_sum<16>(a1);
-        if (l16 == 0 && grp < 12) st_sc1f(p.logits + w * 12 + grp, a0 + a1);
+        if (l16 == 0 && grp < RPW) st_sc1f(p.logits + w * RPW + grp, a0 + a1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        PROF(5 * p.n_layers, 2);
+        PROF(hph, 2);
         if (t == 0) S.last = __hip_atomic_fetch_add(p.head_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(G - 1);
         __syncthreads();
         if (S.last) {
-            if (p.sel.mode != SEL_NONE) select_slot<true>(p.sel, p.logits, 0, S.sel);
+            int tok = -1;
+            SelectSpec sp = p.sel;
+            if (MODE == 1) sp.step = pass - 1;
+            if (sp.mode != SEL_NONE) tok = select_token<true>(sp, p.logits, 0, S.sel);
             if (t == 0) {
+                if (tok >= 0) select_commit(sp, 0, tok);
                 __hip_atomic_store(p.head_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(p.seq, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (pass + 1 == npass) __hip_atomic_store(p.seq, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (MODE == 1 && pass + 1 < npass) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // ticket reset lands before the token
+                    g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
+                }
             }
         }
     }
+    }   // passes
 }
 
 struct StateLayout {
-    size_t gx, gx2, gqkv, gattn, gh, part, gpart, ctr, total;
+    size_t gx, gx2, gqkv, gattn, gh, part, gpart, gtok, ctr, total;
     StateLayout() {
         size_t o = 0;
         auto take = [&](size_t b) { const size_t r = o; o += (b + 255) & ~(size_t)255; return r; };
@@ -602,6 +660,7 @@ struct StateLayout {
         gh = take(INTER / 2 * 8);
         part = take((size_t)NKV * MAXSPLIT * R * (D + 2) * 4);
         gpart = take((size_t)NKV * MAXSPLIT * PSLOT * 8);
+        gtok = take(16 * 8);
         ctr = take(64 * 4);
         total = o;
     }
@@ -631,6 +690,7 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.gh = reinterpret_cast<uint64_t *>(base + L.gh);
     p.part = reinterpret_cast<float *>(base + L.part);
     p.gpart = reinterpret_cast<uint64_t *>(base + L.gpart);
+    p.gtok = reinterpret_cast<uint64_t *>(base + L.gtok);
     unsigned *ctr = reinterpret_cast<unsigned *>(base + L.ctr);
     p.seq = ctr;               // [0]
     p.head_ticket = ctr + 16;  // own 64-B line
@@ -638,16 +698,16 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.ticket = ctr + 48;       // [8]
 }
 
-template <int CH>
+template <int MODE, int CH>
 static bool launch_ch(const PersistParams &p, hipStream_t s) {
     const size_t lds = std::max(sizeof(Lds), (size_t)96 * 1024);   // > 80 KB: one workgroup per CU
     static bool attr = false;
     if (!attr) {
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_talker_persist<CH>),
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_persist<MODE, CH>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = true;
     }
-    hipLaunchKernelGGL((k_talker_persist<CH>), dim3(G), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_persist<MODE, CH>), dim3(G), dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
 }
@@ -660,12 +720,21 @@ bool persist_talker_step(const PersistParams &p, hipStream_t s) {
         return false;
     }
     switch (persist_chunk(p.n_ctx)) {
-        case 64: return launch_ch<64>(p, s);
-        case 128: return launch_ch<128>(p, s);
-        case 192: return launch_ch<192>(p, s);
-        case 256: return launch_ch<256>(p, s);
+        case 64: return launch_ch<0, 64>(p, s);
+        case 128: return launch_ch<0, 128>(p, s);
+        case 192: return launch_ch<0, 192>(p, s);
+        case 256: return launch_ch<0, 256>(p, s);
         default: set_error("persist_talker_step: context too long"); return false;
     }
+}
+
+bool persist_cp_frame(const PersistParams &p, hipStream_t s) {
+    if (!p.L || p.n_layers <= 0 || p.n_layers > MAXL || !p.heads || !p.logits || !p.rope || !p.kc || !p.vc || !p.gx ||
+        !p.x_in || !p.gs.tok || !p.gs.tabs || p.n_ctx != 16 || p.sel.mode != SEL_CP || p.sel.V != 2048) {
+        set_error("persist_cp_frame: bad parameters");
+        return false;
+    }
+    return launch_ch<1, 16>(p, s);
 }
 
 }  // namespace q3t

@@ -20,16 +20,20 @@ pytestmark = pytest.mark.gpu
 
 
 def _engine(tts, tok, persist, **kw):
+    """persist=False: the launch-per-op graphs, with the code predictor's attention as its own k_attn launch
+    (Q3T_CP_FUSED_ATTN=0), whose arithmetic the persistent frame reproduces bit for bit"""
     import q3t
-    old = os.environ.get("Q3T_PERSIST")
-    os.environ["Q3T_PERSIST"] = "1" if persist else "0"
+    env = {"Q3T_PERSIST": "1" if persist else "0", "Q3T_CP_FUSED_ATTN": "1" if persist else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return q3t.Engine(tts, tok, device=0, **kw)
     finally:
-        if old is None:
-            del os.environ["Q3T_PERSIST"]
-        else:
-            os.environ["Q3T_PERSIST"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -56,6 +60,21 @@ def test_talker_step_bit_exact(engines):
         if not (np.array_equal(hp, hg) and np.array_equal(lp, lg)):
             bad.append((pos, float(np.abs(hp - hg).max()), float(np.abs(lp - lg).max())))
     assert not bad, (len(bad), bad[:8])
+    assert ep.persist_status() == 0
+
+
+@pytest.mark.parametrize("temperature", [0.0, 0.9])
+def test_cp_frame_bit_exact(engines, temperature):
+    """the 16-pass code-predictor frame as one persistent launch vs 16 x (5 layers + head + selection) launches"""
+    ep, eg = engines
+    H = ep.cfg["hidden"]
+    rng = np.random.default_rng(21)
+    for frame in range(12):
+        hid = (rng.standard_normal(H) * 1.5).astype(np.float32)
+        cb0 = int(rng.integers(0, 2048))
+        cp = ep.codepred_frame(hid[None], [cb0], temperature=temperature, top_k=50, seed=3, frame=frame)
+        cg = eg.codepred_frame(hid[None], [cb0], temperature=temperature, top_k=50, seed=3, frame=frame)
+        assert np.array_equal(cp, cg), (frame, cp, cg)
     assert ep.persist_status() == 0
 
 
