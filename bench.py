@@ -268,7 +268,8 @@ def main():
                 "breakdown_ms_per_step": {k: round(v, 1) for k, v in stats.items()},
                 "talker_step_ms": round(bt, 4), "cp_frame_ms": round(bc, 4),
                 "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots "
-                                                       "(MFMA projections + batched split-K attention)",
+                                                       "(MFMA f16 GEMMs on hoisted norms, split-K slabs, batched split-K "
+                                                       "attention: 7 launches per layer)",
                              "achieved": round(b_bytes / (bt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(b_bytes / (bt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": pmc_traffic(batched)[0], "traffic_source": pmc_traffic(batched)[1],
@@ -289,8 +290,9 @@ def main():
             "x_realtime": round(args.frames * FRAME_SEC * B / (ms_per_step / 1e3), 1),
             "breakdown_ms_per_step": {k: round(v / args.steps, 2) for k, v in main_stats.items()},
             "talker_step_ms": round(t_talker, 4), "cp_frame_ms": round(t_cp, 4),
-            "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid} (28 layers + codec head: "
-                                                  "141 kernels, one hipGraph replay)",
+            "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid} (28 layers + codec head + "
+                                                  "CB0 selection: ONE persistent launch, k_persist<0,64>, persist.hip)"
+                                                  if B == 1 else f"talker decode step at KV position {p_mid}, {B} slots",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(B)[0],
                          "traffic_source": pmc_traffic(B)[1],

@@ -8,6 +8,7 @@ import sys
 
 
 def short(n):
+    n = n.replace("(anonymous namespace)::", "")
     n = re.sub(r"\(.*", "", n)
     return n[:110]
 
