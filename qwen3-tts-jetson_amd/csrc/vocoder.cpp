@@ -246,6 +246,7 @@ bool Vocoder::ensure(int F) {
         big = std::max(big, (size_t)T * dec_[d].ct.oc);
     }
     for (int i = 0; i < 3; ++i) if (!(buf_[i] = (float *)alloc(big * 4))) { set_error("vocoder scratch alloc"); return false; }
+    if (!(xh_ = (uint16_t *)alloc(big * 2))) { set_error("vocoder scratch alloc"); return false; }
     codes_ = (int32_t *)alloc((size_t)F * 16 * 4);
     cols_ = (int *)alloc((size_t)F * 16 * 4);
     pcm_ = (float *)alloc((size_t)std::max<int64_t>(full_len(F), (int64_t)F * 1920) * 4);
@@ -272,7 +273,12 @@ bool Vocoder::run_conv(const Conv &c, const float *x, int T, int pad, int dil, c
                        const float *resid, int act, hipStream_t s) {
     ConvParams p;
     p.x = x; p.T_in = T; p.C_in = c.ic;
-    if (sn) { p.snake_a = sn->a; p.snake_ib = sn->ib; }
+    if (c.ic % 8 == 0) {   // SnakeBeta + f16 rounding once per element, not once per output tile and tap window
+        if (!snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, T, c.ic, s)) return false;
+        p.xh = xh_;
+    } else if (sn) {
+        p.snake_a = sn->a; p.snake_ib = sn->ib;
+    }
     p.n_taps = c.k;
     for (int j = 0; j < c.k; ++j) p.taps[j] = ConvTap{c.w + (size_t)j * c.oc * c.ic, j * dil - pad};
     p.dmin = -pad; p.dmax = (c.k - 1) * dil - pad;
@@ -285,10 +291,13 @@ bool Vocoder::run_conv(const Conv &c, const float *x, int T, int pad, int dil, c
 // decomposed into st output phases: output t = st*m + phi gathers taps k = k0 + j*st with input row m + dj.
 bool Vocoder::run_convT(const Conv &c, const float *x, int T, int st, int trim, const Snake *sn, float *y, int T_out,
                         hipStream_t s) {
+    const bool pre = c.ic % 8 == 0;   // one snake/f16 pass shared by the st output phases
+    if (pre && !snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, T, c.ic, s)) return false;
     for (int phi = 0; phi < st; ++phi) {
         ConvParams p;
         p.x = x; p.T_in = T; p.C_in = c.ic;
-        if (sn) { p.snake_a = sn->a; p.snake_ib = sn->ib; }
+        if (pre) p.xh = xh_;
+        else if (sn) { p.snake_a = sn->a; p.snake_ib = sn->ib; }
         const int k0 = (phi + trim) % st;
         int n = 0, dmin = 1 << 30, dmax = -(1 << 30);
         for (int k = k0; k < c.k; k += st) {

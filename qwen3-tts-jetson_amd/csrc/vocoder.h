@@ -63,6 +63,7 @@ private:
     // scratch (grown by ensure)
     int cap_frames_ = 0;
     float *buf_[3] = {nullptr, nullptr, nullptr};
+    uint16_t *xh_ = nullptr;   // f16 (snake'd) conv input, one activation
     int32_t *codes_ = nullptr;
     int *cols_ = nullptr;
     float *pcm_ = nullptr, *rope_ = nullptr;

@@ -10,6 +10,7 @@ struct ConvTap { const uint16_t *w; int dj; };   // w: [C_out][C_in] f16 of one 
 // x: [T_in][C_in] f32 (rows outside [0,T_in) read as 0 = causal zero padding); y: [T_out][C_out] f32
 struct ConvParams {
     const float *x = nullptr;
+    const uint16_t *xh = nullptr;   // alternative input: f16 rows [T_in][C_in] with SnakeBeta already applied (C_in % 8 == 0)
     int T_in = 0, C_in = 0;
     const float *snake_a = nullptr, *snake_ib = nullptr;   // exp(alpha), exp(-beta) per input channel (nullable)
     int n_taps = 0;
@@ -21,6 +22,9 @@ struct ConvParams {
     int act = 0;   // 1 = tanh
 };
 bool conv(const ConvParams &p, hipStream_t s);
+// out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
+// the conv input computed ONCE per element instead of once per (output tile, tap window) inside k_conv
+bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, int64_t T, int C, hipStream_t s);
 bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s);
 bool attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s);
 bool codes_cols(const int32_t *codes, int *cols, int F, int ncb, hipStream_t s);

@@ -26,7 +26,16 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
     const int r = lane & 31, h = lane >> 5;
     for (int c0 = 0; c0 < p.C_in; c0 += CT_K) {
-        // ---- stage the input window (snake + f16 rounding fused), 4 channels per thread-step
+        // ---- stage the input window: f16 rows as they are (snake applied by snake_f16), or snake + f16 rounding here
+        if (p.xh) {
+            for (int e = tid; e < win * (CT_K / 8); e += 256) {
+                const int row = e / (CT_K / 8), c8 = (e % (CT_K / 8)) * 8;
+                const int i = m0 + p.dmin + row;
+                uint4 u = make_uint4(0, 0, 0, 0);
+                if (i >= 0 && i < p.T_in && c0 + c8 < p.C_in) u = *reinterpret_cast<const uint4 *>(p.xh + (size_t)i * p.C_in + c0 + c8);
+                *reinterpret_cast<uint4 *>(xs + row * CT_LD + c8) = u;
+            }
+        } else
         for (int e = tid; e < win * (CT_K / 4); e += 256) {
             const int row = e / (CT_K / 4), cq = (e % (CT_K / 4)) * 4;
             const int i = m0 + p.dmin + row;
@@ -108,6 +117,33 @@ bool conv(const ConvParams &p, hipStream_t s) {
     }
     const dim3 grid((p.M + CT_M - 1) / CT_M, (p.C_out + CT_N - 1) / CT_N);
     hipLaunchKernelGGL(k_conv, grid, dim3(256), 0, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+__global__ void __launch_bounds__(256) k_snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, int64_t n4, int C) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const int c = (int)((i * 4) % C);
+    const float4 v = reinterpret_cast<const float4 *>(x)[i];
+    float y[4] = {v.x, v.y, v.z, v.w};
+    if (a) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // the k_conv staging expression, term for term
+            const float sn = sinf(y[q] * a[c + q]);
+            y[q] = y[q] + (sn * sn) * ib[c + q];
+        }
+    }
+    uint2 h;
+    h.x = (uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16);
+    h.y = (uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16);
+    reinterpret_cast<uint2 *>(out)[i] = h;
+}
+bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, int64_t T, int C, hipStream_t s) {
+    if (C % 4 != 0) { set_error("snake_f16: C % 4 != 0"); return false; }
+    const int64_t n4 = T * C / 4;
+    if (n4 <= 0) return true;
+    hipLaunchKernelGGL(k_snake_f16, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, x, a, ib, out, n4, C);
     Q3T_HIP(hipGetLastError());
     return true;
 }
