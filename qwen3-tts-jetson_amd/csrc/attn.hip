@@ -278,7 +278,183 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
     if (t == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------------------------------------ batched: one workgroup per
+// (slot, kv head) streaming the whole context.  At 64 slots the split grid (slot x kv x 64-position split, partials,
+// tickets, last-arriver combine) ran at ~2.9 TB/s; here each workgroup walks its context in 64-position chunks with
+// the next chunk's K/V loads in flight (register double buffer), and each wave keeps its own online-softmax state
+// (max, sum, 8-dim accumulator per head) over its 16 positions of every chunk, so no barrier is taken per chunk; the
+// four waves merge once at the end.  Same per-position arithmetic as k_attn (explicit roundings); the rescaling order
+// of the online softmax differs from the split combine (f32).
+template <int D, int R>
+__global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
+    constexpr int LPP = D / 8, NP = 4;       // 16 lanes per position, 4 passes of 16 positions per 64-chunk
+    static_assert(LPP == 16, "D = 128");
+    const int slot = blockIdx.x, g = blockIdx.y;
+    const int pos = p.pos[slot];
+    const int nch = pos / 64 + 1;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
+    __shared__ float q_s[R][D];
+    __shared__ float kn_s[D], vn_s[D];
+    __shared__ float wm[4][R], wl[4][R];
+    __shared__ float wa[4][R][D];
+
+    const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
+    uint4 ka[NP], va[NP], kb[NP], vb[NP];
+    auto issue = [&](int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = min(c * 64 + pi * 16 + pg, pos);
+            kr[pi] = ldg16(p.kc + head_off + (size_t)j * D + li * 8);
+            vr[pi] = ldg16(p.vc + head_off + (size_t)j * D + li * 8);
+        }
+    };
+    issue(0, ka, va);
+
+    // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded
+    const int QKV = (p.nH + 2 * p.nKV) * D;
+    const float *qkv = p.qkv + (size_t)slot * QKV;
+    const float *rope = p.rope + (size_t)pos * D;
+    for (int v = wave; v < R + 2; v += 4) {
+        if (v == R + 1) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) vn_s[lane + 64 * e] = f16r(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
+            continue;
+        }
+        const bool isk = v == R;
+        const float *src = isk ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
+        const float *w = isk ? p.kn : p.qn;
+        float x[2];
+        double ss = 0.0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) { x[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(x[e], x[e]); }
+        ss = wave_sum_d(ss);
+        const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+        const float c = rope[2 * lane], s = rope[2 * lane + 1];
+        const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
+        const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
+        float *dst = isk ? kn_s : q_s[v];
+        dst[lane] = f16r(y0);
+        dst[lane + 64] = f16r(y1);
+    }
+    __syncthreads();
+    for (int e = t; e < D; e += 256) {   // KV append at pos
+        p.kc[head_off + (size_t)pos * D + e] = f2h(kn_s[e]);
+        p.vc[head_off + (size_t)pos * D + e] = f2h(vn_s[e]);
+    }
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    float q8[R][8];
+#pragma unroll
+    for (int h = 0; h < R; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q8[h][e] = q_s[h][li * 8 + e];
+
+    float m[R], l[R], acc[R][8];
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        m[h] = -INFINITY;
+        l[h] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
+    }
+    auto chunk = [&](int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
+        float sc[NP][R];
+        bool ok[NP];
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = c * 64 + pi * 16 + pg;
+            ok[pi] = j <= pos;
+            float k8[8];
+            if (j == pos) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) k8[e] = kn_s[li * 8 + e];
+            } else {
+                unpack8(kr[pi], k8);
+            }
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                float s = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);
+                s = group_sum<LPP>(s);
+                sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            float mc = sc[0][h];
+#pragma unroll
+            for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
+            mc = rows_max(mc);                      // this wave's 16 positions of the chunk
+            const float mn = fmaxf(m[h], mc);
+            if (mn == -INFINITY) continue;          // no live position in this wave yet
+            const float alpha = expf(__fsub_rn(m[h], mn));
+            l[h] *= alpha;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[h][e] *= alpha;
+            m[h] = mn;
+        }
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = c * 64 + pi * 16 + pg;
+            float v8[8];
+            if (j == pos) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v8[e] = vn_s[li * 8 + e];
+            } else {
+                unpack8(vr[pi], v8);
+            }
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                const float pr = ok[pi] ? expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
+                l[h] += pr;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, acc[h][e]);
+            }
+        }
+    };
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) issue(c + 1, kb, vb);
+        chunk(c, ka, va);
+        if (c + 1 < nch) {
+            if (c + 2 < nch) issue(c + 2, ka, va);
+            chunk(c + 1, kb, vb);
+        }
+    }
+    // merge the four waves
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const float ls = rows_sum(l[h]);
+        if (lane == 0) { wm[wave][h] = m[h]; wl[wave][h] = ls; }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float a = rows_sum(acc[h][e]);
+            if (lane < 16) wa[wave][h][li * 8 + e] = a;
+        }
+    }
+    __syncthreads();
+    for (int o = t; o < R * D; o += 256) {
+        const int h = o / D, d = o % D;
+        const float M = fmaxf(fmaxf(wm[0][h], wm[1][h]), fmaxf(wm[2][h], wm[3][h]));
+        float num = 0.0f, den = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            if (wm[w][h] == -INFINITY) continue;
+            const float f = expf(__fsub_rn(wm[w][h], M));
+            num = __fmaf_rn(wa[w][h][d], f, num);
+            den = __fmaf_rn(wl[w][h], f, den);
+        }
+        p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(num / den);
+    }
+}
+
 bool attn_decode(const AttnParams &p, hipStream_t s) {
+    if (p.seqk && p.D == 128 && p.nH == 2 * p.nKV) {
+        hipLaunchKernelGGL((k_attn_seq<128, 2>), dim3(p.S, p.nKV), dim3(256), 0, s, p);
+        Q3T_HIP(hipGetLastError());
+        return true;
+    }
     if (p.nH % p.nKV != 0 || p.nH / p.nKV > 4 || (p.D != 64 && p.D != 128)) {
         set_error("attn_decode: unsupported head layout");
         return false;

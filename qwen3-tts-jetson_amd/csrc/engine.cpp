@@ -410,6 +410,7 @@ static bool decoder_stack_mm(const Config &c, const std::vector<DevLayer> &layer
         a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
         a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
         a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
+        a.seqk = S >= 16 && std::getenv("Q3T_ATTN_SPLIT") == nullptr;   // enough (slot, kv head) pairs to fill the chip
         a.part = part; a.ticket = ticket; a.out = attn;
         if (!attn_decode(a, s)) return false;
         GemvParams o;

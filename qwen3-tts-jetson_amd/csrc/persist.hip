@@ -633,7 +633,9 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             int tok = -1;
             SelectSpec sp = p.sel;
             if (MODE == 1) sp.step = pass - 1;
+            if (p.prof && t == 0) p.prof[((size_t)w * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection start
             if (sp.mode != SEL_NONE) tok = select_token<true>(sp, p.logits, 0, S.sel);
+            if (p.prof && t == 0) p.prof[((size_t)0 * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection end (row 0)
             if (t == 0) {
                 if (tok >= 0) select_commit(sp, 0, tok);
                 __hip_atomic_store(p.head_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -53,6 +53,14 @@ for ps in range(1, 16):
 hd = np.array(hd)
 print(f"head: edge {np.nanmean(hd[:, 0]):.2f}, body to last logits {np.nanmean(hd[:, 1]):.2f}, "
       f"last logits -> next pass A published (median) {np.nanmean(hd[:, 2]):.2f} us")
+sel = []
+for ps in range(1, 16):
+    h = ps * PPH + 25
+    st = T[:, h, 3][(T[:, h, 3] >= 0) & (np.arange(256) != 0)]
+    if len(st) and T[0, h, 3] >= 0:
+        sel.append(T[0, h, 3] - st.max())
+if sel:
+    print(f"selection (last workgroup, select_token): {np.mean(sel):.2f} us per pass")
 per_pass = np.diff([T[:, ps * PPH + 24, 2].max() for ps in range(16)])
 print(f"per-pass span: mean {per_pass.mean():.2f} us (min {per_pass.min():.2f}, max {per_pass.max():.2f})")
 eng.close()
