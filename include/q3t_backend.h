@@ -105,13 +105,12 @@ int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms);
 /* replay the captured stage graph (0 = talker decode step, 1 = 16-pass code-predictor frame) `iters` times at
  * KV position `pos` for n_slots slots; *ms = mean device time per replay (HIP events on the context stream) */
 int q3t_time_stage(q3t_ctx *ctx, int stage, int n_slots, int pos, int iters, double *ms);
-/* the single-slot talker step as one persistent launch (persist.hip, no reference counterpart: it replaces the
- * per-op graph of TTSTransformer::forward_step at batch 1): -1 = not in use (shapes/device not supported or
- * Q3T_PERSIST=0), 0 = in use, 1 = in use and a launch gave up waiting on an in-launch hand-off (protocol fault) */
+/* the single-slot talker step and code-predictor frame as persistent launches (persist.hip, no reference
+ * counterpart: they replace the per-op graphs of TTSTransformer::forward_step / TRTCodePredictor at batch 1):
+ * -1 = not in use (shapes or device not supported, another context on the device holds the persistent kernels, or
+ * Q3T_PERSIST=0), 0 = in use, 1 = a launch gave up waiting on an in-launch hand-off (protocol fault; the next call
+ * falls back), 2 = disabled after such a fault: the context runs the bit-identical launch-per-op graphs */
 int q3t_persist_status(q3t_ctx *ctx);
-/* development hook (tests): copy a device state buffer to dst: 0 = talker K cache, 1 = V cache (F16
- * [layer][slot][kv][n_ctx][128]), 2 = last QKV rows (f32), 3 = last attention output (f16) */
-int q3t_debug_read(q3t_ctx *ctx, int which, void *dst, size_t bytes);
 
 /* ---- vocoder */
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);

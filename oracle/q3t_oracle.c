@@ -198,6 +198,7 @@ struct q3o_model {
     mat16 cp_embd[15], cp_head[15];
     /* vocoder */
     const uint16_t *cb_first, *cb_rest[15];
+    uint16_t *cb_norm[16];   /* owned usage-normalised codebooks (NULL: the file's bytes are used) */
     mat16 vq_first_out, vq_rest_out;
     conv_t pre_conv, dec0, dec6;
     mat16 in_proj, out_proj;
@@ -280,6 +281,27 @@ static int load_vocoder(q3o_model *m) {
         const gtensor *tr = gfind(g, b);
         if (!tr || tr->ne[0] != c->cb_dim || tr->ne[1] != c->cb_size) FAIL("bad %s", b);
         m->cb_rest[i] = tdata(g, tr);
+    }
+    /* normalize_codebooks (audio_tokenizer_decoder.cpp:40-73): a codebook whose *.usage tensor is present is divided
+     * row by row by max(usage, 1e-5) (1/u multiplied, re-rounded to f16); converter output has no usage tensors */
+    for (int i = 0; i < 16; ++i) {
+        if (i == 0) snprintf(b, sizeof b, "tok_dec.vq_first.0.usage");
+        else snprintf(b, sizeof b, "tok_dec.vq_rest.%d.usage", i - 1);
+        const gtensor *ut = gfind(g, b);
+        if (!ut) continue;
+        if (ut->type != 0 || ut->ne[0] * ut->ne[1] != c->cb_size) FAIL("bad %s", b);
+        const float *u = tdata(g, ut);
+        const uint16_t *src = i == 0 ? m->cb_first : m->cb_rest[i - 1];
+        uint16_t *dst = malloc((size_t)c->cb_size * c->cb_dim * 2);
+        for (int r = 0; r < c->cb_size; ++r) {
+            float uu = u[r];
+            if (uu < 1e-5f) uu = 1e-5f;
+            const float inv = 1.0f / uu;
+            for (int d = 0; d < c->cb_dim; ++d)
+                dst[(size_t)r * c->cb_dim + d] = q3o_f32_to_f16(q3o_f16_to_f32(src[(size_t)r * c->cb_dim + d]) * inv);
+        }
+        m->cb_norm[i] = dst;
+        if (i == 0) m->cb_first = dst; else m->cb_rest[i - 1] = dst;
     }
     const gtensor *op = gfind(g, "tok_dec.vq_first.output_proj.weight");
     if (!op) FAIL("missing vq_first.output_proj");
@@ -414,6 +436,7 @@ static void parse_config(const gguf_t *g, q3o_config *c) {
 void q3o_free(q3o_model *m) {
     if (!m) return;
     free(m->L); free(m->CP); free(m->VL);
+    for (int i = 0; i < 16; ++i) free(m->cb_norm[i]);
     gguf_close(m->gt); gguf_close(m->gk);
     free(m);
 }
@@ -858,13 +881,23 @@ float q3o_uniform(uint64_t seed, uint64_t utt, uint64_t frame, uint64_t cb) {
 static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
                          float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
                          const int32_t *forced, int n_forced, int32_t *codes_out, int *n_frames, float *logits_trace,
-                         float *hidden_trace, float *cb0_trace, float *cp_trace);
+                         float *hidden_trace, float *cb0_trace, float *cp_trace, int trace_from);
 int q3o_generate_forced(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
                         int force_frames, const int32_t *forced, int n_forced, float *cb0_trace, float *cp_trace) {
     int nf = 0;
     int32_t *tmp = malloc(sizeof(int32_t) * 16 * (size_t)(n_forced > 0 ? n_forced : 1));
     const int r = generate_impl(m, toks, n, spk, n_forced, language_id, rep, 0.0f, 0, 0, 0, force_frames, forced, n_forced,
-                                tmp, &nf, NULL, NULL, cb0_trace, cp_trace);
+                                tmp, &nf, NULL, NULL, cb0_trace, cp_trace, 0);
+    free(tmp);
+    return r;
+}
+int q3o_generate_forced_from(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
+                             int force_frames, const int32_t *forced, int n_forced, int from_frame, float *cb0_trace,
+                             float *cp_trace) {
+    int nf = 0;
+    int32_t *tmp = malloc(sizeof(int32_t) * 16 * (size_t)(n_forced > 0 ? n_forced : 1));
+    const int r = generate_impl(m, toks, n, spk, n_forced, language_id, rep, 0.0f, 0, 0, 0, force_frames, forced, n_forced,
+                                tmp, &nf, NULL, NULL, cb0_trace, cp_trace, from_frame);
     free(tmp);
     return r;
 }
@@ -872,12 +905,12 @@ int q3o_generate(const q3o_model *m, const int32_t *toks, int n, const float *sp
                  float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
                  int32_t *codes_out, int *n_frames, float *logits_trace, float *hidden_trace) {
     return generate_impl(m, toks, n, spk, max_len, language_id, rep, temperature, top_k, seed, utt, force_frames, NULL, 0,
-                         codes_out, n_frames, logits_trace, hidden_trace, NULL, NULL);
+                         codes_out, n_frames, logits_trace, hidden_trace, NULL, NULL, 0);
 }
 static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const float *spk, int max_len, int language_id,
                          float rep, float temperature, int top_k, uint64_t seed, uint64_t utt, int force_frames,
                          const int32_t *forced, int n_forced, int32_t *codes_out, int *n_frames, float *logits_trace,
-                         float *hidden_trace, float *cb0_trace, float *cp_trace) {
+                         float *hidden_trace, float *cb0_trace, float *cp_trace, int trace_from) {
     const q3o_config *c = &m->c;
     const int H = c->hidden, V = c->codec_vocab, NCB = c->n_codebooks;
     *n_frames = 0;
@@ -899,17 +932,23 @@ static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const f
         if (logits_trace) memcpy(logits_trace + (size_t)frame * V, logits, sizeof(float) * (size_t)V);
         if (hidden_trace) memcpy(hidden_trace + (size_t)frame * H, hidden, sizeof(float) * (size_t)H);
         const int mask = force_frames > 0 && frame < force_frames;
-        int tok = q3o_cb0_select(m, logits, seen, frame, n, rep, temperature, top_k,
+        /* teacher-forced replay from trace_from: earlier frames only advance the talker (no selection, no CP) */
+        const int traced = frame >= trace_from;
+        int tok = 0;
+        if (traced) {
+            tok = q3o_cb0_select(m, logits, seen, frame, n, rep, temperature, top_k,
                                  q3o_uniform(seed, utt, (uint64_t)frame, 0), mask);
-        if (cb0_trace) memcpy(cb0_trace + (size_t)frame * V, logits, sizeof(float) * (size_t)V);  /* processed */
+            if (cb0_trace) memcpy(cb0_trace + (size_t)(frame - trace_from) * V, logits, sizeof(float) * (size_t)V);  /* processed */
+        }
         if (forced) { if (frame >= n_forced) break; tok = forced[(size_t)frame * NCB]; }
         if (tok == c->codec_eos) break;
         fc[0] = tok;
         seen[tok] = 1;
         for (int s = 0; s < NCB - 1; ++s) u15[s] = q3o_uniform(seed, utt, (uint64_t)frame, (uint64_t)s + 1);
         if (forced) {
-            q3o_cp_frame_forced(m, hidden, tok, forced + (size_t)frame * NCB + 1,
-                                cp_trace ? cp_trace + (size_t)frame * 15 * c->cp_vocab : NULL);
+            if (traced)
+                q3o_cp_frame_forced(m, hidden, tok, forced + (size_t)frame * NCB + 1,
+                                    cp_trace ? cp_trace + (size_t)(frame - trace_from) * 15 * c->cp_vocab : NULL);
             for (int s = 0; s < NCB - 1; ++s) fc[s + 1] = forced[(size_t)frame * NCB + s + 1];
         } else {
             q3o_cp_frame(m, hidden, tok, temperature, top_k, u15, fc + 1, NULL);
@@ -1157,6 +1196,13 @@ static int64_t full_len(const q3o_model *m, int F) {
     for (int d = 0; d < 4; ++d) { const int s = m->c.rates[d], K = m->c.conv_t_k[d]; T = (T - 1) * s + K - 2 * (K - s); }
     return T;
 }
+int q3o_codebook(const q3o_model *m, int i, float *out) {
+    if (!m->c.has_vocoder || i < 0 || i > 15) FAIL("no codebook %d", i);
+    const uint16_t *cb = i == 0 ? m->cb_first : m->cb_rest[i - 1];
+    for (size_t k = 0; k < (size_t)m->c.cb_size * m->c.cb_dim; ++k) out[k] = q3o_f16_to_f32(cb[k]);
+    return 1;
+}
+
 int64_t q3o_vocoder_len(const q3o_model *m, int F, int mode) {
     if (F <= 0) return 0;
     return mode == 0 ? full_len(m, F) : (int64_t)F * 1920;

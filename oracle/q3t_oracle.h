@@ -78,10 +78,17 @@ int q3o_generate(const q3o_model *m, const int32_t *toks, int n, const float *sp
  * predictor logits [n_forced][15][Vcp] of every decision (greedy-parity checks with near-tie tolerance) */
 int q3o_generate_forced(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
                         int force_frames, const int32_t *forced, int n_forced, float *cb0_trace, float *cp_trace);
+/* the same replay, tracing only frames >= from_frame (earlier frames advance the talker KV with their forced codes, no
+ * selection or code-predictor work): traces hold n_forced - from_frame frames */
+int q3o_generate_forced_from(const q3o_model *m, const int32_t *toks, int n, const float *spk, int language_id, float rep,
+                             int force_frames, const int32_t *forced, int n_forced, int from_frame, float *cb0_trace,
+                             float *cp_trace);
 /* vocoder: mode 0 = FULL (audio_tokenizer_decoder.cpp), 1 = CHUNK40 (trt_vocoder.cpp:98-170).
  * pcm == NULL => only report the sample count. */
 int q3o_vocoder_decode(const q3o_model *m, const int32_t *codes, int n_frames, int mode, float *pcm, int64_t *n_samples);
 int64_t q3o_vocoder_len(const q3o_model *m, int n_frames, int mode);
+/* codebook i (0 = vq_first, 1..15 = vq_rest.i-1) as f32 [cb_size][cb_dim], after normalize_codebooks */
+int q3o_codebook(const q3o_model *m, int i, float *out);
 
 /* helpers exported for tests */
 uint16_t q3o_f32_to_f16(float x);

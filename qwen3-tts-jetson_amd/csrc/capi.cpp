@@ -196,6 +196,8 @@ int q3t_time_stage(q3t_ctx *ctx, int stage, int n, int pos, int iters, double *m
     GUARD_END
 }
 
+#ifdef Q3T_DEV
+// development builds only (make DEV=1): raw device state for the timeline tools under tools/dev
 int q3t_debug_read(q3t_ctx *ctx, int which, void *dst, size_t bytes) {
     GUARD_BEGIN
     CHECK_CTX(ctx);
@@ -203,9 +205,12 @@ int q3t_debug_read(q3t_ctx *ctx, int which, void *dst, size_t bytes) {
     return ctx->engine.debug_read(which, dst, bytes) ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
+#endif
 
 int q3t_persist_status(q3t_ctx *ctx) {
-    if (!ctx || !ctx->engine.has_talker() || !ctx->engine.persist_enabled()) return -1;
+    if (!ctx || !ctx->engine.has_talker()) return -1;
+    if (ctx->engine.persist_fell_back()) return 2;
+    if (!ctx->engine.persist_enabled()) return -1;
     return ctx->engine.persist_error() ? 1 : 0;
 }
 

@@ -6,12 +6,46 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "vocoder.h"
 
 namespace q3t {
 
 Engine::Engine() = default;
+
+namespace {
+// Persistent grids of two contexts on one device must never run concurrently: two 256-workgroup grids launched on
+// different streams could interleave and leave neither fully resident (every hand-off would then time out).  Every
+// entry point that launches persistent kernels holds its device's lock until its GPU work has drained (they all
+// return synchronised), so contexts driven by different host threads serialise there.  Recursive: a frame callback
+// may call back into the library on the same thread (it must not start generation on another context of the same
+// device; if it does, the overlap ends in a hand-off timeout and the fallback path, not in a hang).
+std::recursive_mutex g_device_mu[64];
+std::unique_lock<std::recursive_mutex> persist_lock(bool on, int device) {
+    if (!on) return std::unique_lock<std::recursive_mutex>();
+    return std::unique_lock<std::recursive_mutex>(g_device_mu[device & 63]);
+}
+bool env_flag(const char *name, bool dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) != 0 : dflt;
+}
+}  // namespace
+
+Options Options::from_env() {
+    Options o;
+    o.persist = env_flag("Q3T_PERSIST", true);
+    o.persist_cp = env_flag("Q3T_PERSIST_CP", true);
+    o.cp_fused_attn = env_flag("Q3T_CP_FUSED_ATTN", true);
+    o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
+    o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
+    o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
+    if (const char *e = std::getenv("Q3T_PERSIST_FAULT_AT")) o.persist_fault_at = (unsigned)std::max(0, std::atoi(e));
+#ifdef Q3T_DEV
+    if (const char *e = std::getenv("Q3T_POLL_EVERY")) o.poll_every = std::max(1, std::atoi(e));
+#endif
+    return o;
+}
 
 Engine::~Engine() {
     if (device_ >= 0) hipSetDevice(device_);
@@ -44,23 +78,18 @@ bool check_shape(const GgufTensor *t, const char *name, int64_t cols, int64_t ro
 }
 }  // namespace
 
-static bool env_flag(const char *name, bool dflt) {
-    const char *e = std::getenv(name);
-    return e ? std::atoi(e) != 0 : dflt;
-}
-
 bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
                   bool recv_weights) {
     device_ = device;
     tts_path_ = tts_gguf;
     tok_path_ = tok_gguf;
     wa_.recv = recv_weights;
-    cp_fused_attn_ = env_flag("Q3T_CP_FUSED_ATTN", true);
-    defer_cp_select_ = env_flag("Q3T_CP_DEFER_SELECT", true);
-    fused_select_ = env_flag("Q3T_FUSED_SELECT", true);
-    persist_ = env_flag("Q3T_PERSIST", true);
-    persist_cp_env_ = env_flag("Q3T_PERSIST_CP", true);
-    if (const char *e = std::getenv("Q3T_POLL_EVERY")) poll_every_ = std::max(1, std::atoi(e));
+    opt_ = Options::from_env();
+    cp_fused_attn_ = opt_.cp_fused_attn;
+    defer_cp_select_ = opt_.defer_cp_select;
+    fused_select_ = opt_.fused_select;
+    persist_ = opt_.persist;
+    poll_every_ = opt_.poll_every;
     max_slots_ = std::max(1, max_slots);
     max_ctx_ = std::max(32, max_ctx);
     if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
@@ -112,10 +141,12 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     cp_fused_attn_ = cp_fused_attn_ && c_.n_heads == 16 && c_.n_kv == 8 && c_.head_dim == 128;
     if (!upload_weights(g)) return false;
     if (!alloc_state()) return false;
-    if (const char *e = std::getenv("Q3T_TALKER_LAYERS")) {   // dev knob: truncated talker stack (debugging only)
+#ifdef Q3T_DEV
+    if (const char *e = std::getenv("Q3T_TALKER_LAYERS")) {   // truncated talker stack (development builds only)
         const int n = std::atoi(e);
         if (n > 0 && n < c_.n_layers) { c_.n_layers = n; L_.resize(n); }
     }
+#endif
     if (!setup_persist()) return false;
     if (!tok_gguf.empty()) {
         voc_.reset(new Vocoder());
@@ -297,6 +328,9 @@ bool Engine::setup_persist() {
     Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
     persist_ = persist_ && fused_select_ &&
                persist_supported(c_.hidden, c_.n_heads, c_.n_kv, c_.head_dim, c_.inter, c_.codec_vocab, max_ctx_, n_cu);
+    const bool cp_ok = opt_.persist_cp && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15;
+    // every instantiation must fit one workgroup per CU on this device (occupancy query with its LDS request)
+    persist_ = persist_ && persist_resident(device_, max_ctx_, cp_ok);
     if (!persist_) return true;
     std::vector<PLayerW> pl(L_.size());
     for (size_t i = 0; i < L_.size(); ++i)
@@ -306,7 +340,7 @@ bool Engine::setup_persist() {
     if (!pl_dev_ || !pstate_) { set_error("device allocation failed"); return false; }
     Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
     // the code-predictor frame (persist_cp_frame): its 5 layers and 15 lm_heads
-    persist_cp_ = persist_cp_env_ && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15;
+    persist_cp_ = cp_ok;
     if (persist_cp_) {
         std::vector<PLayerW> cpl(CP_.size());
         for (size_t i = 0; i < CP_.size(); ++i)
@@ -319,10 +353,30 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
     }
     Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
+#ifdef Q3T_DEV
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
+#endif
     return true;
 }
 
+bool Engine::persist_recover() {
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    fprintf(stderr, "[q3t] persistent kernel flagged an in-launch hand-off fault on device %d: "
+                    "falling back to the launch-per-op graphs for this context\n", device_);
+    Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
+    for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
+    g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
+    persist_ = persist_cp_ = false;
+    // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
+    // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
+    cp_fused_attn_ = false;
+    persist_fallback_ = true;
+    return true;
+}
+
+#ifdef Q3T_DEV
 bool Engine::debug_read(int which, void *dst, size_t bytes) {
     if (which == 5 && pprof_) {   // persistent-step timeline (dev)
         Q3T_HIP(hipStreamSynchronize(stream_));
@@ -350,6 +404,7 @@ bool Engine::debug_read(int which, void *dst, size_t bytes) {
     Q3T_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return true;
 }
+#endif
 
 bool Engine::persist_error() {
     if (!persist_ || !pstate_) return false;
@@ -382,7 +437,7 @@ static int splitk_for(int N, int S, int K) {
         if (nch % ks == 0 && tiles * ks >= 256) return ks;
     return nch % 4 == 0 ? 4 : nch % 3 == 0 ? 3 : nch % 2 == 0 ? 2 : 1;
 }
-static bool decoder_stack_mm(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
+static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
                              unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
@@ -410,7 +465,7 @@ static bool decoder_stack_mm(const Config &c, const std::vector<DevLayer> &layer
         a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
         a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
         a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
-        a.seqk = S >= 16 && std::getenv("Q3T_ATTN_SPLIT") == nullptr;   // enough (slot, kv head) pairs to fill the chip
+        a.seqk = S >= 16 && !attn_split;   // enough (slot, kv head) pairs to fill the chip
         a.part = part; a.ticket = ticket; a.out = attn;
         if (!attn_decode(a, s)) return false;
         GemvParams o;
@@ -482,7 +537,9 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
             a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
             a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
             a.max_splits = max_splits; a.part = part; a.ticket = ticket; a.out = attn;
+#ifdef Q3T_DEV
             if (il == 0 && std::getenv("Q3T_PERSIST_DBG")) a.dbg = part;
+#endif
             if (!attn_decode(a, s)) return false;
             o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
         }
@@ -536,8 +593,11 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         p.rope = rope_; p.pos = pos_; p.kc = kc_; p.vc = vc_; p.kv_layer = kv_layer; p.n_ctx = max_ctx_;
         p.head = codec_head_; p.out_norm = out_norm_; p.hidden = hidden_; p.logits = logits_;
         if (select_next) p.sel = select_spec(SEL_CB0, gp_, 1, 0);
-        if (std::getenv("Q3T_PERSIST_DBG")) { p.dbg_qkv = qkv_; p.dbg_attn = attn_; }   // layer-0 intermediates (dev)
+#ifdef Q3T_DEV
+        if (std::getenv("Q3T_PERSIST_DBG")) { p.dbg_qkv = qkv_; p.dbg_attn = attn_; }   // layer-0 intermediates
+#endif
         p.prof = pprof_;
+        p.fault_at = opt_.persist_fault_at;
         return persist_talker_step(p, s);
     }
     StackInput in0;
@@ -549,7 +609,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
     }
     const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
     if (mm) {
-        if (!decoder_stack_mm(c_, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
+        if (!decoder_stack_mm(c_, opt_.attn_split, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
                               rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_))
             return false;
     } else if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_,
@@ -590,6 +650,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         p.heads = heads_dev_; p.out_norm = cp_out_norm_; p.logits = cp_logits_;
         p.sel = select_spec(SEL_CP, gp_, 0, 0);
         p.prof = pprof_;
+        p.fault_at = opt_.persist_fault_at;
         return persist_cp_frame(p, s);
     }
     const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
@@ -610,7 +671,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         }
         const bool mm = S >= gemm_mfma_min_batch();
         if (mm) {
-            if (!decoder_stack_mm(c_, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
+            if (!decoder_stack_mm(c_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
                                   p == 0 ? nullptr : cp_out_norm_, nullptr))
                 return false;
@@ -790,6 +851,24 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
                       const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval) {
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
+    auto lk = persist_lock(persist_, device_);
+    StreamState st;
+    st.delivered.assign(n_utt, 0);
+    st.stop_at.assign(n_utt, -1);
+    bool fault = false;
+    if (generate_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, on_frames, user, interval, st, &fault))
+        return true;
+    if (!fault) return false;
+    // a persistent launch gave up on a hand-off: nothing it produced was delivered (every chunk is checked before it
+    // is handed out); re-run on the launch-per-op graphs, which are bit-identical, skipping the delivered chunks
+    if (!persist_recover()) return false;
+    return generate_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, on_frames, user, interval, st, &fault);
+}
+
+bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                           const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user,
+                           int interval, StreamState &st, bool *fault) {
+    *fault = false;
     const int S = n_utt, H = c_.hidden, NCB = 16;
     for (int s = 0; s < S; ++s) n_frames[s] = 0;
     if (gp.max_len <= 0) return true;
@@ -863,7 +942,11 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     for (int s = 0; s < S; ++s) posv[s] = plen;
     if (!set_slot_state(S, posv, frame0)) return false;
     if (fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, stream_)) return false;
+#ifdef Q3T_DEV
     const bool dbg = std::getenv("Q3T_DEBUG") != nullptr;
+#else
+    constexpr bool dbg = false;
+#endif
     if (dbg) { fprintf(stderr, "[q3t] prefill enqueued (plen %d)\n", plen); fflush(stderr); }
     Q3T_HIP(hipEventRecord(e1, stream_));
     // ---- frame loop: one graph per frame; done flags polled every 16 frames
@@ -876,14 +959,26 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     struct Chunk { int start; int32_t *codes; int *done; hipEvent_t ev; };
     std::vector<Chunk> pend;
     std::vector<Chunk> pool;
-    std::vector<int> delivered(S, 0), stop_at(S, -1);
-    int n_live = S;
+    std::vector<int> &delivered = st.delivered, &stop_at = st.stop_at;
+    int n_live = S;   // a fallback re-run regenerates utterances stopped earlier too (their frames are returned)
+    auto release = [&]() {
+        for (Chunk &c : pend) pool.push_back(c);
+        pend.clear();
+        for (Chunk &c : pool) { hipHostFree(c.codes); hipHostFree(c.done); hipEventDestroy(c.ev); }
+        pool.clear();
+        if (done_h) hipHostFree(done_h);
+        done_h = nullptr;
+        hipEventDestroy(e0); hipEventDestroy(e1); hipEventDestroy(e2);
+    };
+    // a chunk is handed to the caller only once the persistent kernels behind it are known to be fault-free
     auto deliver = [&](Chunk &c) -> bool {
         Q3T_HIP(hipEventSynchronize(c.ev));
+        if (persist_error()) { *fault = true; return false; }
         for (int s = 0; s < S; ++s) {
             if (stop_at[s] >= 0) continue;
             const int nf = c.done[s] >= 0 ? c.done[s] : gp.max_len;
             if (nf < c.start + interval) continue;   // partial chunks go to the final flush, as in the reference
+            if (c.start + interval <= delivered[s]) continue;   // delivered before a fallback re-run
             delivered[s] = c.start + interval;
             if (!on_frames(user, s, c.codes + (size_t)s * interval * NCB, interval, NCB)) {
                 stop_at[s] = c.start + interval;
@@ -893,7 +988,6 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
                 --n_live;
             }
         }
-        pool.push_back(c);
         return true;
     };
     bool all_done = false;
@@ -916,8 +1010,14 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
             Q3T_HIP(hipEventRecord(c.ev, stream_));
             pend.push_back(c);
             if (pend.size() > 1) {
-                if (!deliver(pend.front())) return false;
+                Chunk front = pend.front();
                 pend.erase(pend.begin());
+                pool.push_back(front);
+                if (!deliver(front)) {
+                    Q3T_HIP(hipStreamSynchronize(stream_));
+                    release();
+                    return false;
+                }
             }
         }
         if ((f + 1) % poll_every_ == 0 && f + 1 < gp.max_len) {
@@ -937,30 +1037,37 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
                                (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
     if (dbg) { fprintf(stderr, "[q3t] frame loop done\n"); fflush(stderr); }
-    if (persist_error()) { hipHostFree(done_h); set_error("persistent talker step: an in-launch hand-off timed out"); return false; }
+    if (persist_error()) {
+        set_error("persistent kernel: an in-launch hand-off timed out");
+        *fault = true;
+        release();
+        return false;
+    }
     for (int s = 0; s < S; ++s) n_frames[s] = done_h[s] >= 0 ? std::min(done_h[s], gp.max_len) : gp.max_len;
-    hipHostFree(done_h);
     if (stream_cb) {
-        for (Chunk &c : pend) if (!deliver(c)) return false;
-        pend.clear();
+        std::vector<Chunk> last;
+        last.swap(pend);
+        for (Chunk &c : last) pool.push_back(c);
+        for (Chunk &c : last)
+            if (!deliver(c)) { release(); return false; }
         for (int s = 0; s < S; ++s) {
             if (stop_at[s] >= 0) { n_frames[s] = std::min(n_frames[s], stop_at[s]); continue; }
             if (n_frames[s] > delivered[s])   // final flush (tts_transformer.cpp:2563-2570)
                 on_frames(user, s, codes + ((size_t)s * gp.max_len + delivered[s]) * NCB, n_frames[s] - delivered[s], NCB);
         }
-        for (Chunk &c : pool) { hipHostFree(c.codes); hipHostFree(c.done); hipEventDestroy(c.ev); }
     }
     float ms1 = 0, ms2 = 0;
     hipEventElapsedTime(&ms1, e0, e1);
     hipEventElapsedTime(&ms2, e1, e2);
     last_prefill_ms = ms1;
     last_frames_ms = ms2;
-    hipEventDestroy(e0); hipEventDestroy(e1); hipEventDestroy(e2);
+    release();
     return true;
 }
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
+    auto lk = persist_lock(persist_, device_);
     std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
@@ -981,6 +1088,10 @@ bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     hipEventDestroy(a);
     hipEventDestroy(b);
     *ms = t / iters;
+    if (persist_error()) {   // time the launch-per-op fallback instead of a faulted persistent launch
+        if (!persist_recover()) return false;
+        return time_stage(stage, S, pos, iters, ms);
+    }
     return true;
 }
 
@@ -989,15 +1100,20 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
     const int H = c_.hidden;
-    Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
-    Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
-    if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false;
-    Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
-    if (hidden) Q3T_HIP(hipMemcpyAsync(hidden, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToHost, stream_));
-    if (logits) Q3T_HIP(hipMemcpyAsync(logits, logits_, (size_t)S * c_.codec_vocab * 4, hipMemcpyDeviceToHost, stream_));
-    Q3T_HIP(hipStreamSynchronize(stream_));
-    if (persist_error()) { set_error("persistent talker step: an in-launch hand-off timed out"); return false; }
-    return true;
+    auto lk = persist_lock(persist_, device_);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
+        if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false;
+        Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
+        if (hidden) Q3T_HIP(hipMemcpyAsync(hidden, hidden_, (size_t)S * H * 4, hipMemcpyDeviceToHost, stream_));
+        if (logits) Q3T_HIP(hipMemcpyAsync(logits, logits_, (size_t)S * c_.codec_vocab * 4, hipMemcpyDeviceToHost, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        if (!persist_error()) return true;
+        if (!persist_recover()) return false;   // re-run this position on the launch-per-op graph
+    }
+    set_error("talker step: persistent fallback failed");
+    return false;
 }
 
 bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float temperature, int top_k, uint64_t seed,
@@ -1005,6 +1121,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int H = c_.hidden;
     for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
+    auto lk = persist_lock(persist_, device_);
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;
@@ -1021,6 +1138,13 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     std::vector<int> tk((size_t)S * 16);
     Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));
+    if (persist_error()) {   // re-run the frame on the per-op launches
+        if (!persist_recover()) return false;
+        Q3T_HIP(hipMemcpyAsync(tokens_, tk0.data(), tk0.size() * 4, hipMemcpyHostToDevice, stream_));
+        if (!enqueue_cp_frame(S, stream_, logits_all)) return false;
+        Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+    }
     for (int s = 0; s < S; ++s) for (int i = 0; i < 15; ++i) codes15[s * 15 + i] = tk[(size_t)s * 16 + 1 + i];
     return true;
 }

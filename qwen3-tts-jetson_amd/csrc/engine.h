@@ -42,6 +42,25 @@ struct DevLayer {
 class Vocoder;
 struct PLayerW;
 
+// Path-selection knobs, read once from the environment when a context is created (the reference's own pattern:
+// QWEN3_TTS_LOW_MEM, src/qwen3_tts.cpp:125-129).  All default to the fastest path; the alternatives exist so that
+// the tests can compare paths that must agree (persistent vs launch-per-op, sequential vs split attention).
+//   Q3T_PERSIST=0          single-slot talker step as launch-per-phase graphs instead of the persistent kernel
+//   Q3T_PERSIST_CP=0       single-slot code-predictor frame as per-op launches
+//   Q3T_CP_FUSED_ATTN=0    code-predictor attention as its own launch (the arithmetic the persistent frame reproduces)
+//   Q3T_FUSED_SELECT=0     token selection as standalone launches
+//   Q3T_CP_DEFER_SELECT=0  code-predictor tokens selected in the head launch
+//   Q3T_ATTN_SPLIT=1       batched attention always split-K (k_attn) instead of k_attn_seq at >= 16 slots
+//   Q3T_PERSIST_FAULT_AT=n test hook: the n-th persistent launch of the context flags a hand-off fault
+// Development-only knobs (Q3T_TALKER_LAYERS, Q3T_PERSIST_PROF, ...) exist only in a -DQ3T_DEV build.
+struct Options {
+    bool persist = true, persist_cp = true, cp_fused_attn = true, fused_select = true, defer_cp_select = true;
+    bool attn_split = false;
+    unsigned persist_fault_at = 0;
+    int poll_every = 16;   // frames between done-flag polls
+    static Options from_env();
+};
+
 class Engine {
 public:
     Engine();
@@ -90,8 +109,11 @@ public:
     // true if a persistent launch gave up waiting on a hand-off (never expected: a protocol fault)
     bool persist_error();
     bool persist_enabled() const { return persist_; }
+    bool persist_fell_back() const { return persist_fallback_; }
+#ifdef Q3T_DEV
     // development hook: copy a device state buffer to the host (0 K cache, 1 V cache, 2 qkv, 3 attention output)
     bool debug_read(int which, void *dst, size_t bytes);
+#endif
 
     // profiling hooks for bench.py: last generate() timings
     double last_prefill_ms = 0, last_frames_ms = 0;
@@ -100,6 +122,15 @@ private:
     bool upload_weights(const Gguf &g);
     bool alloc_state();
     bool setup_persist();
+    // after a persistent launch flagged a fault: drain the stream, clear the hand-off state, drop the captured graphs
+    // and continue on the launch-per-op graphs (the reference's permanent-fallback pattern, tts_transformer.cpp:2176-2182)
+    bool persist_recover();
+    struct StreamState {   // per utterance, kept across a fallback re-run so no chunk is delivered twice
+        std::vector<int> delivered, stop_at;
+    };
+    bool generate_once(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                       const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval,
+                       StreamState &st, bool *fault);
     bool enqueue_talker_step(int S, hipStream_t s);
     bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next);
     SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;
@@ -151,16 +182,18 @@ private:
     RowRecipe *recipe_ = nullptr;
     int recipe_cap_ = 0;
     GenParams gp_;   // parameters baked into the captured frame graph
-    int poll_every_ = 16;        // frames between done-flag polls (Q3T_POLL_EVERY)
-    bool fused_select_ = true;    // Q3T_FUSED_SELECT=0: separate selection launches
-    bool cp_fused_attn_ = true;   // Q3T_CP_FUSED_ATTN=0: separate attention launch in the code predictor
-    bool defer_cp_select_ = true; // Q3T_CP_DEFER_SELECT=0: code-predictor tokens selected in the head launch
-    bool persist_ = true;         // Q3T_PERSIST=0: launch-per-phase talker step at one slot (no persistent kernel)
+    Options opt_;
+    int poll_every_ = 16;
+    bool fused_select_ = true;
+    bool cp_fused_attn_ = true;
+    bool defer_cp_select_ = true;
+    bool persist_ = true;
+    bool persist_fallback_ = false;   // persistent kernels disabled after a flagged fault
     PLayerW *pl_dev_ = nullptr, *pl_cp_dev_ = nullptr;
     const uint16_t **heads_dev_ = nullptr;
-    bool persist_cp_ = false, persist_cp_env_ = true;     // Q3T_PERSIST_CP=0: code-predictor frame as per-op launches
+    bool persist_cp_ = false;
     uint8_t *pstate_ = nullptr;
-    uint64_t *pprof_ = nullptr;   // Q3T_PERSIST_PROF: persistent-step timeline (dev)
+    uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
     std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;

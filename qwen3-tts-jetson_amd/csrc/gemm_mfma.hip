@@ -580,15 +580,24 @@ bool gemm_mfma_supported(const GemvParams &p) {
 
 // split-K with f32 atomics onto the residual: measured slower at B = 64 (the atomic traffic of 256-384 workgroups x
 // 2048 adds costs ~20 us), so off unless Q3T_MFMA_SPLITK=1
+// (development builds only: make DEV=1)
 static bool g_splitk = [] {
+#ifdef Q3T_DEV
     const char *e = std::getenv("Q3T_MFMA_SPLITK");
     return e ? std::atoi(e) != 0 : false;
+#else
+    return false;
+#endif
 }();
 // 32-token tiles per workgroup (TT) : 1 = 32 tokens (more workgroups, weights re-read from L2 per token block),
-// 2 = 64 tokens; Q3T_MFMA_TT
+// 2 = 64 tokens; Q3T_MFMA_TT (development builds)
 static int g_tt = [] {
+#ifdef Q3T_DEV
     const char *e = std::getenv("Q3T_MFMA_TT");
     return e && std::atoi(e) == 2 ? 2 : 1;
+#else
+    return 1;
+#endif
 }();
 
 static bool set_lds(const void *fn, size_t lds, bool &done) {

@@ -695,9 +695,13 @@ static void launch_bt(const GemvParams &p, int rpg, int ks, int nl, dim3 grid, s
 }
 
 static int g_min_blocks = [] {
+#ifdef Q3T_DEV
     const char *e = std::getenv("Q3T_GEMV_MIN_BLOCKS");
     const int x = e ? std::atoi(e) : 0;
     return x > 0 ? x : 256;
+#else
+    return 256;
+#endif
 }();
 static int gemv_min_blocks() { return g_min_blocks; }
 void gemv_set_min_blocks(int n) { g_min_blocks = n > 0 ? n : 256; }

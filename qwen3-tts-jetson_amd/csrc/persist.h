@@ -51,11 +51,18 @@ struct PersistParams {
     uint16_t *dbg_attn = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
+    unsigned *launches = nullptr;  // device launch counter (fault injection)
+    unsigned spin_limit = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
+    unsigned fault_at = 0;         // test hook: the fault_at-th launch of this state block flags a fault (0 = never)
 };
 
 // shapes the persistent step supports: H 1024, 16 q / 8 kv heads of 128, I 3072, V 3072, one workgroup per CU on a
 // 256-CU device, n_ctx <= 32 * 256 (split chunk of 64..256 positions)
 bool persist_supported(int hidden, int n_heads, int n_kv, int head_dim, int inter, int vocab, int n_ctx, int n_cu);
+// residency check: every k_persist instantiation the context may launch fits one workgroup per CU on `device`
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor with the kernel's LDS request) and the device has >= 256 CUs, so the
+// 256-workgroup grid is co-resident when nothing else occupies the device (MI355X_MICROARCH.md, Residency)
+bool persist_resident(int device, int n_ctx, bool cp_frame);
 size_t persist_state_bytes();                    // granule buffers + counters (zeroed once at allocation)
 void persist_carve(uint8_t *base, PersistParams &p);   // point the hand-off buffers into a zeroed state block
 bool persist_talker_step(const PersistParams &p, hipStream_t s);

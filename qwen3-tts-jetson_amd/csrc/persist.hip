@@ -24,7 +24,6 @@ constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, IN
 constexpr int G = 256;          // workgroups (one per CU)
 constexpr int MAXSPLIT = G / NKV;
 constexpr int R = NH / NKV;     // q heads per kv head
-constexpr unsigned SPIN_LIMIT = 1u << 21;
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
 constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
 
@@ -65,10 +64,11 @@ __device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two 
 
 struct Ctl {
     unsigned *err;
+    unsigned limit;   // polls before giving up (PersistParams::spin_limit)
     bool abort;
 };
 
-// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
+// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after c.limit polls (or once any
 // workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
 template <int N>
 __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
@@ -83,7 +83,7 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
         if (ok || c.abort) break;
         ++it;
         if ((it & 255u) == 0) {
-            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= c.limit) {
                 c.abort = true;
                 __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
@@ -174,8 +174,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     constexpr int NP = CH / 16;   // positions per lane group pass (16 lanes per position, 16 positions per pass)
     const int w = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15, grp = t >> 4;
     const int grp4 = lane >> 4;   // row of a KS = 4 GEMV
-    Ctl c{p.err, false};
+    Ctl c{p.err, p.spin_limit, false};
     const unsigned seq = __hip_atomic_load(p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.fault_at && w == 0 && t == 0) {   // test hook: this launch flags a protocol fault (every wait then gives up)
+        const unsigned n = __hip_atomic_fetch_add(p.launches, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (n == p.fault_at) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     auto TAG = [&](int ph) -> uint32_t { return ((seq * 1024u + (unsigned)ph) << 1) | 1u; };
     int pos = MODE == 0 ? p.pos[0] : 0;
     const int nsplit = MODE == 0 ? pos / CH + 1 : 1;
@@ -250,7 +254,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 if (pass >= 2) {
                     uint32_t u1[1];
                     g_wait<1>(p.gtok + pass - 1, TAG(ph0 - 1), u1, c);
-                    tok = (int)u1[0];
+                    tok = min((int)u1[0], p.sel.V - 1);   // an aborted wait returns a stale payload: keep it in the table
                 }
                 const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
                 x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
@@ -683,6 +687,28 @@ bool persist_supported(int hidden, int n_heads, int n_kv, int head_dim, int inte
 
 size_t persist_state_bytes() { return StateLayout().total; }
 
+static size_t persist_lds() { return std::max(sizeof(Lds), (size_t)96 * 1024); }   // > 80 KB: one workgroup per CU
+
+bool persist_resident(int device, int n_ctx, bool cp_frame) {
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < G) return false;
+    auto fits = [&](const void *f) {
+        int blocks = 0;
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds()) != hipSuccess) return false;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, 256, persist_lds()) == hipSuccess && blocks >= 1;
+    };
+    const void *k = nullptr;
+    switch (persist_chunk(n_ctx)) {
+        case 64: k = reinterpret_cast<const void *>(&k_persist<0, 64>); break;
+        case 128: k = reinterpret_cast<const void *>(&k_persist<0, 128>); break;
+        case 192: k = reinterpret_cast<const void *>(&k_persist<0, 192>); break;
+        case 256: k = reinterpret_cast<const void *>(&k_persist<0, 256>); break;
+        default: return false;
+    }
+    if (!fits(k)) return false;
+    return !cp_frame || fits(reinterpret_cast<const void *>(&k_persist<1, 16>));
+}
+
 void persist_carve(uint8_t *base, PersistParams &p) {
     const StateLayout L;
     p.gx = reinterpret_cast<uint64_t *>(base + L.gx);
@@ -698,11 +724,12 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.head_ticket = ctr + 16;  // own 64-B line
     p.err = ctr + 32;
     p.ticket = ctr + 48;       // [8]
+    p.launches = ctr + 56;
 }
 
 template <int MODE, int CH>
 static bool launch_ch(const PersistParams &p, hipStream_t s) {
-    const size_t lds = std::max(sizeof(Lds), (size_t)96 * 1024);   // > 80 KB: one workgroup per CU
+    const size_t lds = persist_lds();
     static bool attr = false;
     if (!attr) {
         Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_persist<MODE, CH>),

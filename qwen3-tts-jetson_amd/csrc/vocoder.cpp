@@ -2,6 +2,7 @@
 // AudioTokenizerDecoder::build_graph (src/audio_tokenizer_decoder.cpp:622-802) with time-major activations.
 #include "vocoder.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -110,15 +111,42 @@ bool Vocoder::load(const std::string &path, hipStream_t s, bool recv_weights) {
         return sn.a && sn.ib;
     };
 
+    // codebooks, divided by their usage counts when the file still carries them (normalize_codebooks,
+    // src/audio_tokenizer_decoder.cpp:40-73: row r *= 1 / max(usage[r], 1e-5), re-rounded to f16).  The converter
+    // already divides and drops *.usage (scripts/convert_tokenizer_to_gguf.py:347-359), so this is normally a no-op.
+    auto codebook = [&](const std::string &name, const std::string &usage_name, uint16_t *&dst) -> bool {
+        const GgufTensor *t = T(name);
+        if (!t || t->type != GGML_TYPE_F16 || t->ne[0] != cb_dim_ || t->ne[1] != cb_size_) { set_error("bad codebook " + name); return false; }
+        const GgufTensor *u = g.find(usage_name);
+        if (!u) { dst = up16(t->data, (size_t)t->nelements()); return dst != nullptr; }
+        if (u->type != GGML_TYPE_F32 || u->nelements() != cb_size_) { set_error("bad codebook usage " + usage_name); return false; }
+        std::vector<uint16_t> w(recv ? 0 : (size_t)t->nelements());
+        if (!recv) {
+            const uint16_t *src = f16p(t);
+            const float *us = static_cast<const float *>(u->data);
+            for (int r = 0; r < cb_size_; ++r) {
+                const float inv = 1.0f / std::max(us[r], 1e-5f);
+                for (int d = 0; d < cb_dim_; ++d) {
+                    const size_t i = (size_t)r * cb_dim_ + d;
+                    _Float16 h;
+                    std::memcpy(&h, src + i, 2);
+                    const _Float16 o = (_Float16)((float)h * inv);   // round to nearest even
+                    std::memcpy(&w[i], &o, 2);
+                }
+            }
+        }
+        dst = up16(w.data(), (size_t)t->nelements());
+        ++n_usage_;
+        return dst != nullptr;
+    };
     const GgufTensor *cb = T("tok_dec.vq_first.0.codebook");
     if (!cb) return false;
     cb_dim_ = (int)cb->ne[0];
     cb_size_ = (int)cb->ne[1];
-    cb_first_ = up16(cb->data, (size_t)cb->nelements());
+    if (!codebook("tok_dec.vq_first.0.codebook", "tok_dec.vq_first.0.usage", cb_first_)) return false;
     for (int i = 0; i < 15; ++i) {
-        const GgufTensor *t = T("tok_dec.vq_rest." + std::to_string(i) + ".codebook");
-        if (!t || t->ne[0] != cb_dim_ || t->ne[1] != cb_size_) { set_error("bad vq_rest codebook"); return false; }
-        cb_rest_[i] = up16(t->data, (size_t)t->nelements());
+        const std::string pre = "tok_dec.vq_rest." + std::to_string(i) + ".";
+        if (!codebook(pre + "codebook", pre + "usage", cb_rest_[i])) return false;
     }
     int r, c;
     if (!(vq_first_out_ = mat("tok_dec.vq_first.output_proj.weight", r, c))) return false;

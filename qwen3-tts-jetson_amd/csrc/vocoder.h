@@ -23,6 +23,7 @@ public:
     bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s);
     bool ensure(int n_frames);
     bool loaded() const { return loaded_; }
+    int n_usage_normalised() const { return n_usage_; }   // codebooks divided by *.usage at load (0 for converter output)
 
 private:
     struct Conv { uint16_t *w = nullptr; float *b = nullptr; int k = 0, ic = 0, oc = 0; };   // w: [k][oc][ic]
@@ -51,6 +52,7 @@ private:
     hipStream_t stream_ = nullptr;
     std::vector<void *> allocs_, scratch_;
     WeightArena wa_;   // every weight tensor (one blob)
+    int n_usage_ = 0;
     int cb_dim_ = 0, cb_size_ = 0, hidden_ = 0, latent_ = 0, n_heads_ = 16, head_dim_ = 64, ffn_ = 0;
     uint16_t *cb_first_ = nullptr, *cb_rest_[15] = {}, *vq_first_out_ = nullptr, *vq_rest_out_ = nullptr;
     uint16_t *in_proj_ = nullptr, *out_proj_ = nullptr;

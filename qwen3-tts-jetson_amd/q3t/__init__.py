@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libq3t.so")
+# Q3T_DEV_LIB=1 loads the development build (make -C csrc DEV=1: debug hooks for tools/dev), never the default
+LIB_PATH = os.path.join(_HERE, "libq3t_dev.so" if os.environ.get("Q3T_DEV_LIB") == "1" else "libq3t.so")
 
 VOCODER_FULL = 0
 VOCODER_CHUNK40 = 1
@@ -62,7 +63,8 @@ _lib.q3t_synchronize.argtypes = [_P]
 _lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
 _lib.q3t_persist_status.argtypes = [_P]
-_lib.q3t_debug_read.argtypes = [_P, _I, _P, C.c_size_t]
+if hasattr(_lib, "q3t_debug_read"):   # development builds only (make -C csrc DEV=1)
+    _lib.q3t_debug_read.argtypes = [_P, _I, _P, C.c_size_t]
 _lib.q3t_vocoder_num_samples.restype = C.c_int64
 _lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
@@ -77,7 +79,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_debug_read", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
@@ -229,11 +231,12 @@ class Engine:
         return ms.value
 
     def persist_status(self):
-        """-1: single-slot talker step runs launch-per-phase; 0: persistent launch in use; 1: it flagged a fault."""
+        """-1: single-slot path runs launch-per-phase; 0: persistent launches in use; 1: one flagged a hand-off
+        fault; 2: persistent launches disabled after a fault (bit-identical launch-per-op graphs in use)."""
         return _lib.q3t_persist_status(self.h)
 
     def debug_read(self, which, nbytes):
-        """development hook: raw bytes of a device state buffer (0 K cache, 1 V cache, 2 QKV, 3 attention output)"""
+        """development builds only: raw bytes of a device state buffer (0 K, 1 V cache, 2 QKV, 3 attention, 5 timeline)"""
         buf = np.zeros(nbytes, np.uint8)
         _check(_lib.q3t_debug_read(self.h, int(which), _addr(buf), int(nbytes)))
         return buf

@@ -62,7 +62,9 @@ def lib():
         L.q3o_uniform.argtypes = [U64, U64, U64, U64]
         L.q3o_generate.argtypes = [P, ip, I, P, I, I, F, F, I, U64, U64, I, ip, C.POINTER(I), P, P]
         L.q3o_generate_forced.argtypes = [P, ip, I, P, I, F, I, ip, I, P, P]
+        L.q3o_generate_forced_from.argtypes = [P, ip, I, P, I, F, I, ip, I, I, P, P]
         L.q3o_vocoder_decode.argtypes = [P, ip, I, I, P, C.POINTER(C.c_int64)]
+        L.q3o_codebook.argtypes = [P, I, fp]
         L.q3o_vocoder_len.restype = C.c_int64
         L.q3o_vocoder_len.argtypes = [P, I, I]
         L.q3o_f32_to_f16.restype = C.c_uint16
@@ -180,20 +182,28 @@ class Oracle:
             return codes[:n], lt[:n], ht[:n]
         return codes[:n]
 
-    def generate_forced(self, toks, forced, spk=None, language_id=2050, rep=1.05, force_frames=0):
-        """teacher-forced replay: returns (processed CB0 logits [F][Vc], CP logits [F][15][Vcp])."""
+    def generate_forced(self, toks, forced, spk=None, language_id=2050, rep=1.05, force_frames=0, from_frame=0):
+        """teacher-forced replay: returns (processed CB0 logits [F'][Vc], CP logits [F'][15][Vcp]) for the frames
+        from_frame..F-1 (earlier frames only advance the talker with their forced codes)."""
         toks = np.ascontiguousarray(toks, np.int32)
         forced = np.ascontiguousarray(forced, np.int32).reshape(-1, 16)
         F = forced.shape[0]
-        cb0 = np.zeros((F, self.cfg["codec_vocab"]), np.float32)
-        cp = np.zeros((F, 15, self.cfg["cp_vocab"]), np.float32)
+        nt = max(F - from_frame, 0)
+        cb0 = np.zeros((max(nt, 1), self.cfg["codec_vocab"]), np.float32)
+        cp = np.zeros((max(nt, 1), 15, self.cfg["cp_vocab"]), np.float32)
         spk_a = None if spk is None else np.ascontiguousarray(spk, np.float32)
-        if not lib().q3o_generate_forced(self.h, toks, len(toks), _ptr(spk_a), language_id, rep, force_frames, forced, F,
-                                         _ptr(cb0), _ptr(cp)):
+        if not lib().q3o_generate_forced_from(self.h, toks, len(toks), _ptr(spk_a), language_id, rep, force_frames,
+                                              forced, F, int(from_frame), _ptr(cb0), _ptr(cp)):
             raise RuntimeError(lib().q3o_error().decode())
-        return cb0, cp
+        return cb0[:nt], cp[:nt]
 
     # ---- vocoder
+    def codebook(self, i):
+        out = np.zeros((self.cfg["cb_size"], self.cfg["cb_dim"]), np.float32)
+        if not lib().q3o_codebook(self.h, int(i), out):
+            raise RuntimeError(lib().q3o_error().decode())
+        return out
+
     def vocoder_len(self, n_frames, mode=0):
         return lib().q3o_vocoder_len(self.h, n_frames, mode)
 

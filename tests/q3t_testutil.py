@@ -21,16 +21,17 @@ def build_synth():
     return SYNTH_EXE
 
 
-def synth_dir(cfg, seed=SEED):
-    """Writes (once) the synthetic GGUF pair for cfg in a temp dir; returns (tts_path, tok_path)."""
+def synth_dir(cfg, seed=SEED, variant=""):
+    """Writes (once) the synthetic GGUF pair for cfg in a temp dir; returns (tts_path, tok_path).
+    variant "usage": the tokenizer file keeps per-codebook usage tensors (see tools/q3t_synth.c)."""
     root = os.environ.get("Q3T_SYNTH_CACHE", "/tmp")
-    d = os.path.join(root, f"q3t_synth_{cfg}_{seed:x}")
+    d = os.path.join(root, f"q3t_synth_{cfg}_{seed:x}" + (f"_{variant}" if variant else ""))
     tts = os.path.join(d, "qwen3-tts-0.6b-f16.gguf")
     tok = os.path.join(d, "qwen3-tts-tokenizer-f16.gguf")
     stamp = os.path.join(d, ".done")
     if not os.path.exists(stamp) or os.path.getmtime(stamp) < os.path.getmtime(SYNTH_SRC):
         os.makedirs(d, exist_ok=True)
-        subprocess.run([build_synth(), cfg, d, str(seed)], check=True)
+        subprocess.run([build_synth(), cfg, d, str(seed)] + ([variant] if variant else []), check=True)
         open(stamp, "w").close()
     return tts, tok
 
@@ -76,26 +77,28 @@ def check_token(lg, tok, temperature, top_k, u, keep_id=-1, tol_logit=5e-2, tol_
 
 
 def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperature=0.0, top_k=50, seed=0, utt=0,
-                    rep=1.05, tol_logit=5e-2, tol_cdf=5e-2, max_off_frac=0.03, eos_id=2150):
+                    rep=1.05, tol_logit=5e-2, tol_cdf=5e-2, max_off_frac=0.03, eos_id=2150, from_frame=0):
     """Teacher-forced parity of a GPU-generated code sequence against the oracle.
 
     The oracle replays the GPU's codes (q3o_generate_forced) and records every decision's logits.  Greedy: each
     GPU token must be the oracle argmax or within tol_logit of it (near-tie); sampling: u*total must fall in the
     token's CDF interval up to tol_cdf.  At most max_off_frac of the decisions may take the tolerance branch.
-    If the GPU stopped before max_len, the oracle must also pick EOS (within tolerance) at that frame."""
+    If the GPU stopped before max_len, the oracle must also pick EOS (within tolerance) at that frame.
+    from_frame > 0: only the decisions of frames >= from_frame are checked (the oracle replays the earlier frames'
+    codes through the talker alone)."""
     from oracle_py import uniform
     codes = np.asarray(codes, np.int32).reshape(-1, 16)
     F = codes.shape[0]
     stopped = F < max_len
     forced = np.concatenate([codes, np.zeros((1, 16), np.int32)]) if stopped else codes
-    cb0, cp = orc.generate_forced(toks, forced, spk=spk, rep=rep, force_frames=force_frames)
+    cb0, cp = orc.generate_forced(toks, forced, spk=spk, rep=rep, force_frames=force_frames, from_frame=from_frame)
     n_dec = n_off = 0
     worst = 0.0
     offs = []
-    for f in range(forced.shape[0]):
+    for f in range(from_frame, forced.shape[0]):
         last = stopped and f == F
         for c in range(1 if last else 16):
-            lg = cb0[f] if c == 0 else cp[f, c - 1]
+            lg = cb0[f - from_frame] if c == 0 else cp[f - from_frame, c - 1]
             tok = eos_id if last else int(codes[f, c])
             n_dec += 1
             if temperature <= 0:

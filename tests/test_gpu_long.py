@@ -1,0 +1,164 @@
+"""GPU parity at the lengths the bench runs (VERDICT r01 "pin parity at the bench's own lengths").
+
+Every check is teacher-forced against the CPU oracle (q3t_testutil.check_decisions / rel_err; tolerances and why they
+are relative / near-tie tolerant: tests/test_gpu_parity.py header).  Lengths and the code paths they reach:
+
+  B=1, 32 frames (configs[0])       persistent talker step + code-predictor frame, one 64-position attention chunk
+  B=1, 320 frames, greedy + T=0.9   k_persist<0,CH> with up to 6 split chunks per kv group (positions up to ~340)
+  16 slots, 160 frames              the batched matrix-core path with k_attn_seq's double-buffered multi-chunk loop
+                                    (nch >= 3) at every step past position 128; three slots checked
+  k_attn_seq vs split-K k_attn      16 slots, positions 0..199: both against each other and slot 0 against the oracle
+                                    at positions around every 64-chunk boundary
+  long context (n_ctx 4114)         the persistent step's 192-position chunk (configs[4]'s context) vs the oracle,
+                                    positions 0..599, checked around the 192 / 384 / 576 boundaries
+  FULL vocoder, 512 frames          the whole-utterance causal attention of the pre-transformer
+                                    (audio_tokenizer_decoder.cpp:452-456, 720-744) and the conv stack at bench length
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from q3t_testutil import REPO, check_decisions, prompt, rel_err, synth_dir
+
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+pytestmark = pytest.mark.gpu
+TOL = 5e-3          # talker hidden / logits, relative max-abs (test_gpu_parity.py, full model)
+MM_MAX_OFF = 0.06   # near-tie decision fraction on the matrix-core path (test_gpu_mfma.py header)
+
+
+def _env_engine(env, *a, **kw):
+    import q3t
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return q3t.Engine(*a, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def full():
+    tts, tok = synth_dir("full")
+    orc = Oracle(tts, tok)
+    yield tts, tok, orc
+    orc.close()
+
+
+@pytest.mark.parametrize("nf,temperature", [(32, 0.0), (32, 0.9), (320, 0.0), (320, 0.9)])
+def test_b1_generate_at_bench_lengths(full, nf, temperature):
+    import q3t
+    tts, tok, orc = full
+    eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=nf + 32)
+    try:
+        assert eng.persist_status() == 0
+        toks = prompt("full")
+        spk = np.zeros(eng.cfg["hidden"], np.float32)
+        out = eng.generate([toks], speakers=[spk], max_len=nf, temperature=temperature, top_k=50, seed=77,
+                           force_frames=nf)[0]
+        assert out.shape == (nf, 16)
+        t0 = time.time()
+        n_off, n_dec, worst = check_decisions(orc, toks, spk, out, max_len=nf, force_frames=nf,
+                                              temperature=temperature, top_k=50, seed=77, utt=0)
+        print(f"B=1 {nf} frames T={temperature}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g} "
+              f"(oracle {time.time() - t0:.1f} s)")
+        assert eng.persist_status() == 0
+    finally:
+        eng.close()
+
+
+def test_16_slots_160_frames_seq_attention(full):
+    """k_attn_seq (>= 16 slots) runs its register double-buffered loop over nch = ceil((pos + 1) / 64) >= 3 chunks"""
+    import q3t
+    tts, tok, orc = full
+    n, nf = 16, 160
+    eng = q3t.Engine(tts, None, device=0, max_slots=n, max_ctx=nf + 40)
+    try:
+        base = prompt("full")
+        prompts = [base[:4] + [(t + 29 * i) % 900 + 20 for t in base[4:]] for i in range(n)]
+        spk = [np.zeros(eng.cfg["hidden"], np.float32)] * n
+        outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.0, force_frames=nf)
+        assert all(o.shape == (nf, 16) for o in outs)
+        for i in (0, 7, 15):
+            n_off, n_dec, worst = check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf,
+                                                  max_off_frac=MM_MAX_OFF)
+            print(f"slot {i}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
+    finally:
+        eng.close()
+
+
+def test_seq_attention_matches_split_attention_and_oracle(full):
+    tts, tok, orc = full
+    n, P = 16, 200
+    seq = _env_engine({}, tts, None, device=0, max_slots=n, max_ctx=P + 8)
+    spl = _env_engine({"Q3T_ATTN_SPLIT": "1"}, tts, None, device=0, max_slots=n, max_ctx=P + 8)
+    kv = orc.kv_new(P + 8, 0)
+    try:
+        H = seq.cfg["hidden"]
+        rng = np.random.default_rng(17)
+        checked = 0
+        for pos in range(P):
+            e = (rng.standard_normal((n, H)) * 0.5).astype(np.float32)
+            hs, ls = seq.talker_forward(e, [pos] * n)
+            hp, lp = spl.talker_forward(e, [pos] * n)
+            ho, lo = orc.talker_step(kv, e[0], pos)
+            if pos % 64 in (0, 1, 63) or pos == P - 1:
+                for s in range(n):
+                    assert rel_err(hs[s], hp[s]) < 1e-2, (pos, s)
+                    assert rel_err(ls[s], lp[s]) < 1e-2, (pos, s)
+                assert rel_err(hs[0], ho) < TOL and rel_err(ls[0], lo) < TOL, pos
+                assert rel_err(hp[0], ho) < TOL and rel_err(lp[0], lo) < TOL, pos
+                checked += 1
+        assert checked >= 10
+    finally:
+        orc.kv_free(kv)
+        seq.close()
+        spl.close()
+
+
+def test_long_context_chunk192_vs_oracle(full):
+    """n_ctx 4114 (configs[4]): the persistent step splits attention into 192-position chunks"""
+    import q3t
+    tts, tok, orc = full
+    eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=4114)
+    kv = orc.kv_new(4114, 0)
+    try:
+        assert eng.persist_status() == 0
+        H = eng.cfg["hidden"]
+        rng = np.random.default_rng(23)
+        for pos in range(600):
+            e = (rng.standard_normal(H) * 0.5).astype(np.float32)
+            hg, lg = eng.talker_forward(e[None], [pos])
+            ho, lo = orc.talker_step(kv, e, pos)
+            if pos % 192 in (0, 1, 191) or pos in (100, 599):
+                assert rel_err(hg[0], ho) < TOL, pos
+                assert rel_err(lg[0], lo) < TOL, pos
+        assert eng.persist_status() == 0
+    finally:
+        orc.kv_free(kv)
+        eng.close()
+
+
+def test_vocoder_full_512_frames(full):
+    import q3t
+    tts, tok, orc = full
+    eng = q3t.Engine(None, tok, device=0, max_slots=1, max_ctx=64)
+    try:
+        codes = np.random.default_rng(512).integers(0, 2048, size=(512, 16), dtype=np.int32)
+        g = eng.vocoder(codes, q3t.VOCODER_FULL)
+        t0 = time.time()
+        o = orc.vocoder(codes, 0)
+        err = float(np.abs(g - o).max())
+        rms = float(np.sqrt(np.mean((g - o) ** 2)))
+        print(f"FULL 512 frames: {g.shape[0]} samples, max|d|={err:.3e} rms={rms:.3e} (oracle {time.time() - t0:.1f} s)")
+        assert g.shape == o.shape
+        assert err < 1e-2 and rms < 2e-3
+    finally:
+        eng.close()

@@ -127,3 +127,72 @@ def test_long_context_chunk(engines):
     finally:
         ep.close()
         eg.close()
+
+
+def test_injected_fault_falls_back_bit_exact():
+    """A hand-off fault (injected: the 40th persistent launch flags it, mid-stream) must never reach the caller: no
+    chunk is delivered from a faulted launch, the context drops to the bit-identical launch-per-op graphs and re-runs,
+    every frame is delivered exactly once, and later calls keep working (VERDICT r01 weak #8 / ADVICE persist.hip)."""
+    import q3t
+    tts, tok = synth_dir("full")
+    ref = _engine(tts, None, False, max_slots=1, max_ctx=160)
+    old = os.environ.get("Q3T_PERSIST_FAULT_AT")
+    os.environ["Q3T_PERSIST_FAULT_AT"] = "40"
+    try:
+        flt = _engine(tts, None, True, max_slots=1, max_ctx=160)
+    finally:
+        if old is None:
+            del os.environ["Q3T_PERSIST_FAULT_AT"]
+        else:
+            os.environ["Q3T_PERSIST_FAULT_AT"] = old
+    try:
+        assert flt.persist_status() == 0
+        toks = prompt("full")
+        spk = np.zeros(flt.cfg["hidden"], np.float32)
+        kw = dict(speakers=[spk], max_len=60, temperature=0.9, top_k=50, seed=8, force_frames=60)
+        want = ref.generate([toks], **kw)[0]
+        got_chunks = []
+        codes = flt.generate_stream([toks], lambda u, c: got_chunks.append(c) or True, interval=10, **kw)[0]
+        assert flt.persist_status() == 2, "the injected fault did not trigger the fallback"
+        assert np.array_equal(codes, want)
+        streamed = np.concatenate(got_chunks)
+        assert streamed.shape == want.shape and np.array_equal(streamed, want)
+        # the context keeps working on the per-op graphs
+        assert np.array_equal(flt.generate([toks], **kw)[0], want)
+        h1, l1 = flt.talker_forward(np.ones((1, flt.cfg["hidden"]), np.float32), [5])
+        h2, l2 = ref.talker_forward(np.ones((1, ref.cfg["hidden"]), np.float32), [5])
+        assert np.isfinite(h1).all() and np.isfinite(l1).all()
+    finally:
+        flt.close()
+        ref.close()
+
+
+def test_two_contexts_on_one_device_serialise():
+    """two persistent contexts on the same device, driven from two host threads at once: the per-device lock keeps
+    their persistent grids from overlapping, so both stay fault-free and produce identical codes"""
+    import threading
+    import q3t
+    tts, tok = synth_dir("full")
+    a = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=96)
+    b = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=96)
+    try:
+        assert a.persist_status() == 0 and b.persist_status() == 0
+        toks = prompt("full")
+        spk = np.zeros(a.cfg["hidden"], np.float32)
+        kw = dict(speakers=[spk], max_len=48, temperature=0.9, top_k=50, seed=3, force_frames=48)
+        res = {}
+
+        def run(name, eng):
+            res[name] = [eng.generate([toks], **kw)[0] for _ in range(3)]
+
+        ts = [threading.Thread(target=run, args=(n, e)) for n, e in (("a", a), ("b", b))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert a.persist_status() == 0 and b.persist_status() == 0
+        for x in res["a"] + res["b"]:
+            assert np.array_equal(x, res["a"][0])
+    finally:
+        a.close()
+        b.close()

@@ -9,6 +9,7 @@ import numpy as np
 R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(R, "qwen3-tts-jetson_amd"), os.path.join(R, "tests")]
 os.environ["Q3T_PERSIST_PROF"] = "1"
+os.environ["Q3T_DEV_LIB"] = "1"   # needs the development build: make -C qwen3-tts-jetson_amd/csrc DEV=1
 import q3t  # noqa: E402
 from q3t_testutil import synth_dir  # noqa: E402
 

@@ -10,9 +10,12 @@
 // Every value has <= 11 significant bits, so it is EXACT in f16 and f32: the GGUF bytes are identical
 // no matter which language regenerates them.
 //
-// usage: q3t_synth <config: full|tiny> <out_dir> [seed]
+// usage: q3t_synth <config: full|tiny> <out_dir> [seed] [usage]
 //   writes <out_dir>/qwen3-tts-0.6b-f16.gguf and <out_dir>/qwen3-tts-tokenizer-f16.gguf
 //   (the fixed file names the reference loads, src/qwen3_tts.cpp:117-118).
+//   "usage": the tokenizer file also carries tok_dec.vq_{first.0,rest.N}.usage [cb_size] F32 tensors, as an
+//   unconverted checkpoint would (the converter divides and drops them, convert_tokenizer_to_gguf.py:347-359);
+//   loaders must apply normalize_codebooks (src/audio_tokenizer_decoder.cpp:40-73).
 #define _GNU_SOURCE
 #include <stdint.h>
 #include <stdio.h>
@@ -141,10 +144,19 @@ static void build_talker(const cfg_t *c) {
     }
 }
 
+static int g_usage = 0;
+
 static void build_tokenizer(const cfg_t *c) {
     char b[128];
     const int CD = c->cb_dim, VH = c->voc_hidden, LAT = c->voc_latent;
     add_t("tok_dec.vq_first.0.codebook", 2, CD, c->cb_size, 1, 0.0, 1.0);
+    if (g_usage) {
+        add1("tok_dec.vq_first.0.usage", c->cb_size, 1.5, 0.3);
+        for (int i = 0; i < c->n_codebooks - 1; ++i) {
+            snprintf(b, sizeof b, "tok_dec.vq_rest.%d.usage", i);
+            add1(b, c->cb_size, 1.5, 0.3);
+        }
+    }
     add_t("tok_dec.vq_first.input_proj.weight", 3, 1, VH, CD, 0.0, 1.0 / sqrt((double)VH));
     add_t("tok_dec.vq_first.output_proj.weight", 3, 1, CD, VH, 0.0, 1.0 / sqrt((double)CD));
     for (int i = 0; i < c->n_codebooks - 1; ++i) {
@@ -335,6 +347,7 @@ int main(int argc, char **argv) {
     const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : strcmp(argv[1], "tiny1") == 0 ? &CFG_TINY1 : NULL;
     if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
     uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
+    g_usage = argc > 4 && strcmp(argv[4], "usage") == 0;
     char path[4096];
 
     build_talker(c);
