@@ -595,38 +595,49 @@ void q3o_kv_free(q3o_kv *kv) { if (kv) { free(kv->k); free(kv->v); free(kv); } }
 /* ------------------------------------------------------------------ one Qwen3 decoder layer, one token
  * tts_transformer.cpp:1410-1494 (talker step) == :1721-1811 (CP step).  Attention of the step graph is
  * ggml_flash_attn_ext (Q->f16, K/V f16 from the cache, f32 online softmax); restated with f32 accumulation. */
-static void decoder_layer(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos) {
-    const q3o_config *c = &m->c;
-    const int H = c->hidden, D = c->head_dim, nH = c->n_heads, nKV = c->n_kv, rep = nH / nKV;
-    float *xn = malloc(sizeof(float) * (size_t)(H > c->inter ? H : c->inter) * 4);
-    float *q = malloc(sizeof(float) * (size_t)nH * D), *k = malloc(sizeof(float) * (size_t)nKV * D);
-    float *v = malloc(sizeof(float) * (size_t)nKV * D), *att = malloc(sizeof(float) * (size_t)nH * D);
-    float *cache = malloc(sizeof(float) * (size_t)D);
-    rms_norm_w(x, l->attn_norm, xn, H, c->eps);
-    mul_mat_vec(m, &l->q, xn, q);
-    mul_mat_vec(m, &l->k, xn, k);
-    mul_mat_vec(m, &l->v, xn, v);
-    q3o_rope_cache((float)pos, D, c->rope_theta, cache);
-    for (int h = 0; h < nH; ++h) { rms_norm_w(q + h * D, l->q_norm, q + h * D, D, c->eps); rope_neox(q + h * D, D, cache); }
-    for (int h = 0; h < nKV; ++h) { rms_norm_w(k + h * D, l->k_norm, k + h * D, D, c->eps); rope_neox(k + h * D, D, cache); }
-    /* ggml_cpy Kcur/Vcur -> F16 cache at n_past */
-    float *kc = kv->k + (size_t)il * kv->n_ctx * nKV * D, *vc = kv->v + (size_t)il * kv->n_ctx * nKV * D;
-    for (int i = 0; i < nKV * D; ++i) {
-        kc[(size_t)pos * nKV * D + i] = m->round ? f16r(k[i]) : k[i];
-        vc[(size_t)pos * nKV * D + i] = m->round ? f16r(v[i]) : v[i];
+static void decoder_layer_block(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos0, int T);
+
+/* f32 dot product, 4 x 8-lane accumulators combined in a fixed order (n % 8 == 0 lanes vectorised, tail scalar) */
+static inline float dot_f32(const float *a, const float *b, int n) {
+#ifdef Q3O_SIMD
+    __m256 a0 = _mm256_setzero_ps(), a1 = a0, a2 = a0, a3 = a0;
+    int i = 0;
+    for (; i + 32 <= n; i += 32) {
+        a0 = _mm256_fmadd_ps(_mm256_loadu_ps(a + i), _mm256_loadu_ps(b + i), a0);
+        a1 = _mm256_fmadd_ps(_mm256_loadu_ps(a + i + 8), _mm256_loadu_ps(b + i + 8), a1);
+        a2 = _mm256_fmadd_ps(_mm256_loadu_ps(a + i + 16), _mm256_loadu_ps(b + i + 16), a2);
+        a3 = _mm256_fmadd_ps(_mm256_loadu_ps(a + i + 24), _mm256_loadu_ps(b + i + 24), a3);
     }
+    a0 = _mm256_add_ps(_mm256_add_ps(a0, a1), _mm256_add_ps(a2, a3));
+    __m128 s = _mm_add_ps(_mm256_castps256_ps128(a0), _mm256_extractf128_ps(a0, 1));
+    s = _mm_hadd_ps(s, s); s = _mm_hadd_ps(s, s);
+    float r = _mm_cvtss_f32(s);
+    for (; i < n; ++i) r += a[i] * b[i];
+    return r;
+#else
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += a[i] * b[i];
+    return r;
+#endif
+}
+
+/* ggml_flash_attn_ext of one token (q [nH][D], at position pos) over the cached rows 0..pos of layer il: f16-rounded
+ * Q, f32 scores and online-softmax sums (double), f32 V accumulation -> att [nH][D].  `par`: heads in parallel. */
+static void attend(const q3o_model *m, const q3o_kv *kv, int il, const float *q, int pos, float *att, int par) {
+    const q3o_config *c = &m->c;
+    const int D = c->head_dim, nH = c->n_heads, nKV = c->n_kv, rep = nH / nKV;
+    const float *kc = kv->k + (size_t)il * kv->n_ctx * nKV * D, *vc = kv->v + (size_t)il * kv->n_ctx * nKV * D;
     const float scale = 1.0f / sqrtf((float)D);
-    float *sc = malloc(sizeof(float) * (size_t)(pos + 1));
+    float *sc_all = malloc(sizeof(float) * (size_t)(pos + 1) * nH);
+#pragma omp parallel for schedule(static) if (par)
     for (int h = 0; h < nH; ++h) {
         const int hk = h / rep;
+        float *sc = sc_all + (size_t)h * (pos + 1);
         float qr[512];
         for (int d = 0; d < D; ++d) qr[d] = m->round ? f16r(q[h * D + d]) : q[h * D + d];
         float mx = -INFINITY;
         for (int j = 0; j <= pos; ++j) {
-            const float *kr = kc + ((size_t)j * nKV + hk) * D;
-            float s = 0.f;
-            for (int d = 0; d < D; ++d) s += kr[d] * qr[d];
-            sc[j] = s * scale;
+            sc[j] = dot_f32(kc + ((size_t)j * nKV + hk) * D, qr, D) * scale;
             if (sc[j] > mx) mx = sc[j];
         }
         double sum = 0.0;
@@ -640,18 +651,64 @@ static void decoder_layer(const q3o_model *m, const layer_t *l, q3o_kv *kv, int 
         const float inv = (float)(1.0 / sum);
         for (int d = 0; d < D; ++d) o[d] *= inv;
     }
-    free(sc);
-    float *y = malloc(sizeof(float) * (size_t)H);
-    mul_mat_vec(m, &l->o, att, y);
-    for (int i = 0; i < H; ++i) x[i] += y[i];
-    rms_norm_w(x, l->ffn_norm, xn, H, c->eps);
-    float *g = malloc(sizeof(float) * (size_t)c->inter), *u = malloc(sizeof(float) * (size_t)c->inter);
-    mul_mat_vec(m, &l->gate, xn, g);
-    mul_mat_vec(m, &l->up, xn, u);
-    for (int i = 0; i < c->inter; ++i) g[i] = silu_f(g[i]) * u[i];
-    mul_mat_vec(m, &l->down, g, y);
-    for (int i = 0; i < H; ++i) x[i] += y[i];
-    free(g); free(u); free(y); free(xn); free(q); free(k); free(v); free(att); free(cache);
+    free(sc_all);
+}
+
+/* head RMSNorms + NEOX RoPE of one token's raw q/k, then its K/V rows written to the cache (ggml_cpy -> F16) */
+static void qk_norm_rope_store(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *q, float *k,
+                               const float *v, int pos) {
+    const q3o_config *c = &m->c;
+    const int D = c->head_dim, nH = c->n_heads, nKV = c->n_kv;
+    float cache[512];
+    q3o_rope_cache((float)pos, D, c->rope_theta, cache);
+    for (int h = 0; h < nH; ++h) { rms_norm_w(q + h * D, l->q_norm, q + h * D, D, c->eps); rope_neox(q + h * D, D, cache); }
+    for (int h = 0; h < nKV; ++h) { rms_norm_w(k + h * D, l->k_norm, k + h * D, D, c->eps); rope_neox(k + h * D, D, cache); }
+    float *kc = kv->k + (size_t)il * kv->n_ctx * nKV * D, *vc = kv->v + (size_t)il * kv->n_ctx * nKV * D;
+    for (int i = 0; i < nKV * D; ++i) {
+        kc[(size_t)pos * nKV * D + i] = m->round ? f16r(k[i]) : k[i];
+        vc[(size_t)pos * nKV * D + i] = m->round ? f16r(v[i]) : v[i];
+    }
+}
+
+/* ------------------------------------------------------------------ one Qwen3 decoder layer, one token
+ * tts_transformer.cpp:1410-1494 (talker step) == :1721-1811 (CP step).  Attention of the step graph is
+ * ggml_flash_attn_ext (Q->f16, K/V f16 from the cache, f32 online softmax); restated with f32 accumulation. */
+static void decoder_layer(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos) {
+    decoder_layer_block(m, l, kv, il, x, pos, 1);
+}
+
+/* the same layer over T consecutive tokens at positions pos0..pos0+T-1 (x [T][H] in place): every weight row is read
+ * once per block and reused by the T tokens, each token computed exactly as decoder_layer computes it alone (the
+ * teacher-forced replay of q3o_generate_forced_from uses it for the frames it does not trace) */
+static void decoder_layer_block(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos0, int T) {
+    const q3o_config *c = &m->c;
+    const int H = c->hidden, D = c->head_dim, nH = c->n_heads, nKV = c->n_kv, I = c->inter;
+    float *xn = malloc(sizeof(float) * (size_t)T * (H > I ? H : I));
+    float *q = malloc(sizeof(float) * (size_t)T * nH * D), *k = malloc(sizeof(float) * (size_t)T * nKV * D);
+    float *v = malloc(sizeof(float) * (size_t)T * nKV * D), *att = malloc(sizeof(float) * (size_t)T * nH * D);
+    float *y = malloc(sizeof(float) * (size_t)T * H);
+    float *g = malloc(sizeof(float) * (size_t)T * I), *u = malloc(sizeof(float) * (size_t)T * I);
+    for (int t = 0; t < T; ++t) rms_norm_w(x + (size_t)t * H, l->attn_norm, xn + (size_t)t * H, H, c->eps);
+    mul_mat_rows(m, &l->q, xn, T, q);
+    mul_mat_rows(m, &l->k, xn, T, k);
+    mul_mat_rows(m, &l->v, xn, T, v);
+    for (int t = 0; t < T; ++t)
+        qk_norm_rope_store(m, l, kv, il, q + (size_t)t * nH * D, k + (size_t)t * nKV * D, v + (size_t)t * nKV * D, pos0 + t);
+    if (T == 1) {
+        attend(m, kv, il, q, pos0, att, 1);
+    } else {
+#pragma omp parallel for schedule(dynamic)
+        for (int t = 0; t < T; ++t) attend(m, kv, il, q + (size_t)t * nH * D, pos0 + t, att + (size_t)t * nH * D, 0);
+    }
+    mul_mat_rows(m, &l->o, att, T, y);
+    for (size_t i = 0; i < (size_t)T * H; ++i) x[i] += y[i];
+    for (int t = 0; t < T; ++t) rms_norm_w(x + (size_t)t * H, l->ffn_norm, xn + (size_t)t * H, H, c->eps);
+    mul_mat_rows(m, &l->gate, xn, T, g);
+    mul_mat_rows(m, &l->up, xn, T, u);
+    for (size_t i = 0; i < (size_t)T * I; ++i) g[i] = silu_f(g[i]) * u[i];
+    mul_mat_rows(m, &l->down, g, T, y);
+    for (size_t i = 0; i < (size_t)T * H; ++i) x[i] += y[i];
+    free(g); free(u); free(y); free(xn); free(q); free(k); free(v); free(att);
 }
 
 int q3o_talker_step_n(const q3o_model *m, q3o_kv *kv, const float *embd, int pos, int n_layers, float *hidden, float *logits) {
@@ -927,8 +984,45 @@ static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const f
     uint8_t *seen = calloc((size_t)V, 1);
     int32_t fc[16], u15_i = 0; (void)u15_i;
     float u15[15];
-    int n_past = plen;
-    for (int frame = 0; frame < max_len; ++frame) {
+    int n_past = plen, frame0 = 0;
+    if (forced && trace_from > 0) {
+        /* frames before trace_from: their forced codes only advance the talker, in blocks of up to 64 tokens (each
+         * token computed exactly as the one-token step would compute it); hidden / logits of the last one feed frame
+         * trace_from's decisions */
+        int F0 = trace_from < n_forced ? trace_from : n_forced;
+        if (F0 > max_len) F0 = max_len;
+        for (int f = 0; f < F0; ++f)
+            if (forced[(size_t)f * NCB] == c->codec_eos) { F0 = f; break; }
+        const int BLK = 64;
+        float *X = malloc(sizeof(float) * (size_t)BLK * H);
+        for (int f0 = 0; f0 < F0; f0 += BLK) {
+            const int T = F0 - f0 < BLK ? F0 - f0 : BLK;
+            for (int t = 0; t < T; ++t) {
+                const int f = f0 + t;
+                const int32_t *fc_f = forced + (size_t)f * NCB;
+                float *xt = X + (size_t)t * H;
+                seen[fc_f[0]] = 1;
+                memcpy(codes_out + (size_t)f * NCB, fc_f, sizeof(int32_t) * (size_t)NCB);
+                embd_row(&m->codec_embd, fc_f[0], xt);
+                for (int cb = 1; cb < NCB; ++cb) {
+                    embd_row(&m->cp_embd[cb - 1], fc_f[cb], row);
+                    for (int h = 0; h < H; ++h) xt[h] += row[h];
+                }
+                const float *tr = f < tlen ? trailing + (size_t)f * H : pad;
+                for (int h = 0; h < H; ++h) xt[h] += tr[h];
+            }
+            for (int il = 0; il < c->n_layers; ++il) decoder_layer_block(m, &m->L[il], kv, il, X, n_past, T);
+            n_past += T;
+            if (f0 + T == F0) {   /* :1496-1505 on the last token */
+                rms_norm_w(X + (size_t)(T - 1) * H, m->out_norm, hidden, H, c->eps);
+                mul_mat_vec(m, &m->codec_head, hidden, logits);
+            }
+        }
+        free(X);
+        *n_frames = F0;
+        frame0 = F0;
+    }
+    for (int frame = frame0; frame < max_len; ++frame) {
         if (logits_trace) memcpy(logits_trace + (size_t)frame * V, logits, sizeof(float) * (size_t)V);
         if (hidden_trace) memcpy(hidden_trace + (size_t)frame * H, hidden, sizeof(float) * (size_t)H);
         const int mask = force_frames > 0 && frame < force_frames;

@@ -40,6 +40,7 @@ def test_configs4_4096_frames_chunk40_stream():
         codes = eng.generate_stream([toks], on_frames, interval=IV, speakers=[spk], max_len=NF, temperature=0.9,
                                     top_k=50, seed=SEED, force_frames=NF)[0]
         t_gpu = time.time() - t0
+        print(f"4096 frames streamed + CHUNK40 in {t_gpu:.1f} s", flush=True)
         assert codes.shape == (NF, 16)
         assert len(chunks) == NF // IV + (NF % IV > 0)
         assert np.array_equal(np.concatenate(chunks), codes)
@@ -50,6 +51,7 @@ def test_configs4_4096_frames_chunk40_stream():
         t0 = time.time()
         first = check_decisions(orc, toks, spk, codes[:IV], max_len=IV, force_frames=NF, temperature=0.9, top_k=50,
                                 seed=SEED)
+        print(f"first chunk checked ({time.time() - t0:.1f} s); replaying {NF - IV} frames in the oracle", flush=True)
         last = check_decisions(orc, toks, spk, codes, max_len=NF, force_frames=NF, temperature=0.9, top_k=50,
                                seed=SEED, from_frame=NF - IV)
         print(f"4096 frames streamed + CHUNK40 in {t_gpu:.1f} s (GPU); oracle checks {time.time() - t0:.1f} s; "
