@@ -46,6 +46,13 @@ __device__ __forceinline__ float dot8(const uint4 &a, const uint4 &b, float acc)
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// 16-byte load through a global (address space 1) pointer: global_load_dwordx4, never a flat load (a flat load counts
+// in both vmcnt and lgkmcnt, so its waits also drain the LDS traffic around it)
+__device__ __forceinline__ uint4 ldg16(const void *p) {
+    typedef const __attribute__((address_space(1))) u32x4_t gv;
+    const u32x4_t v = *(gv *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 // 16-byte streaming load of once-read weights (non-temporal policy, microarch 'nt-weights')
 __device__ __forceinline__ uint4 ld_nt16(const void *ptr) {
     const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(ptr));

@@ -274,7 +274,7 @@ bool Vocoder::ensure(int F) {
         big = std::max(big, (size_t)T * dec_[d].ct.oc);
     }
     for (int i = 0; i < 3; ++i) if (!(buf_[i] = (float *)alloc(big * 4))) { set_error("vocoder scratch alloc"); return false; }
-    if (!(xh_ = (uint16_t *)alloc(big * 2))) { set_error("vocoder scratch alloc"); return false; }
+    if (!(xh_ = (uint16_t *)alloc(big * 2)) || !(xh2_ = (uint16_t *)alloc(big * 2))) { set_error("vocoder scratch alloc"); return false; }
     codes_ = (int32_t *)alloc((size_t)F * 16 * 4);
     cols_ = (int *)alloc((size_t)F * 16 * 4);
     pcm_ = (float *)alloc((size_t)std::max<int64_t>(full_len(F), (int64_t)F * 1920) * 4);
@@ -338,6 +338,44 @@ bool Vocoder::run_convT(const Conv &c, const float *x, int T, int st, int trim, 
         p.n_taps = n; p.dmin = dmin; p.dmax = dmax;
         p.y = y; p.C_out = c.oc; p.M = (T_out - phi + st - 1) / st; p.so = st; p.ob = phi;
         p.bias = c.b;
+        if (!conv(p, s)) return false;
+    }
+    return true;
+}
+
+bool Vocoder::conv16(const Conv &c, const uint16_t *xh, int T, int pad, int dil, float *y, const float *resid,
+                     uint16_t *y16, const Snake *next, hipStream_t s) {
+    ConvParams p;
+    p.xh = xh; p.T_in = T; p.C_in = c.ic;
+    p.n_taps = c.k;
+    for (int j = 0; j < c.k; ++j) p.taps[j] = ConvTap{c.w + (size_t)j * c.oc * c.ic, j * dil - pad};
+    p.dmin = -pad; p.dmax = (c.k - 1) * dil - pad;
+    p.y = y; p.C_out = c.oc; p.M = T + pad - dil * (c.k - 1); p.so = 1; p.ob = 0;
+    p.bias = c.b; p.resid = resid;
+    p.y16 = y16;
+    if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
+    return conv(p, s);
+}
+
+bool Vocoder::convT16(const Conv &c, const uint16_t *xh, int T, int st, int trim, float *y, int T_out, uint16_t *y16,
+                      const Snake *next, hipStream_t s) {
+    for (int phi = 0; phi < st; ++phi) {
+        ConvParams p;
+        p.xh = xh; p.T_in = T; p.C_in = c.ic;
+        const int k0 = (phi + trim) % st;
+        int n = 0, dmin = 1 << 30, dmax = -(1 << 30);
+        for (int k = k0; k < c.k; k += st) {
+            const int dj = (phi + trim - k) / st;
+            p.taps[n++] = ConvTap{c.w + (size_t)k * c.oc * c.ic, dj};
+            dmin = std::min(dmin, dj);
+            dmax = std::max(dmax, dj);
+        }
+        if (n == 0) continue;
+        p.n_taps = n; p.dmin = dmin; p.dmax = dmax;
+        p.y = y; p.C_out = c.oc; p.M = (T_out - phi + st - 1) / st; p.so = st; p.ob = phi;
+        p.bias = c.b;
+        p.y16 = y16;
+        if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
         if (!conv(p, s)) return false;
     }
     return true;
@@ -419,26 +457,40 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
         float *nxt = h;
         f0 = cur; cur = nxt; T = T1;
     }
-    // 5) dec0 conv k7 (left pad 6) -> [T][dec_dim]   (:759-763)
-    if (!run_conv(dec0_, cur, (int)T, 6, 1, nullptr, f0, nullptr, 0, s)) return false;
-    std::swap(cur, f0);
+    // 5) dec0 conv k7 (left pad 6) -> [T][dec_dim]   (:759-763).  From here on every conv input is the f16
+    // SnakeBeta of its predecessor's output, written by that conv's epilogue (snake + rounding once per element,
+    // the f32 tensor itself only where a residual needs it): ha / hb ping-pong
+    uint16_t *ha = xh_, *hb = xh2_;
+    if (!snake_f16(cur, nullptr, nullptr, ha, T, dec0_.ic, s)) return false;
+    if (!conv16(dec0_, ha, (int)T, 6, 1, nullptr, nullptr, hb, &dec_[0].snake, s)) return false;   // snake(dec0) only
+    std::swap(ha, hb);
     // 6) decoder blocks: SnakeBeta -> conv-transpose (trim K-s both sides) + bias -> 3 residual units (:551-620)
     for (int d = 0; d < 4; ++d) {
         const Dec &D = dec_[d];
         const int st = D.rate, K = D.ct.k;
         const int64_t T2 = (T - 1) * st + K - 2 * (K - st);
-        if (!run_convT(D.ct, cur, (int)T, st, K - st, &D.snake, f0, (int)T2, s)) return false;
+        // x = convT(snake(x)): f32 residual stream + f16 snake1 of residual unit 0
+        if (!convT16(D.ct, ha, (int)T, st, K - st, f0, (int)T2, hb, &D.res[0].a1, s)) return false;
+        std::swap(ha, hb);
         std::swap(cur, f0);
         T = T2;
         for (int ri = 0; ri < 3; ++ri) {
             const Res &R = D.res[ri];
-            // h1 = conv1(snake1(x)) with causal pad 6*dil; x += conv2(snake2(h1))
-            if (!run_conv(R.c1, cur, (int)T, 6 * R.dil, R.dil, &R.a1, f0, nullptr, 0, s)) return false;
-            if (!run_conv(R.c2, f0, (int)T, 0, 1, &R.a2, cur, cur, 0, s)) return false;
+            const Snake *next = ri < 2 ? &D.res[ri + 1].a1 : d < 3 ? &dec_[d + 1].snake : &dec5_;
+            // h1 = conv1(snake1(x)) with causal pad 6*dil -> only snake2(h1) in f16; x += conv2(snake2(h1)) (f32, in
+            // place) plus the next conv's f16 input
+            if (!conv16(R.c1, ha, (int)T, 6 * R.dil, R.dil, nullptr, nullptr, hb, &R.a2, s)) return false;
+            if (!conv16(R.c2, hb, (int)T, 0, 1, cur, cur, ha, next, s)) return false;
         }
     }
-    // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790)
-    if (!run_conv(dec6_, cur, (int)T, 6, 1, &dec5_, pcm_dev, nullptr, 1, s)) return false;
+    // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790): ha holds f16(snake(dec5)) of the stream
+    ConvParams p6;
+    p6.xh = ha; p6.T_in = (int)T; p6.C_in = dec6_.ic;
+    p6.n_taps = dec6_.k;
+    for (int j = 0; j < dec6_.k; ++j) p6.taps[j] = ConvTap{dec6_.w + (size_t)j * dec6_.oc * dec6_.ic, j - 6};
+    p6.dmin = -6; p6.dmax = dec6_.k - 1 - 6;
+    p6.y = pcm_dev; p6.C_out = dec6_.oc; p6.M = (int)T + 6 - (dec6_.k - 1); p6.bias = dec6_.b; p6.act = 1;
+    if (!conv(p6, s)) return false;
     *n_out = T;
     return true;
 }

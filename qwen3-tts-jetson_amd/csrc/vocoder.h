@@ -47,6 +47,12 @@ private:
                   int act, hipStream_t s);
     bool run_convT(const Conv &c, const float *x, int T, int stride, int trim, const Snake *sn, float *y, int T_out,
                    hipStream_t s);
+    // the same convs on an f16 input already snake'd by the producer's epilogue; outputs f32 y and/or
+    // y16 = f16(next_snake(y)) (the next conv's input), either may be null
+    bool conv16(const Conv &c, const uint16_t *xh, int T, int pad, int dil, float *y, const float *resid, uint16_t *y16,
+                const Snake *next, hipStream_t s);
+    bool convT16(const Conv &c, const uint16_t *xh, int T, int stride, int trim, float *y, int T_out, uint16_t *y16,
+                 const Snake *next, hipStream_t s);
 
     bool loaded_ = false;
     hipStream_t stream_ = nullptr;
@@ -66,6 +72,7 @@ private:
     int cap_frames_ = 0;
     float *buf_[3] = {nullptr, nullptr, nullptr};
     uint16_t *xh_ = nullptr;   // f16 (snake'd) conv input, one activation
+    uint16_t *xh2_ = nullptr;  // second f16 activation: the decoder blocks ping-pong conv inputs written by epilogues
     int32_t *codes_ = nullptr;
     int *cols_ = nullptr;
     float *pcm_ = nullptr, *rope_ = nullptr;

@@ -16,10 +16,14 @@ struct ConvParams {
     int n_taps = 0;
     ConvTap taps[CONV_MAX_TAPS];
     int dmin = 0, dmax = 0;
-    float *y = nullptr;
+    float *y = nullptr;             // f32 output [T_out][C_out] (nullable when y16 is set)
     int C_out = 0, M = 0, so = 1, ob = 0;
     const float *bias = nullptr, *resid = nullptr;
     int act = 0;   // 1 = tanh
+    // optional f16 output of the same elements: y16[t][co] = f16(snake(v)) with exp(alpha) / exp(-beta) per output
+    // channel (y16_a null: plain rounding) -- the NEXT conv's input, so no separate snake/round pass reads y back
+    uint16_t *y16 = nullptr;
+    const float *y16_a = nullptr, *y16_ib = nullptr;
 };
 bool conv(const ConvParams &p, hipStream_t s);
 // out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
