@@ -122,6 +122,17 @@ int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, 
 int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes /* [n_frames][n_codebooks] */, int32_t n_frames,
                                int32_t n_codebooks, int32_t chunk_frames, float *pcm, int64_t *n_samples);
 
+/* ---- speaker encoder (ECAPA-TDNN; the TTS GGUF's spk_enc.* tensors)
+ * q3t_speaker_dim: embedding length, 0 when the model has no speaker encoder.
+ * q3t_speaker_encode: AudioTokenizerEncoder::encode (src/audio_tokenizer_encoder.h:107-108): samples in [-1, 1] at
+ * 24 kHz -> embedding [q3t_speaker_dim]; Q3T_ERR + q3t_last_error() when the audio is too short (< 5 mel frames).
+ * q3t_speaker_mel: its log-mel front end (compute_mel_spectrogram, audio_tokenizer_encoder.cpp:281-364), time-major
+ * [n_frames][128]; mel may be NULL to query *n_frames. */
+int q3t_speaker_dim(const q3t_ctx *ctx);
+int q3t_speaker_encode(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *embedding);
+int q3t_speaker_mel(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *mel, int32_t cap_frames,
+                    int32_t *n_frames);
+
 /* ---- stage entry points (used by the parity tests; each syncs the context stream) */
 int q3t_talker_forward(q3t_ctx *ctx, int n_slots, const float *embd /* [n][H] */, const int32_t *pos /* [n] */,
                        float *hidden /* [n][H] or NULL */, float *logits /* [n][codec_vocab] or NULL */);

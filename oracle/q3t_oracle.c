@@ -207,6 +207,10 @@ struct q3o_model {
     upblk_t up[2];
     decblk_t dec[4];
     snake_t dec5;
+    /* speaker encoder (ECAPA-TDNN), audio_tokenizer_encoder.h:29-83 */
+    int has_spk;
+    conv_t spk_conv0, spk_mfa, spk_asp_tdnn, spk_asp_conv, spk_fc;
+    struct { conv_t tdnn1, tdnn2, res[7], se1, se2; } spk_blk[3];
 };
 
 static const void *tdata(const gguf_t *g, const gtensor *t) { return g->map + g->data_off + t->off; }
@@ -441,6 +445,229 @@ void q3o_free(q3o_model *m) {
     free(m);
 }
 
+static float *conv1d(const q3o_model *m, const conv_t *cv, const float *x, int T, int pad, int dil, int depthwise, int *Tout);
+
+/* ------------------------------------------------------------------ speaker encoder (audio_tokenizer_encoder.cpp) */
+/* tensor names: AudioTokenizerEncoder::load_model (:185-241); conv weights ne [K, IC, OC] F16, biases F32 */
+static int load_speaker_encoder(q3o_model *m) {
+    const gguf_t *g = m->gt;
+    char w[96], b[96];
+#define SPK(cv, nm) do { snprintf(w, sizeof w, "spk_enc.%s.weight", nm); snprintf(b, sizeof b, "spk_enc.%s.bias", nm); \
+                         if (!get_conv(g, w, b, &(cv))) return 0; } while (0)
+    SPK(m->spk_conv0, "conv0");
+    SPK(m->spk_mfa, "mfa");
+    SPK(m->spk_asp_tdnn, "asp.tdnn");
+    SPK(m->spk_asp_conv, "asp.conv");
+    SPK(m->spk_fc, "fc");
+    for (int i = 0; i < 3; ++i) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "blk.%d.tdnn1", i + 1); SPK(m->spk_blk[i].tdnn1, nm);
+        snprintf(nm, sizeof nm, "blk.%d.tdnn2", i + 1); SPK(m->spk_blk[i].tdnn2, nm);
+        snprintf(nm, sizeof nm, "blk.%d.se.conv1", i + 1); SPK(m->spk_blk[i].se1, nm);
+        snprintf(nm, sizeof nm, "blk.%d.se.conv2", i + 1); SPK(m->spk_blk[i].se2, nm);
+        for (int r = 0; r < 7; ++r) { snprintf(nm, sizeof nm, "blk.%d.res2net.%d", i + 1, r); SPK(m->spk_blk[i].res[r], nm); }
+    }
+#undef SPK
+    if (m->spk_conv0.ic != 128 || m->spk_conv0.oc != 512 || m->spk_mfa.ic != 1536 || m->spk_fc.ic != 3072)
+        FAIL("speaker encoder: unexpected shapes");
+    m->has_spk = 1;
+    return 1;
+}
+
+/* librosa slaney mel filterbank (compute_mel_filterbank_slaney, :16-94), [n_mels][n_bins] */
+static void spk_filterbank(float *fb, int n_mels, int n_fft, int sr, float f_min, float f_max) {
+    const float f_sp = 200.0f / 3.0f, min_log_hz = 1000.0f, min_log_mel = (min_log_hz - 0.0f) / f_sp;
+    const float logstep = logf(6.4f) / 27.0f;
+#define HZ2MEL(hz) ((hz) < min_log_hz ? ((hz) - 0.0f) / f_sp : min_log_mel + logf((hz) / min_log_hz) / logstep)
+#define MEL2HZ(mel) ((mel) < min_log_mel ? 0.0f + f_sp * (mel) : min_log_hz * expf(logstep * ((mel) - min_log_mel)))
+    const float mel_min = HZ2MEL(f_min), mel_max = HZ2MEL(f_max);
+    const int nb = n_fft / 2 + 1;
+    float *hz = malloc(sizeof(float) * (size_t)(n_mels + 2));
+    for (int i = 0; i < n_mels + 2; ++i) {
+        const float mp = mel_min + (mel_max - mel_min) * i / (n_mels + 1);
+        hz[i] = MEL2HZ(mp);
+    }
+#undef HZ2MEL
+#undef MEL2HZ
+    memset(fb, 0, sizeof(float) * (size_t)n_mels * nb);
+    for (int mm = 0; mm < n_mels; ++mm) {
+        const float fl = hz[mm], fc = hz[mm + 1], fr = hz[mm + 2], enorm = 2.0f / (fr - fl);
+        for (int k = 0; k < nb; ++k) {
+            const float freq = (float)k * sr / n_fft;
+            if (freq >= fl && freq <= fc) { if (fc > fl) fb[(size_t)mm * nb + k] = enorm * (freq - fl) / (fc - fl); }
+            else if (freq > fc && freq <= fr) { if (fr > fc) fb[(size_t)mm * nb + k] = enorm * (fr - freq) / (fr - fc); }
+        }
+    }
+    free(hz);
+}
+
+/* compute_mel_spectrogram (:281-364): reflect pad (n_fft-hop)/2, Hann window, DFT magnitude sqrt(re^2+im^2+1e-9),
+ * slaney mel, log(max(x, 1e-5)) -> mel [128][F] (channel-major).  The DFT's cos/sin terms are the reference's own
+ * expressions (float angle = -2*M_PI*k*t/n), tabulated once; sums in the reference's order. */
+int q3o_mel(const q3o_model *m, const float *samples, int n, float *mel, int *n_frames) {
+    (void)m;
+    const int NFFT = 1024, HOP = 256, WIN = 1024, NM = 128, SR = 24000, NB = NFFT / 2 + 1;
+    const int pad = (NFFT - HOP) / 2, plen = n + 2 * pad;
+    const int F = (plen - NFFT) / HOP + 1;
+    if (n < 2 || F <= 0) FAIL("Audio too short for mel spectrogram");
+    *n_frames = F;
+    if (!mel) return 1;
+    float *padded = malloc(sizeof(float) * (size_t)plen);
+    for (int i = 0; i < plen; ++i) {
+        int src = i < pad ? pad - i : i >= pad + n ? 2 * n - (i - pad) - 2 : i - pad;
+        src = src < 0 ? 0 : src > n - 1 ? n - 1 : src;
+        padded[i] = samples[src];
+    }
+    float *fb = malloc(sizeof(float) * (size_t)NM * NB), *win = calloc(NFFT, sizeof(float));
+    spk_filterbank(fb, NM, NFFT, SR, 0.0f, 12000.0f);
+    const int off = (NFFT - WIN) / 2;
+    for (int i = 0; i < WIN; ++i) win[off + i] = 0.5f * (1.0f - cosf(2.0f * M_PI * i / WIN));
+    float *ct = malloc(sizeof(float) * (size_t)NB * NFFT), *st = malloc(sizeof(float) * (size_t)NB * NFFT);
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < NB; ++k)
+        for (int t = 0; t < NFFT; ++t) {
+            const float angle = -2.0f * M_PI * k * t / NFFT;
+            ct[(size_t)k * NFFT + t] = cosf(angle);
+            st[(size_t)k * NFFT + t] = sinf(angle);
+        }
+#pragma omp parallel for schedule(dynamic)
+    for (int f = 0; f < F; ++f) {
+        float frame[1024], mag[513];
+        for (int i = 0; i < NFFT; ++i) frame[i] = padded[(size_t)f * HOP + i] * win[i];
+        for (int k = 0; k < NB; ++k) {
+            float re = 0.0f, im = 0.0f;
+            for (int t = 0; t < NFFT; ++t) { re += frame[t] * ct[(size_t)k * NFFT + t]; im += frame[t] * st[(size_t)k * NFFT + t]; }
+            mag[k] = sqrtf(re * re + im * im + 1e-9f);
+        }
+        for (int mm = 0; mm < NM; ++mm) {
+            float sum = 0.0f;
+            for (int k = 0; k < NB; ++k) sum += fb[(size_t)mm * NB + k] * mag[k];
+            mel[(size_t)mm * F + f] = logf(sum > 1e-5f ? sum : 1e-5f);
+        }
+    }
+    free(padded); free(fb); free(win); free(ct); free(st);
+    return 1;
+}
+
+/* apply_reflect_pad_1d (:366-408) of [C][T] then a "valid" conv (ggml_conv_1d, F16 im2col) + bias */
+static float *spk_conv(const q3o_model *m, const conv_t *cv, const float *x, int T, int pad, int dil) {
+    const int C = cv->ic, Tp = T + 2 * pad;
+    float *xp = malloc(sizeof(float) * (size_t)C * Tp);
+    for (int c = 0; c < C; ++c)
+        for (int i = 0; i < Tp; ++i) {
+            const int t = i < pad ? pad - i : i >= pad + T ? T - 2 - (i - pad - T) : i - pad;
+            xp[(size_t)c * Tp + i] = x[(size_t)c * T + t];
+        }
+    int To;
+    float *y = conv1d(m, cv, xp, Tp, 0, dil, 0, &To);
+    free(xp);
+    return y;   /* [oc][T] */
+}
+static void relu_(float *x, size_t n) { for (size_t i = 0; i < n; ++i) x[i] = x[i] > 0.0f ? x[i] : 0.0f; }
+/* ggml_pool_1d AVG over the whole time axis (f32 sum / T) [ggml-upstream] */
+static float mean_t(const float *x, int T) { float s = 0.0f; for (int t = 0; t < T; ++t) s += x[t]; return s / (float)T; }
+
+/* AudioTokenizerEncoder::encode (:696-750) with build_graph (:438-694): conv0 (k5, reflect 2) + ReLU; 3 SE-Res2Net
+ * blocks (dilations 2,3,4: tdnn1 + ReLU, 8 branches of 64 (branch b>=2 adds the previous branch output) through k3
+ * dilated convs + ReLU, tdnn2 + ReLU, SE (mean -> conv1 + ReLU -> conv2 + sigmoid -> scale), + residual); MFA
+ * (concat blocks 1..3, 1x1 1536 + ReLU); ASP (global mean/std, tdnn 4608->128 + ReLU + tanh, conv 128->1536, softmax
+ * over time, weighted mean/std); FC 3072 -> E */
+int q3o_speaker_encode(const q3o_model *m, const float *samples, int n, float *emb) {
+    if (!m->has_spk) FAIL("No speaker encoder tensors found in model");
+    int T;
+    if (!q3o_mel(m, samples, n, NULL, &T)) return 0;
+    float *mel = malloc(sizeof(float) * (size_t)128 * T);
+    q3o_mel(m, samples, n, mel, &T);
+    float *cur = spk_conv(m, &m->spk_conv0, mel, T, 2, 1);
+    free(mel);
+    relu_(cur, (size_t)512 * T);
+    float *outs[3];
+    const int dils[3] = {2, 3, 4};
+    for (int blk = 0; blk < 3; ++blk) {
+        const int dl = dils[blk];
+        float *h = spk_conv(m, &m->spk_blk[blk].tdnn1, cur, T, 0, 1);
+        relu_(h, (size_t)512 * T);
+        float *cat = malloc(sizeof(float) * (size_t)512 * T);
+        memcpy(cat, h, sizeof(float) * (size_t)64 * T);   /* branch 0: identity */
+        float *prev = NULL, *in = malloc(sizeof(float) * (size_t)64 * T);
+        for (int b = 1; b < 8; ++b) {
+            for (size_t i = 0; i < (size_t)64 * T; ++i) in[i] = h[(size_t)b * 64 * T + i] + (b >= 2 ? prev[i] : 0.0f);
+            float *o = spk_conv(m, &m->spk_blk[blk].res[b - 1], in, T, dl, dl);
+            relu_(o, (size_t)64 * T);
+            memcpy(cat + (size_t)b * 64 * T, o, sizeof(float) * (size_t)64 * T);
+            free(prev);
+            prev = o;
+        }
+        free(prev); free(in); free(h);
+        float *y = spk_conv(m, &m->spk_blk[blk].tdnn2, cat, T, 0, 1);
+        free(cat);
+        relu_(y, (size_t)512 * T);
+        float se_in[512], se_mid[128], se_out[512];
+        for (int c = 0; c < 512; ++c) se_in[c] = mean_t(y + (size_t)c * T, T);
+        float *s1 = spk_conv(m, &m->spk_blk[blk].se1, se_in, 1, 0, 1);
+        for (int c = 0; c < 128; ++c) se_mid[c] = s1[c] > 0.0f ? s1[c] : 0.0f;
+        free(s1);
+        float *s2 = spk_conv(m, &m->spk_blk[blk].se2, se_mid, 1, 0, 1);
+        for (int c = 0; c < 512; ++c) se_out[c] = 1.0f / (1.0f + expf(-s2[c]));
+        free(s2);
+        for (int c = 0; c < 512; ++c)
+            for (int t = 0; t < T; ++t) y[(size_t)c * T + t] = y[(size_t)c * T + t] * se_out[c] + cur[(size_t)c * T + t];
+        if (blk > 0) outs[blk - 1] = cur;
+        else free(cur);
+        cur = y;
+    }
+    outs[2] = cur;
+    float *mfa_in = malloc(sizeof(float) * (size_t)1536 * T);
+    /* block outputs 1, 2, 3 (outs[0..2]) concatenated on channels (:599-600) */
+    for (int i = 0; i < 3; ++i) memcpy(mfa_in + (size_t)i * 512 * T, outs[i], sizeof(float) * (size_t)512 * T);
+    float *hs = spk_conv(m, &m->spk_mfa, mfa_in, T, 0, 1);
+    free(mfa_in); free(outs[0]); free(outs[1]); free(outs[2]);
+    relu_(hs, (size_t)1536 * T);
+    float *att_in = malloc(sizeof(float) * (size_t)4608 * T);
+    memcpy(att_in, hs, sizeof(float) * (size_t)1536 * T);
+    for (int c = 0; c < 1536; ++c) {
+        const float *xc = hs + (size_t)c * T;
+        const float mu = mean_t(xc, T);
+        float sq = 0.0f;
+        for (int t = 0; t < T; ++t) sq += xc[t] * xc[t];
+        float var = sq / (float)T - mu * mu;
+        var = var < 1e-12f ? 1e-12f : var > 1e10f ? 1e10f : var;
+        const float sd = sqrtf(var);
+        for (int t = 0; t < T; ++t) { att_in[(size_t)(1536 + c) * T + t] = mu; att_in[(size_t)(3072 + c) * T + t] = sd; }
+    }
+    float *a1 = spk_conv(m, &m->spk_asp_tdnn, att_in, T, 0, 1);
+    free(att_in);
+    for (size_t i = 0; i < (size_t)128 * T; ++i) a1[i] = tanhf(a1[i] > 0.0f ? a1[i] : 0.0f);
+    float *a2 = spk_conv(m, &m->spk_asp_conv, a1, T, 0, 1);
+    free(a1);
+    float pooled[3072];
+    for (int c = 0; c < 1536; ++c) {
+        float *ac = a2 + (size_t)c * T;
+        const float *xc = hs + (size_t)c * T;
+        float mx = -INFINITY;
+        for (int t = 0; t < T; ++t) mx = ac[t] > mx ? ac[t] : mx;
+        double sum = 0.0;   /* ggml_soft_max: f32 exp, ggml_float (double) sum [ggml-upstream] */
+        for (int t = 0; t < T; ++t) { ac[t] = expf(ac[t] - mx); sum += ac[t]; }
+        const float inv = (float)(1.0 / sum);
+        for (int t = 0; t < T; ++t) ac[t] *= inv;
+        float wm = 0.0f;
+        for (int t = 0; t < T; ++t) wm += ac[t] * xc[t];
+        wm = (wm / (float)T) * (float)T;   /* pool AVG then scale by T (:659-661) */
+        float wv = 0.0f;
+        for (int t = 0; t < T; ++t) { const float d = xc[t] - wm; wv += ac[t] * (d * d); }
+        wv = (wv / (float)T) * (float)T;
+        wv = wv < 1e-12f ? 1e-12f : wv > 1e10f ? 1e10f : wv;
+        pooled[c] = wm;
+        pooled[1536 + c] = sqrtf(wv);
+    }
+    free(a2); free(hs);
+    float *e = spk_conv(m, &m->spk_fc, pooled, 1, 0, 1);
+    memcpy(emb, e, sizeof(float) * (size_t)m->spk_fc.oc);
+    free(e);
+    return 1;
+}
+int q3o_speaker_dim(const q3o_model *m) { return m->has_spk ? m->spk_fc.oc : 0; }
+
 q3o_model *q3o_load(const char *tts_gguf, const char *tok_gguf, int ggml_rounding) {
     q3o_model *m = calloc(1, sizeof *m);
     m->round = ggml_rounding;
@@ -476,6 +703,7 @@ q3o_model *q3o_load(const char *tts_gguf, const char *tok_gguf, int ggml_roundin
         m->gk = gguf_open(tok_gguf);
         if (!m->gk || !load_vocoder(m)) { q3o_free(m); return NULL; }
     }
+    if (gfind(g, "spk_enc.conv0.weight") && !load_speaker_encoder(m)) { q3o_free(m); return NULL; }
     return m;
 }
 

@@ -87,6 +87,11 @@ int q3o_generate_forced_from(const q3o_model *m, const int32_t *toks, int n, con
  * pcm == NULL => only report the sample count. */
 int q3o_vocoder_decode(const q3o_model *m, const int32_t *codes, int n_frames, int mode, float *pcm, int64_t *n_samples);
 int64_t q3o_vocoder_len(const q3o_model *m, int n_frames, int mode);
+/* speaker encoder (AudioTokenizerEncoder, src/audio_tokenizer_encoder.cpp): mel spectrogram [128][F] of 24 kHz samples
+ * (mel == NULL: only *n_frames), and the ECAPA-TDNN embedding [q3o_speaker_dim] */
+int q3o_mel(const q3o_model *m, const float *samples, int n, float *mel, int *n_frames);
+int q3o_speaker_encode(const q3o_model *m, const float *samples, int n, float *embedding);
+int q3o_speaker_dim(const q3o_model *m);
 /* codebook i (0 = vq_first, 1..15 = vq_rest.i-1) as f32 [cb_size][cb_dim], after normalize_codebooks */
 int q3o_codebook(const q3o_model *m, int i, float *out);
 

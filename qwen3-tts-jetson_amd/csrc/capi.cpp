@@ -1,10 +1,12 @@
 // capi.cpp — extern "C" boundary (include/q3t_backend.h).  No exception crosses it.
 #include "../../include/q3t_backend.h"
 
+#include <algorithm>
 #include <exception>
 
 #include "comm.h"
 #include "engine.h"
+#include "speaker.h"
 #include "vocoder.h"
 
 struct q3t_ctx {
@@ -242,6 +244,41 @@ int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes, int32_t n_fra
     if (chunk_frames <= 0) { q3t::set_error("chunk_frames must be > 0"); return Q3T_ERR; }
     if (n_frames > 0 && (!codes || !pcm)) { q3t::set_error("null argument"); return Q3T_ERR; }
     return v->decode(codes, n_frames, Q3T_VOCODER_CHUNK40, pcm, n_samples, chunk_frames) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_speaker_dim(const q3t_ctx *ctx) {
+    if (!ctx) return 0;
+    q3t::SpeakerEncoder *s = const_cast<q3t::Engine &>(ctx->engine).speaker();
+    return s && s->loaded() ? s->dim() : 0;
+}
+
+int q3t_speaker_encode(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *embedding) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::SpeakerEncoder *s = ctx->engine.speaker();
+    if (!s || !s->loaded()) { q3t::set_error("Model not loaded (no speaker encoder tensors in the TTS GGUF)"); return Q3T_ERR; }
+    if (!samples || !embedding || n_samples <= 0) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return s->encode(samples, n_samples, embedding) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_speaker_mel(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *mel, int32_t cap_frames,
+                    int32_t *n_frames) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::SpeakerEncoder *s = ctx->engine.speaker();
+    if (!s || !s->loaded()) { q3t::set_error("Model not loaded (no speaker encoder tensors in the TTS GGUF)"); return Q3T_ERR; }
+    if (!samples || !n_frames || n_samples <= 0) { q3t::set_error("null argument"); return Q3T_ERR; }
+    std::vector<float> m;
+    int F = 0;
+    if (!s->mel(samples, n_samples, m, &F)) return Q3T_ERR;
+    *n_frames = F;
+    if (mel) {
+        if (cap_frames < F) { q3t::set_error("mel buffer too small"); return Q3T_ERR; }
+        std::copy(m.begin(), m.end(), mel);
+    }
+    return Q3T_OK;
     GUARD_END
 }
 

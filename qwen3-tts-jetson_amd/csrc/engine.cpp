@@ -8,6 +8,7 @@
 #include <cstring>
 #include <mutex>
 
+#include "speaker.h"
 #include "vocoder.h"
 
 namespace q3t {
@@ -240,6 +241,11 @@ bool Engine::upload_weights(const Gguf &g) {
         if (!(cp_embd_[i] = up16(b, H, c_.cp_vocab))) return false;
         snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
         if (!(cp_head_[i] = up16(b, H, c_.cp_vocab))) return false;
+    }
+    // speaker encoder (ECAPA-TDNN, audio_tokenizer_encoder.cpp): optional, the GGUF's spk_enc.* tensors
+    if (g.find("spk_enc.conv0.weight")) {
+        spk_.reset(new SpeakerEncoder());
+        if (!spk_->load(g, wa_, stream_)) return false;
     }
     // the 16 tables of the step embedding: codec_embd (code 0) + code_pred.codec_embd[0..14] (codes 1..15)
     std::vector<uint16_t *> tabs16(16);

@@ -40,6 +40,7 @@ struct DevLayer {
 };
 
 class Vocoder;
+class SpeakerEncoder;
 struct PLayerW;
 
 // Path-selection knobs, read once from the environment when a context is created (the reference's own pattern:
@@ -80,6 +81,7 @@ public:
     int max_ctx() const { return max_ctx_; }
     hipStream_t stream() const { return stream_; }
     Vocoder *vocoder() { return voc_.get(); }
+    SpeakerEncoder *speaker() { return spk_.get(); }   // null when the TTS GGUF has no spk_enc.* tensors
 
     // ---- hot path: prefill + frame loop for n_utt utterances (codes [n_utt][max_len][ncb])
     // on_frames (frame_callback_t, src/tts_transformer.h:224): called every `interval` frames per utterance with its
@@ -198,6 +200,7 @@ private:
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
     std::map<int, hipGraphExec_t> g_talker_, g_frame_, g_cp_;
     std::unique_ptr<Vocoder> voc_;
+    std::unique_ptr<SpeakerEncoder> spk_;
 };
 
 }  // namespace q3t

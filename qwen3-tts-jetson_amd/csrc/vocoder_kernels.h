@@ -16,10 +16,11 @@ struct ConvParams {
     int n_taps = 0;
     ConvTap taps[CONV_MAX_TAPS];
     int dmin = 0, dmax = 0;
-    float *y = nullptr;             // f32 output [T_out][C_out] (nullable when y16 is set)
+    float *y = nullptr;             // f32 output [T_out][ldy] (nullable when y16 is set)
     int C_out = 0, M = 0, so = 1, ob = 0;
+    int ldy = 0;                    // row stride of y and resid (0: C_out)
     const float *bias = nullptr, *resid = nullptr;
-    int act = 0;   // 1 = tanh
+    int act = 0;   // 1 = tanh, 2 = ReLU, 3 = tanh(ReLU)
     // optional f16 output of the same elements: y16[t][co] = f16(snake(v)) with exp(alpha) / exp(-beta) per output
     // channel (y16_a null: plain rounding) -- the NEXT conv's input, so no separate snake/round pass reads y back
     uint16_t *y16 = nullptr;

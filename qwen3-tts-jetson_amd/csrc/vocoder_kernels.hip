@@ -14,6 +14,13 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 // y[m*so + ob][co] = act( bias[co] + resid + sum_j sum_ci W_j[co][ci] * f16( snake(x[m + dj][ci]) ) )
 // Tile 64 (m) x 64 (co); 4 waves as 2 x 2 of 32 x 32; K-chunk = 32 input channels.
 constexpr int CT_M = 64, CT_N = 64, CT_K = 32, CT_LD = CT_K + 8;   // LDS row: 32 f16 + 16 B pad
+
+__device__ __forceinline__ float conv_act(float v, int act) {
+    if (act == 1) return tanhf(v);
+    if (act == 2) return fmaxf(v, 0.0f);
+    if (act == 3) return tanhf(fmaxf(v, 0.0f));
+    return v;
+}
 constexpr int CT_MAXWIN = CT_M + 64;
 
 __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
@@ -113,10 +120,11 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
         const int m = m0 + wm * 32 + row;
         if (m >= p.M) continue;
         const size_t t = (size_t)m * p.so + p.ob;
+        const int ldy = p.ldy ? p.ldy : p.C_out;
         float v = acc[reg] + b;
-        if (p.resid) v = p.resid[t * p.C_out + co] + v;
-        if (p.act == 1) v = tanhf(v);
-        if (p.y) p.y[t * p.C_out + co] = v;
+        if (p.resid) v = p.resid[t * ldy + co] + v;
+        v = conv_act(v, p.act);
+        if (p.y) p.y[t * ldy + co] = v;
         if (p.y16) {
             float z = v;
             if (p.y16_a) {
@@ -234,7 +242,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
             const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
             const int m = m0 + wave * 32 * RB + i * 32 + row;
             if (m >= p.M) continue;
-            const size_t t = (size_t)m * p.so + p.ob, o = t * p.C_out + co0 + q4;
+            const size_t t = (size_t)m * p.so + p.ob, o = t * (p.ldy ? p.ldy : p.C_out) + co0 + q4;
+            const size_t o16 = t * p.C_out + co0 + q4;
             const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
             float v[4] = {a.x, a.y, a.z, a.w};
             if (p.bias) {
@@ -245,9 +254,9 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
                 const float4 rr = *reinterpret_cast<const float4 *>(p.resid + o);
                 v[0] = rr.x + v[0]; v[1] = rr.y + v[1]; v[2] = rr.z + v[2]; v[3] = rr.w + v[3];
             }
-            if (p.act == 1) {
+            if (p.act) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = tanhf(v[q]);
+                for (int q = 0; q < 4; ++q) v[q] = conv_act(v[q], p.act);
             }
             if (p.y) *reinterpret_cast<float4 *>(p.y + o) = make_float4(v[0], v[1], v[2], v[3]);
             if (p.y16) {
@@ -265,7 +274,7 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
                 uint2 hv;
                 hv.x = (uint32_t)f2h(z[0]) | ((uint32_t)f2h(z[1]) << 16);
                 hv.y = (uint32_t)f2h(z[2]) | ((uint32_t)f2h(z[3]) << 16);
-                *reinterpret_cast<uint2 *>(p.y16 + o) = hv;
+                *reinterpret_cast<uint2 *>(p.y16 + o16) = hv;
             }
         }
         __builtin_amdgcn_wave_barrier();

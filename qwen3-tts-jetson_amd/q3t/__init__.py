@@ -69,6 +69,9 @@ _lib.q3t_vocoder_num_samples.restype = C.c_int64
 _lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_vocoder_decode_chunked.argtypes = [_P, _ip, C.c_int32, C.c_int32, C.c_int32, _fp, C.POINTER(C.c_int64)]
+_lib.q3t_speaker_dim.argtypes = [_P]
+_lib.q3t_speaker_encode.argtypes = [_P, _fp, C.c_int32, _fp]
+_lib.q3t_speaker_mel.argtypes = [_P, _fp, C.c_int32, _P, C.c_int32, C.POINTER(C.c_int32)]
 _lib.q3t_talker_forward.argtypes = [_P, _I, _fp, _ip, _P, _P]
 _lib.q3t_codepred_frame.argtypes = [_P, _I, _fp, _ip, _F, C.c_int32, C.c_uint64, C.c_int32, _ip, _P]
 _lib.q3t_cb0_select.argtypes = [_P, _I, _fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _ip, _ip,
@@ -80,7 +83,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
            "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
-           "q3t_vocoder_decode_chunked", "q3t_talker_forward",
+           "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_speaker_encode", "q3t_speaker_mel", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -262,6 +265,28 @@ class Engine:
         ns = C.c_int64(0)
         _check(_lib.q3t_vocoder_decode_chunked(self.h, codes, codes.shape[0], 16, int(chunk_frames), pcm, C.byref(ns)))
         return pcm[:ns.value]
+
+    # ---- speaker encoder
+    def speaker_dim(self):
+        """embedding length of the model's speaker encoder (0: the GGUF has none)"""
+        return _lib.q3t_speaker_dim(self.h)
+
+    def encode_speaker(self, samples):
+        """AudioTokenizerEncoder::encode (src/audio_tokenizer_encoder.h:107-108): 24 kHz samples in [-1, 1] ->
+        speaker embedding [speaker_dim]"""
+        x = np.ascontiguousarray(samples, np.float32).ravel()
+        emb = np.zeros(max(self.speaker_dim(), 1), np.float32)
+        _check(_lib.q3t_speaker_encode(self.h, x, len(x), emb))
+        return emb
+
+    def speaker_mel(self, samples):
+        """the speaker encoder's log-mel front end, [n_frames][128] (time-major)"""
+        x = np.ascontiguousarray(samples, np.float32).ravel()
+        nf = C.c_int32(0)
+        _check(_lib.q3t_speaker_mel(self.h, x, len(x), None, 0, C.byref(nf)))
+        mel = np.zeros((max(nf.value, 1), 128), np.float32)
+        _check(_lib.q3t_speaker_mel(self.h, x, len(x), _addr(mel), nf.value, C.byref(nf)))
+        return mel[:nf.value]
 
     # ---- stages
     def talker_forward(self, embd, pos):

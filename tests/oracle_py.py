@@ -65,6 +65,9 @@ def lib():
         L.q3o_generate_forced_from.argtypes = [P, ip, I, P, I, F, I, ip, I, I, P, P]
         L.q3o_vocoder_decode.argtypes = [P, ip, I, I, P, C.POINTER(C.c_int64)]
         L.q3o_codebook.argtypes = [P, I, fp]
+        L.q3o_mel.argtypes = [P, fp, I, P, C.POINTER(I)]
+        L.q3o_speaker_encode.argtypes = [P, fp, I, fp]
+        L.q3o_speaker_dim.argtypes = [P]
         L.q3o_vocoder_len.restype = C.c_int64
         L.q3o_vocoder_len.argtypes = [P, I, I]
         L.q3o_f32_to_f16.restype = C.c_uint16
@@ -216,6 +219,29 @@ class Oracle:
         if not lib().q3o_vocoder_decode(self.h, codes, F, mode, _ptr(pcm), C.byref(ns)):
             raise RuntimeError(lib().q3o_error().decode())
         return pcm[:ns.value]
+
+
+    # ---- speaker encoder
+    def speaker_dim(self):
+        return lib().q3o_speaker_dim(self.h)
+
+    def mel(self, samples):
+        """[n_frames][128] (transposed from the oracle's [128][F] to the engine's time-major layout)"""
+        x = np.ascontiguousarray(samples, np.float32)
+        nf = C.c_int(0)
+        if not lib().q3o_mel(self.h, x, len(x), None, C.byref(nf)):
+            raise RuntimeError(lib().q3o_error().decode())
+        mel = np.zeros((128, max(nf.value, 1)), np.float32)
+        if not lib().q3o_mel(self.h, x, len(x), _ptr(mel), C.byref(nf)):
+            raise RuntimeError(lib().q3o_error().decode())
+        return np.ascontiguousarray(mel[:, :nf.value].T)
+
+    def encode_speaker(self, samples):
+        x = np.ascontiguousarray(samples, np.float32)
+        emb = np.zeros(max(self.speaker_dim(), 1), np.float32)
+        if not lib().q3o_speaker_encode(self.h, x, len(x), emb):
+            raise RuntimeError(lib().q3o_error().decode())
+        return emb
 
 
 def uniform(seed, utt, frame, cb):

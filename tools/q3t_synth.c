@@ -136,6 +136,24 @@ static void build_talker(const cfg_t *c) {
         }
     }
     add1("code_pred.output_norm.weight", H, 1.0, 0.1);
+    // speaker encoder (ECAPA-TDNN) in the TTS file, as the converter writes it (convert_tts_to_gguf.py:58-124;
+    // loader audio_tokenizer_encoder.cpp:185-241): conv weights [OC, IC, K] -> ne [K, IC, OC], F32 biases
+#define SPK(nm, oc, ic, k, g) do { snprintf(b, sizeof b, "spk_enc.%s.weight", nm); addconv(b, oc, ic, k, g); \
+                                   snprintf(b, sizeof b, "spk_enc.%s.bias", nm); add1(b, oc, 0.0, 0.02); } while (0)
+    SPK("conv0", 512, 128, 5, 1.0);
+    for (int i = 1; i <= 3; ++i) {
+        char nm[64];
+        snprintf(nm, sizeof nm, "blk.%d.tdnn1", i); SPK(nm, 512, 512, 1, 1.41);
+        for (int r = 0; r < 7; ++r) { snprintf(nm, sizeof nm, "blk.%d.res2net.%d", i, r); SPK(nm, 64, 64, 3, 1.41); }
+        snprintf(nm, sizeof nm, "blk.%d.tdnn2", i); SPK(nm, 512, 512, 1, 1.41);
+        snprintf(nm, sizeof nm, "blk.%d.se.conv1", i); SPK(nm, 128, 512, 1, 1.41);
+        snprintf(nm, sizeof nm, "blk.%d.se.conv2", i); SPK(nm, 512, 128, 1, 1.0);
+    }
+    SPK("mfa", 1536, 1536, 1, 1.41);
+    SPK("asp.tdnn", 128, 4608, 1, 1.41);
+    SPK("asp.conv", 1536, 128, 1, 1.0);
+    SPK("fc", H, 3072, 1, 1.0);
+#undef SPK
     for (int i = 0; i < c->n_codebooks - 1; ++i) {
         snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
         addw(b, c->cp_vocab, H, 0.02 * sqrt((double)H) * 8.0);
@@ -381,6 +399,8 @@ int main(int argc, char **argv) {
         {"qwen3-tts.tts_bos_token_id", GV_U32, (uint32_t)c->tts_bos, 0, 0, 0, 0},
         {"qwen3-tts.tts_eos_token_id", GV_U32, (uint32_t)c->tts_eos, 0, 0, 0, 0},
         {"qwen3-tts.tts_pad_token_id", GV_U32, (uint32_t)c->tts_pad, 0, 0, 0, 0},
+        {"qwen3-tts.speaker_encoder.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
+        {"qwen3-tts.speaker_encoder.sample_rate", GV_U32, 24000, 0, 0, 0, 0},
     };
     snprintf(path, sizeof path, "%s/qwen3-tts-0.6b-f16.gguf", argv[2]);
     if (write_gguf(path, kt, (int)(sizeof kt / sizeof kt[0]), seed)) return 1;
