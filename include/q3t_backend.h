@@ -129,9 +129,26 @@ int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes /* [n_frames][
  * q3t_speaker_mel: its log-mel front end (compute_mel_spectrogram, audio_tokenizer_encoder.cpp:281-364), time-major
  * [n_frames][128]; mel may be NULL to query *n_frames. */
 int q3t_speaker_dim(const q3t_ctx *ctx);
+/* a context holding only the speaker encoder (AudioTokenizerEncoder::load_model reads only spk_enc.* tensors) */
+int q3t_ctx_create_speaker(const char *tts_gguf, int device, q3t_ctx **out);
 int q3t_speaker_encode(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *embedding);
 int q3t_speaker_mel(q3t_ctx *ctx, const float *samples, int32_t n_samples, float *mel, int32_t cap_frames,
                     int32_t *n_frames);
+
+/* ---- text tokenizer (host side; TextTokenizer, src/text_tokenizer.h:21-86 / text_tokenizer.cpp:80-349)
+ * q3t_tokenizer_load reads tokenizer.ggml.tokens / merges / *_token_id from a GGUF (the TTS model file).
+ * q3t_tokenizer_encode: for_tts != 0 wraps the text in the TTS template (encode_for_tts, :293-330); *n_tokens receives
+ * the count, tokens may be NULL to query it, Q3T_ERR when cap is too small.
+ * q3t_tokenizer_decode: bytes of the decoded text (not NUL-terminated), *n_bytes its length; text may be NULL. */
+typedef struct q3t_tokenizer q3t_tokenizer;
+int q3t_tokenizer_load(const char *gguf_path, q3t_tokenizer **out);
+void q3t_tokenizer_free(q3t_tokenizer *tok);
+int q3t_tokenizer_info(const q3t_tokenizer *tok, int32_t *vocab_size, int32_t *bos_id, int32_t *eos_id,
+                       int32_t *pad_id);
+int q3t_tokenizer_encode(const q3t_tokenizer *tok, const char *text, int64_t n_bytes /* < 0: NUL-terminated */,
+                         int for_tts, int32_t *tokens, int32_t cap, int32_t *n_tokens);
+int q3t_tokenizer_decode(const q3t_tokenizer *tok, const int32_t *tokens, int32_t n, char *text, int64_t cap,
+                         int64_t *n_bytes);
 
 /* ---- stage entry points (used by the parity tests; each syncs the context stream) */
 int q3t_talker_forward(q3t_ctx *ctx, int n_slots, const float *embd /* [n][H] */, const int32_t *pos /* [n] */,

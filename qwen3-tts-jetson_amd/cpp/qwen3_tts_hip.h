@@ -4,9 +4,12 @@
 //   qwen3_tts::TTSTransformer        src/tts_transformer.h:164-245
 //   qwen3_tts::AudioTokenizerDecoder src/audio_tokenizer_decoder.h:156-180
 //   qwen3_tts::TRTVocoderDecoder     src/trt_vocoder.h:18-42
-// so the caller (src/qwen3_tts.cpp:437-463, 518) switches by including this header instead of those three and
-// linking libqwen3_tts_hip.so + libq3t.so.  Every method forwards to one q3t_* call; all weights, KV caches and
-// scratch stay resident in HBM inside the q3t_ctx.  No exceptions cross this surface.
+//   qwen3_tts::TextTokenizer         src/text_tokenizer.h:21-86
+//   qwen3_tts::AudioTokenizerEncoder src/audio_tokenizer_encoder.h:95-125
+//   qwen3_tts::Qwen3TTS, tts_params, tts_result, load_audio_file, save_audio_file   src/qwen3_tts.h:17-156
+// so a caller switches by including this header instead of those and linking libqwen3_tts_hip.so + libq3t.so.  Every
+// method forwards to q3t_* calls; all weights, KV caches and scratch stay resident in HBM inside a q3t_ctx.  No
+// exceptions cross this surface.
 //
 // Differences a caller can see (each one deliberate):
 //  - generate() draws its samples from a counter-based generator keyed by set_seed() (default 0) instead of
@@ -17,7 +20,16 @@
 //    from the resident weights, never from the file), not re-allocated per generate() call.
 //  - TRTVocoderDecoder::load_engine takes the tokenizer GGUF (there is no TensorRT engine on MI355X); fixed_frames
 //    keeps its meaning: the independent chunk length of decode().
-//  - Extensions (MI355X-native, no reference counterpart): set_device(), set_seed(), generate_batch().
+//  - TextTokenizer::load_from_gguf takes the GGUF path (the reference takes a ggml gguf_context *: this library has no
+//    ggml); encode / encode_for_tts / decode are token-for-token the reference's (tests/test_tokenizer.py).
+//  - Qwen3TTS keeps talker, code predictor, vocoder and speaker encoder in ONE device context (one weight upload, one
+//    stream); the speaker encoder is loaded with it instead of lazily.  QWEN3_TTS_LOW_MEM is accepted and ignored
+//    (everything stays resident in 288 GB of HBM).  The vocoder follows the reference's load order: a chunked decode
+//    with the fixed_frames of the first vocoder_decoder_{40,30}.trt / vocoder_decoder_fixed.trt present in the model
+//    directory (qwen3_tts.cpp:168-198), streamed from the frame callback every 40 frames; otherwise the whole-utterance
+//    decode after generation (:492-529).
+//  - Extensions (MI355X-native, no reference counterpart): set_device(), set_seed(), generate_batch(),
+//    Qwen3TTS::synthesize_batch() / set_vocoder_chunk() / set_device() / set_seed().
 #ifndef QWEN3_TTS_HIP_H
 #define QWEN3_TTS_HIP_H
 
@@ -184,6 +196,164 @@ private:
     int32_t fixed_frames_ = 0;
     std::string error_msg_;
 };
+
+// ============================================================================ text tokenizer (src/text_tokenizer.h)
+struct tokenizer_config {
+    int32_t vocab_size = 151936;
+    int32_t pad_token_id = 151643;
+    int32_t eos_token_id = 151645;   // <|im_end|>
+    int32_t bos_token_id = 151644;   // <|im_start|>
+};
+
+class TextTokenizer {
+public:
+    TextTokenizer();
+    ~TextTokenizer();
+    TextTokenizer(const TextTokenizer &) = delete;
+    TextTokenizer &operator=(const TextTokenizer &) = delete;
+
+    bool load_from_gguf(const std::string &gguf_path);
+    std::vector<int32_t> encode(const std::string &text) const;
+    // <|im_start|>assistant\n{text}<|im_end|>\n<|im_start|>assistant\n
+    std::vector<int32_t> encode_for_tts(const std::string &text) const;
+    std::string decode(const std::vector<int32_t> &tokens) const;
+    std::string decode_token(int32_t token_id) const;
+    const tokenizer_config &get_config() const { return config_; }
+    const std::string &get_error() const { return error_msg_; }
+    bool is_loaded() const { return tok_ != nullptr; }
+    int32_t bos_token_id() const { return config_.bos_token_id; }
+    int32_t eos_token_id() const { return config_.eos_token_id; }
+    int32_t pad_token_id() const { return config_.pad_token_id; }
+
+private:
+    struct q3t_tokenizer *tok_ = nullptr;
+    tokenizer_config config_;
+    std::string error_msg_;
+};
+
+// ================================================================ speaker encoder (src/audio_tokenizer_encoder.h)
+struct speaker_encoder_config {
+    int32_t sample_rate = 24000;
+    int32_t n_mels = 128;
+    int32_t n_fft = 1024;
+    int32_t hop_length = 256;
+    int32_t win_length = 1024;
+    int32_t embedding_dim = 1024;
+    int32_t hidden_dim = 512;
+    int32_t n_res2net_blocks = 3;
+    int32_t res2net_scale = 8;
+    float f_min = 0.0f;
+    float f_max = 12000.0f;
+};
+
+class AudioTokenizerEncoder {
+public:
+    AudioTokenizerEncoder();
+    ~AudioTokenizerEncoder();
+    AudioTokenizerEncoder(const AudioTokenizerEncoder &) = delete;
+    AudioTokenizerEncoder &operator=(const AudioTokenizerEncoder &) = delete;
+
+    // the TTS GGUF; only its spk_enc.* tensors are read
+    bool load_model(const std::string &model_path);
+    // samples in [-1, 1] at 24 kHz -> embedding [embedding_dim]
+    bool encode(const float *samples, int32_t n_samples, std::vector<float> &embedding);
+    const speaker_encoder_config &get_config() const { return config_; }
+    const std::string &get_error() const { return error_msg_; }
+    bool set_device(int device);
+
+private:
+    q3t_ctx *ctx_ = nullptr;
+    int device_ = 0;
+    speaker_encoder_config config_;
+    std::string error_msg_;
+};
+
+// ====================================================================================== pipeline (src/qwen3_tts.h)
+struct tts_params {
+    int32_t max_audio_tokens = 4096;
+    float temperature = 0.9f;
+    float top_p = 1.0f;       // accepted, unused (as in the reference: no top-p stage exists in its sampler)
+    int32_t top_k = 50;
+    int32_t n_threads = 4;    // accepted, unused (host threads do no numeric work here)
+    bool print_progress = false;
+    bool print_timing = true;
+    float repetition_penalty = 1.05f;
+};
+
+struct tts_result {
+    std::vector<float> audio;
+    int32_t sample_rate = 24000;
+    bool success = false;
+    std::string error_msg;
+    int64_t t_load_ms = 0;
+    int64_t t_tokenize_ms = 0;
+    int64_t t_encode_ms = 0;
+    int64_t t_generate_ms = 0;
+    int64_t t_decode_ms = 0;
+    int64_t t_total_ms = 0;
+    uint64_t mem_rss_start_bytes = 0;
+    uint64_t mem_rss_end_bytes = 0;
+    uint64_t mem_rss_peak_bytes = 0;
+    uint64_t mem_phys_start_bytes = 0;
+    uint64_t mem_phys_end_bytes = 0;
+    uint64_t mem_phys_peak_bytes = 0;
+};
+
+class Qwen3TTS {
+public:
+    Qwen3TTS();
+    ~Qwen3TTS();
+    Qwen3TTS(const Qwen3TTS &) = delete;
+    Qwen3TTS &operator=(const Qwen3TTS &) = delete;
+
+    // model_dir holds qwen3-tts-0.6b-f16.gguf and qwen3-tts-tokenizer-f16.gguf (qwen3_tts.cpp:117-118)
+    bool load_models(const std::string &model_dir);
+    tts_result synthesize(const std::string &text, const tts_params &params = tts_params());
+    tts_result synthesize_with_voice(const std::string &text, const std::string &reference_audio,
+                                     const tts_params &params = tts_params());
+    tts_result synthesize_with_voice(const std::string &text, const float *ref_samples, int32_t n_ref_samples,
+                                     const tts_params &params = tts_params());
+    bool encode_speaker(const std::string &reference_audio, std::vector<float> &embedding);
+    tts_result synthesize_with_embedding(const std::string &text, const std::vector<float> &speaker_embedding,
+                                         const tts_params &params = tts_params());
+    const std::string &get_error() const { return error_msg_; }
+    bool is_loaded() const { return models_loaded_; }
+
+    // ---- MI355X extensions
+    bool set_device(int device);           // before load_models
+    void set_seed(uint64_t seed) { seed_ = seed; }
+    // 0: whole-utterance vocoder after generation; n > 0: n-frame chunks streamed from the frame callback
+    void set_vocoder_chunk(int32_t frames) { vocoder_chunk_ = frames; }
+    int32_t vocoder_chunk() const { return vocoder_chunk_; }
+    // n utterances decoded together on one GPU (lock-step slots); speaker_embeddings empty or one per text (an empty
+    // vector = no speaker row); results[i] as synthesize_with_embedding's
+    std::vector<tts_result> synthesize_batch(const std::vector<std::string> &texts,
+                                             const std::vector<std::vector<float>> &speaker_embeddings,
+                                             const tts_params &params = tts_params());
+
+private:
+    tts_result synthesize_internal(const std::string &text, const float *speaker_embedding, const tts_params &params,
+                                   tts_result &result);
+    bool ensure_slots(int32_t slots, int32_t max_len);
+
+    TextTokenizer tokenizer_;
+    q3t_ctx *ctx_ = nullptr;
+    int device_ = 0;
+    uint64_t seed_ = 0;
+    int32_t slots_ = 0, n_ctx_ = 0, hidden_ = 1024;
+    int32_t vocoder_chunk_ = 0;
+    bool models_loaded_ = false;
+    std::string error_msg_;
+    std::string tts_model_path_;
+    std::string decoder_model_path_;
+};
+
+// WAV: RIFF PCM16 / PCM32 / IEEE float32, channels averaged to mono (qwen3_tts.cpp:567-706)
+bool load_audio_file(const std::string &path, std::vector<float> &samples, int &sample_rate);
+// WAV PCM16 mono, samples clamped to [-1, 1] and scaled by 32767 (qwen3_tts.cpp:708-759)
+bool save_audio_file(const std::string &path, const std::vector<float> &samples, int sample_rate);
+// linear resampling used for reference audio (qwen3_tts.cpp:83-101)
+void resample_linear(const float *input, int input_len, int input_rate, std::vector<float> &output, int output_rate);
 
 }  // namespace qwen3_tts
 

@@ -7,7 +7,12 @@
 #include "comm.h"
 #include "engine.h"
 #include "speaker.h"
+#include "tokenizer.h"
 #include "vocoder.h"
+
+struct q3t_tokenizer {
+    q3t::TextTokenizer tok;
+};
 
 struct q3t_ctx {
     q3t::Engine engine;
@@ -247,6 +252,20 @@ int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes, int32_t n_fra
     GUARD_END
 }
 
+int q3t_ctx_create_speaker(const char *tts_gguf, int device, q3t_ctx **out) {
+    GUARD_BEGIN
+    if (!out || !tts_gguf) { q3t::set_error("null argument"); return Q3T_ERR; }
+    *out = nullptr;
+    q3t_ctx *c = new q3t_ctx();
+    if (!c->engine.load_speaker_only(tts_gguf, device)) {
+        delete c;
+        return Q3T_ERR;
+    }
+    *out = c;
+    return Q3T_OK;
+    GUARD_END
+}
+
 int q3t_speaker_dim(const q3t_ctx *ctx) {
     if (!ctx) return 0;
     q3t::SpeakerEncoder *s = const_cast<q3t::Engine &>(ctx->engine).speaker();
@@ -277,6 +296,57 @@ int q3t_speaker_mel(q3t_ctx *ctx, const float *samples, int32_t n_samples, float
     if (mel) {
         if (cap_frames < F) { q3t::set_error("mel buffer too small"); return Q3T_ERR; }
         std::copy(m.begin(), m.end(), mel);
+    }
+    return Q3T_OK;
+    GUARD_END
+}
+
+int q3t_tokenizer_load(const char *gguf_path, q3t_tokenizer **out) {
+    GUARD_BEGIN
+    if (!gguf_path || !out) { q3t::set_error("null argument"); return Q3T_ERR; }
+    *out = nullptr;
+    q3t_tokenizer *t = new q3t_tokenizer();
+    if (!t->tok.load(std::string(gguf_path))) { delete t; return Q3T_ERR; }
+    *out = t;
+    return Q3T_OK;
+    GUARD_END
+}
+
+void q3t_tokenizer_free(q3t_tokenizer *tok) { delete tok; }
+
+int q3t_tokenizer_info(const q3t_tokenizer *tok, int32_t *vocab_size, int32_t *bos_id, int32_t *eos_id, int32_t *pad_id) {
+    if (!tok) { q3t::set_error("null tokenizer"); return Q3T_ERR; }
+    if (vocab_size) *vocab_size = tok->tok.vocab_size();
+    if (bos_id) *bos_id = tok->tok.bos();
+    if (eos_id) *eos_id = tok->tok.eos();
+    if (pad_id) *pad_id = tok->tok.pad();
+    return Q3T_OK;
+}
+
+int q3t_tokenizer_encode(const q3t_tokenizer *tok, const char *text, int64_t n_bytes, int for_tts, int32_t *tokens,
+                         int32_t cap, int32_t *n_tokens) {
+    GUARD_BEGIN
+    if (!tok || !text || !n_tokens) { q3t::set_error("null argument"); return Q3T_ERR; }
+    const std::string t = n_bytes < 0 ? std::string(text) : std::string(text, (size_t)n_bytes);
+    const std::vector<int32_t> ids = for_tts ? tok->tok.encode_for_tts(t) : tok->tok.encode(t);
+    *n_tokens = (int32_t)ids.size();
+    if (tokens) {
+        if (cap < (int32_t)ids.size()) { q3t::set_error("token buffer too small"); return Q3T_ERR; }
+        std::copy(ids.begin(), ids.end(), tokens);
+    }
+    return Q3T_OK;
+    GUARD_END
+}
+
+int q3t_tokenizer_decode(const q3t_tokenizer *tok, const int32_t *tokens, int32_t n, char *text, int64_t cap,
+                         int64_t *n_bytes) {
+    GUARD_BEGIN
+    if (!tok || !n_bytes || (n > 0 && !tokens)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    const std::string s = tok->tok.decode(std::vector<int32_t>(tokens, tokens + std::max(n, 0)));
+    *n_bytes = (int64_t)s.size();
+    if (text) {
+        if (cap < (int64_t)s.size()) { q3t::set_error("text buffer too small"); return Q3T_ERR; }
+        std::copy(s.begin(), s.end(), text);
     }
     return Q3T_OK;
     GUARD_END

@@ -157,6 +157,25 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     return true;
 }
 
+bool Engine::load_speaker_only(const std::string &tts_gguf, int device) {
+    device_ = device;
+    tts_path_ = tts_gguf;
+    talker_ = false;
+    Q3T_HIP(hipSetDevice(device));
+    Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    Gguf g;
+    if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
+    size_t total = 0;
+    for (const GgufTensor &t : g.tensors())
+        if (t.name.rfind("spk_enc.", 0) == 0) total += (t.nbytes() + 255) & ~(size_t)255;
+    if (total == 0) { set_error("No speaker encoder tensors found in model"); return false; }
+    if (!wa_.reserve(total + ((size_t)1 << 20))) return false;
+    spk_.reset(new SpeakerEncoder());
+    if (!spk_->load(g, wa_, stream_)) return false;
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
 std::vector<WeightArena *> Engine::weight_arenas() {
     std::vector<WeightArena *> v{&wa_};
     if (voc_ && voc_->loaded()) v.push_back(&voc_->weights());

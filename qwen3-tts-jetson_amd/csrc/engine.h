@@ -76,6 +76,9 @@ public:
     int max_slots() const { return max_slots_; }
     int device() const { return device_; }
     const std::string &tts_path() const { return tts_path_; }
+    // speaker-encoder-only context (AudioTokenizerEncoder::load_model, audio_tokenizer_encoder.cpp: only the
+    // spk_enc.* tensors of the TTS GGUF are read)
+    bool load_speaker_only(const std::string &tts_gguf, int device);
     bool has_talker() const { return talker_; }
     const std::string &tok_path() const { return tok_path_; }
     int max_ctx() const { return max_ctx_; }

@@ -57,7 +57,8 @@ bool read_value(Reader &r, uint32_t type, GgufValue &v, int depth = 0) {
         for (uint64_t i = 0; i < n; ++i) {
             GgufValue e;
             if (!read_value(r, et, e, depth + 1)) return false;
-            v.arr.push_back((int64_t)e.u);
+            if (et == 8) v.sarr.push_back(std::move(e.s));
+            else v.arr.push_back((int64_t)e.u);
         }
         return true;
     }
@@ -136,6 +137,11 @@ bool Gguf::open(const std::string &path) {
 const GgufTensor *Gguf::find(const std::string &name) const {
     auto it = index_.find(name);
     return it == index_.end() ? nullptr : &tensors_[it->second];
+}
+
+const GgufValue *Gguf::get(const std::string &key) const {
+    auto it = kv_.find(key);
+    return it == kv_.end() ? nullptr : &it->second;
 }
 
 int64_t Gguf::get_int(std::initializer_list<const char *> keys, int64_t def) const {

@@ -27,6 +27,7 @@ struct GgufValue {
     double f = 0.0;
     std::string s;
     std::vector<int64_t> arr;
+    std::vector<std::string> sarr;   // string arrays (tokenizer.ggml.tokens / merges)
 };
 
 class Gguf {
@@ -38,6 +39,7 @@ public:
     // first present key wins, like the lambdas of tts_transformer.cpp:289-307
     int64_t get_int(std::initializer_list<const char *> keys, int64_t def) const;
     float get_f32(std::initializer_list<const char *> keys, float def) const;
+    const GgufValue *get(const std::string &key) const;
     const std::vector<GgufTensor> &tensors() const { return tensors_; }
     const std::string &error() const { return err_; }
 

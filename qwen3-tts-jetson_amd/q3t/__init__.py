@@ -70,8 +70,14 @@ _lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_vocoder_decode_chunked.argtypes = [_P, _ip, C.c_int32, C.c_int32, C.c_int32, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_speaker_dim.argtypes = [_P]
+_lib.q3t_ctx_create_speaker.argtypes = [C.c_char_p, _I, C.POINTER(_P)]
 _lib.q3t_speaker_encode.argtypes = [_P, _fp, C.c_int32, _fp]
 _lib.q3t_speaker_mel.argtypes = [_P, _fp, C.c_int32, _P, C.c_int32, C.POINTER(C.c_int32)]
+_lib.q3t_tokenizer_load.argtypes = [C.c_char_p, C.POINTER(_P)]
+_lib.q3t_tokenizer_free.argtypes = [_P]
+_lib.q3t_tokenizer_info.argtypes = [_P] + [C.POINTER(C.c_int32)] * 4
+_lib.q3t_tokenizer_encode.argtypes = [_P, C.c_char_p, C.c_int64, _I, _P, C.c_int32, C.POINTER(C.c_int32)]
+_lib.q3t_tokenizer_decode.argtypes = [_P, _P, C.c_int32, _P, C.c_int64, C.POINTER(C.c_int64)]
 _lib.q3t_talker_forward.argtypes = [_P, _I, _fp, _ip, _P, _P]
 _lib.q3t_codepred_frame.argtypes = [_P, _I, _fp, _ip, _F, C.c_int32, C.c_uint64, C.c_int32, _ip, _P]
 _lib.q3t_cb0_select.argtypes = [_P, _I, _fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _ip, _ip,
@@ -83,7 +89,9 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
            "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
-           "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_speaker_encode", "q3t_speaker_mel", "q3t_talker_forward",
+           "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
+           "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
+           "q3t_tokenizer_decode", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -121,6 +129,49 @@ def comm_unique_id():
     return buf.raw
 
 
+class Tokenizer:
+    """TextTokenizer (src/text_tokenizer.h): byte-level BPE + the TTS template, read from the TTS GGUF.  Host only."""
+
+    def __init__(self, gguf_path):
+        h = _P()
+        _check(_lib.q3t_tokenizer_load(gguf_path.encode(), C.byref(h)))
+        self.h = h
+        v, b, e, p = (C.c_int32() for _ in range(4))
+        _check(_lib.q3t_tokenizer_info(self.h, C.byref(v), C.byref(b), C.byref(e), C.byref(p)))
+        self.vocab_size, self.bos, self.eos, self.pad = v.value, b.value, e.value, p.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.q3t_tokenizer_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode(self, text, for_tts=False):
+        raw = text.encode("utf-8", errors="surrogateescape") if isinstance(text, str) else bytes(text)
+        n = C.c_int32(0)
+        _check(_lib.q3t_tokenizer_encode(self.h, raw, len(raw), int(bool(for_tts)), None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.int32)
+        _check(_lib.q3t_tokenizer_encode(self.h, raw, len(raw), int(bool(for_tts)), _addr(out), n.value, C.byref(n)))
+        return out[:n.value].tolist()
+
+    def encode_for_tts(self, text):
+        return self.encode(text, for_tts=True)
+
+    def decode(self, ids):
+        """bytes of the decoded text"""
+        a = np.ascontiguousarray(ids, np.int32)
+        nb = C.c_int64(0)
+        _check(_lib.q3t_tokenizer_decode(self.h, _addr(a), len(a), None, 0, C.byref(nb)))
+        buf = C.create_string_buffer(max(nb.value, 1))
+        _check(_lib.q3t_tokenizer_decode(self.h, _addr(a), len(a), buf, nb.value, C.byref(nb)))
+        return buf.raw[:nb.value]
+
+
 class Engine:
     """One device context (TTSTransformer + code predictor + vocoder resident in HBM)."""
 
@@ -144,6 +195,13 @@ class Engine:
         _check(_lib.q3t_ctx_create_shared(tts_gguf.encode(), tokenizer_gguf.encode() if tokenizer_gguf else None,
                                           int(device), int(max_slots), int(max_ctx), int(rank), int(world), uid,
                                           C.byref(h)))
+        return cls(_handle=h)
+
+    @classmethod
+    def speaker_only(cls, tts_gguf, device=0):
+        """a context with only the speaker encoder loaded (AudioTokenizerEncoder::load_model)"""
+        h = _P()
+        _check(_lib.q3t_ctx_create_speaker(tts_gguf.encode(), int(device), C.byref(h)))
         return cls(_handle=h)
 
     def replica(self, device=0, max_slots=1, max_ctx=4096 + 32):

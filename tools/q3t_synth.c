@@ -252,12 +252,112 @@ static void build_tokenizer(const cfg_t *c) {
     add1("tok_dec.dec.6.conv.bias", 1, 0.0, 0.002);
 }
 
+// ---------------------------------------------------------------- text vocabulary (tokenizer.ggml.*)
+// The converter writes vocab.json's tokens sorted by id, pads the list with "[PAD<id>]" up to text_vocab_size, and adds
+// merges.txt (convert_tts_to_gguf.py:337-377, 498-547); Qwen's special tokens are not in vocab.json, so ids >= 151643
+// are pads and the tokenizer falls back to its default bos / eos ids (text_tokenizer.h:13-18).  Synthetic stand-in:
+// ids 0..255 are the GPT-2 byte symbols in Qwen's own order (id 13 = ".", 198 = "Ċ", 220 = "Ġ"), a word list is
+// merged left to right into whole-word tokens ("Hello" at Qwen's id 9707, "assistant" at 77091, the ids of the
+// reference's known-answer vector, tests/test_tokenizer.cpp:14), the rest are "[SYN<id>]" fillers.
+static const char *VOCAB_WORDS[] = {
+    "Hello", "assistant", "hello", "world", "the", "of", "and", "to", "in", "is", "you", "that", "it", "he", "was",
+    "for", "on", "are", "as", "with", "his", "they", "at", "be", "this", "This", "have", "from", "or", "one", "had",
+    "by", "word", "but", "not", "what", "all", "were", "we", "when", "your", "can", "said", "there", "use", "an",
+    "each", "which", "she", "do", "how", "their", "if", "will", "up", "other", "about", "out", "many", "then", "them",
+    "these", "so", "some", "her", "would", "make", "like", "him", "into", "time", "has", "look", "two", "more",
+    "write", "go", "see", "number", "no", "way", "could", "people", "my", "than", "first", "water", "been", "call",
+    "who", "its", "now", "find", "long", "down", "day", "did", "get", "come", "made", "may", "part", "test", "speech",
+    "voice", "quick", "brown", "fox", "jumps", "over", "lazy", "dog", "The", "It", "We", "GPU", "audio", "text",
+    "model", "ing", "ed", "er", "ly", "tion", "ation", "123", "2026", "!!", "...", ".\n", "\n\n"};
+static char **g_vocab = NULL;
+static int g_nvocab = 0, g_nmerge = 0;
+static char **g_merges = NULL;
+static int *g_toktype = NULL;
+
+static void byte_sym(int b, char out[4]) {   // GPT-2 bytes_to_unicode: printable latin-1 keep their code point
+    int cp;
+    if ((b >= 33 && b <= 126) || (b >= 161 && b <= 172) || b >= 174) cp = b;
+    else {
+        int n = 0;
+        for (int x = 0; x < b; ++x) n += !((x >= 33 && x <= 126) || (x >= 161 && x <= 172) || x >= 174);
+        cp = 256 + n;
+    }
+    if (cp < 0x80) { out[0] = (char)cp; out[1] = 0; }
+    else { out[0] = (char)(0xC0 | (cp >> 6)); out[1] = (char)(0x80 | (cp & 0x3F)); out[2] = 0; }
+}
+static int vocab_find(const char *t) {
+    for (int i = 0; i < g_nvocab; ++i) if (g_vocab[i] && strcmp(g_vocab[i], t) == 0) return i;
+    return -1;
+}
+static int g_next_id = 256;
+static int vocab_add(const char *t, int want) {
+    int id = vocab_find(t);
+    if (id >= 0) return id;
+    if (want < 0) {
+        while (g_next_id < g_nvocab && (g_vocab[g_next_id] || g_next_id == 9707 || g_next_id == 77091)) ++g_next_id;
+        want = g_next_id;
+    }
+    if (want >= g_nvocab || g_vocab[want]) return -1;
+    g_vocab[want] = strdup(t);
+    return want;
+}
+static void build_vocab(const cfg_t *c) {
+    g_nvocab = c->text_vocab;
+    g_vocab = calloc((size_t)g_nvocab, sizeof(char *));
+    g_toktype = malloc(sizeof(int) * (size_t)g_nvocab);
+    g_merges = malloc(sizeof(char *) * 8192);
+    // byte symbols in Qwen order: the printable ones (by byte value), then the remapped ones
+    int id = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int b = 0; b < 256; ++b) {
+            const int printable = (b >= 33 && b <= 126) || (b >= 161 && b <= 172) || b >= 174;
+            if (printable != (pass == 0)) continue;
+            char s[4];
+            byte_sym(b, s);
+            g_vocab[id++] = strdup(s);
+        }
+    const int n_real = c->text_vocab > 151643 ? 151643 : c->text_vocab;   // ids the converter takes from vocab.json
+    for (size_t w = 0; w < sizeof VOCAB_WORDS / sizeof VOCAB_WORDS[0]; ++w)
+        for (int sp = 0; sp < 2; ++sp) {
+            // GPT-2 symbols of (" " +) word, merged left to right
+            char sym[64][8];
+            int n = 0;
+            if (sp) { byte_sym(' ', sym[n]); ++n; }
+            for (const unsigned char *p = (const unsigned char *)VOCAB_WORDS[w]; *p && n < 63; ++p) byte_sym(*p, sym[n++]);
+            char acc[512] = "";
+            strcat(acc, sym[0]);
+            for (int k = 1; k < n; ++k) {
+                char merged[512];
+                snprintf(merged, sizeof merged, "%s%s", acc, sym[k]);
+                int want = -1;
+                if (k == n - 1 && !sp && strcmp(VOCAB_WORDS[w], "Hello") == 0 && 9707 < n_real) want = 9707;
+                if (k == n - 1 && !sp && strcmp(VOCAB_WORDS[w], "assistant") == 0 && 77091 < n_real) want = 77091;
+                if (vocab_find(merged) < 0) {
+                    if (g_next_id >= n_real && want < 0) break;
+                    if (vocab_add(merged, want) < 0) break;
+                    char m[1024];
+                    snprintf(m, sizeof m, "%s %s", acc, sym[k]);
+                    if (g_nmerge < 8192) g_merges[g_nmerge++] = strdup(m);
+                }
+                strcpy(acc, merged);
+            }
+        }
+    for (int i = 0; i < g_nvocab; ++i) {
+        if (!g_vocab[i]) {
+            char b[32];
+            snprintf(b, sizeof b, i < n_real ? "[SYN%d]" : "[PAD%d]", i);
+            g_vocab[i] = strdup(b);
+        }
+        g_toktype[i] = i < n_real ? 1 : 5;   // NORMAL / UNUSED (gguf.TokenType)
+    }
+}
+
 // ---------------------------------------------------------------- GGUF v3 writer
 static void w_u32(FILE *f, uint32_t v) { fwrite(&v, 4, 1, f); }
 static void w_u64(FILE *f, uint64_t v) { fwrite(&v, 8, 1, f); }
 static void w_str(FILE *f, const char *s) { w_u64(f, strlen(s)); fwrite(s, 1, strlen(s), f); }
 
-typedef struct { const char *key; int type; uint32_t u; float fl; const char *s; int arr_n; const int *arr; } kv_t;
+typedef struct { const char *key; int type; uint32_t u; float fl; const char *s; int arr_n; const int *arr; char **sarr; } kv_t;
 
 static uint16_t f32_to_f16_rne(float x) {
     uint32_t u; memcpy(&u, &x, 4);
@@ -309,7 +409,11 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
         if (kvs[i].type == GV_U32) w_u32(f, kvs[i].u);
         else if (kvs[i].type == GV_F32) fwrite(&kvs[i].fl, 4, 1, f);
         else if (kvs[i].type == GV_STR) w_str(f, kvs[i].s);
-        else if (kvs[i].type == GV_ARR) {
+        else if (kvs[i].type == GV_ARR && kvs[i].sarr) {   // string array
+            w_u32(f, GV_STR);
+            w_u64(f, (uint64_t)kvs[i].arr_n);
+            for (int j = 0; j < kvs[i].arr_n; ++j) w_str(f, kvs[i].sarr[j]);
+        } else if (kvs[i].type == GV_ARR) {
             w_u32(f, GV_U32 + 1);  // INT32 array
             w_u64(f, (uint64_t)kvs[i].arr_n);
             for (int j = 0; j < kvs[i].arr_n; ++j) w_u32(f, (uint32_t)kvs[i].arr[j]);
@@ -369,6 +473,7 @@ int main(int argc, char **argv) {
     char path[4096];
 
     build_talker(c);
+    build_vocab(c);
     kv_t kt[] = {
         {"general.architecture", GV_STR, 0, 0, "qwen3-tts", 0, 0},
         {"general.name", GV_STR, 0, 0, c->name, 0, 0},
@@ -401,6 +506,11 @@ int main(int argc, char **argv) {
         {"qwen3-tts.tts_pad_token_id", GV_U32, (uint32_t)c->tts_pad, 0, 0, 0, 0},
         {"qwen3-tts.speaker_encoder.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
         {"qwen3-tts.speaker_encoder.sample_rate", GV_U32, 24000, 0, 0, 0, 0},
+        {"tokenizer.ggml.model", GV_STR, 0, 0, "gpt2", 0, 0},
+        {"tokenizer.ggml.pre", GV_STR, 0, 0, "qwen2", 0, 0},
+        {"tokenizer.ggml.tokens", GV_ARR, 0, 0, 0, g_nvocab, 0, g_vocab},
+        {"tokenizer.ggml.token_type", GV_ARR, 0, 0, 0, g_nvocab, g_toktype},
+        {"tokenizer.ggml.merges", GV_ARR, 0, 0, 0, g_nmerge, 0, g_merges},
     };
     snprintf(path, sizeof path, "%s/qwen3-tts-0.6b-f16.gguf", argv[2]);
     if (write_gguf(path, kt, (int)(sizeof kt / sizeof kt[0]), seed)) return 1;
