@@ -67,7 +67,7 @@ uint16_t q3o_f32_to_f16(float x) {
 static inline float f16r(float x) { return q3o_f16_to_f32(q3o_f32_to_f16(x)); }
 
 /* ------------------------------------------------------------------ GGUF reader (v2/v3) */
-typedef struct { char *name; int nd; int64_t ne[4]; int type; uint64_t off; } gtensor;
+typedef struct { char *name; int nd; int64_t ne[4]; int type, src_type; uint64_t off; uint16_t *own; } gtensor;
 typedef struct { char *key; int type; uint64_t u; double f; } gkv;
 typedef struct {
     uint8_t *map; size_t size; uint64_t data_off;
@@ -111,9 +111,57 @@ static int skip_val(const uint8_t **p, const uint8_t *end, uint32_t type, gkv *o
     }
     return 1;
 }
+/* ggml-quants.c dequantize_row_{q8_0,q4_0,q4_K} (the reference's ggml submodule, not vendored: restated from the
+ * published block layouts).  Weight files of every converter dtype (convert_tts_to_gguf.py:276-335) load as if they
+ * were the F16 file: quantised and 2-D+ F32 matrices become owned F16 copies, exactly as the product reader does. */
+static size_t gtype_bytes(int type, int64_t n) {
+    switch (type) {
+        case 0: return (size_t)n * 4;
+        case 1: return (size_t)n * 2;
+        case 8: return n % 32 ? 0 : (size_t)(n / 32) * 34;
+        case 2: return n % 32 ? 0 : (size_t)(n / 32) * 18;
+        case 12: return n % 256 ? 0 : (size_t)(n / 256) * 144;
+        default: return 0;
+    }
+}
+static float rd_h(const uint8_t *p) { uint16_t h; memcpy(&h, p, 2); return q3o_f16_to_f32(h); }
+static void dequant_row(int type, const uint8_t *b, float *y, int64_t n) {
+    if (type == 0) { memcpy(y, b, (size_t)n * 4); return; }
+    if (type == 8) {
+        for (int64_t k = 0; k < n / 32; ++k, b += 34) {
+            const float d = rd_h(b);
+            for (int j = 0; j < 32; ++j) y[k * 32 + j] = d * (float)(int8_t)b[2 + j];
+        }
+    } else if (type == 2) {
+        for (int64_t k = 0; k < n / 32; ++k, b += 18) {
+            const float d = rd_h(b);
+            for (int j = 0; j < 16; ++j) {
+                y[k * 32 + j] = (float)((b[2 + j] & 15) - 8) * d;
+                y[k * 32 + j + 16] = (float)((b[2 + j] >> 4) - 8) * d;
+            }
+        }
+    } else if (type == 12) {
+        for (int64_t k = 0; k < n / 256; ++k, b += 144) {
+            const float d = rd_h(b), dmin = rd_h(b + 2);
+            const uint8_t *sc = b + 4, *q = b + 16;
+            float *o = y + k * 256;
+            for (int is = 0; is < 8; is += 2, q += 32) {
+                int s[2], m[2];
+                for (int u = 0; u < 2; ++u) {
+                    const int j = is + u;
+                    if (j < 4) { s[u] = sc[j] & 63; m[u] = sc[j + 4] & 63; }
+                    else { s[u] = (sc[j + 4] & 15) | ((sc[j - 4] >> 6) << 4); m[u] = (sc[j + 4] >> 4) | ((sc[j] >> 6) << 4); }
+                }
+                for (int l = 0; l < 32; ++l) *o++ = d * s[0] * (q[l] & 15) - dmin * m[0];
+                for (int l = 0; l < 32; ++l) *o++ = d * s[1] * (q[l] >> 4) - dmin * m[1];
+            }
+        }
+    }
+}
+
 static void gguf_close(gguf_t *g) {
     if (!g) return;
-    for (int64_t i = 0; i < g->nt; ++i) free(g->t[i].name);
+    for (int64_t i = 0; i < g->nt; ++i) { free(g->t[i].name); free(g->t[i].own); }
     for (int64_t i = 0; i < g->nkv; ++i) free(g->kv[i].key);
     free(g->t); free(g->kv);
     if (g->map) munmap(g->map, g->size);
@@ -144,7 +192,7 @@ static gguf_t *gguf_open(const char *path) {
     }
     g->t = calloc((size_t)g->nt + 1, sizeof(gtensor));
     for (int64_t i = 0; i < g->nt; ++i) {
-        uint32_t nd, type;
+        uint32_t nd = 0, type = 0;
         g->t[i].name = rd_str(&p, end);
         if (!g->t[i].name || !rd(&p, end, &nd, 4) || nd > 4) { gguf_close(g); snprintf(g_err, sizeof g_err, "bad tensor info"); return NULL; }
         g->t[i].nd = (int)nd;
@@ -155,6 +203,23 @@ static gguf_t *gguf_open(const char *path) {
     }
     uint64_t pos = (uint64_t)(p - g->map);
     g->data_off = (pos + alignment - 1) / alignment * alignment;
+    for (int64_t i = 0; i < g->nt; ++i) {
+        gtensor *t = &g->t[i];
+        t->src_type = t->type;
+        const int64_t n = t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3], row = t->ne[0];
+        const size_t rb = gtype_bytes(t->type, row);
+        if (t->type == 1 || (t->type == 0 && t->nd == 1) || rb == 0) continue;
+        if (g->data_off + t->off + gtype_bytes(t->type, n) > g->size) continue;
+        t->own = malloc(sizeof(uint16_t) * (size_t)n);
+        float *f = malloc(sizeof(float) * (size_t)row);
+        const uint8_t *src = g->map + g->data_off + t->off;
+        for (int64_t r = 0; r < n / row; ++r) {
+            dequant_row(t->type, src + (size_t)r * rb, f, row);
+            for (int64_t c = 0; c < row; ++c) t->own[(size_t)r * row + c] = q3o_f32_to_f16(f[c]);
+        }
+        free(f);
+        t->type = 1;
+    }
     return g;
 }
 static const gtensor *gfind(const gguf_t *g, const char *name) {
@@ -213,7 +278,7 @@ struct q3o_model {
     struct { conv_t tdnn1, tdnn2, res[7], se1, se2; } spk_blk[3];
 };
 
-static const void *tdata(const gguf_t *g, const gtensor *t) { return g->map + g->data_off + t->off; }
+static const void *tdata(const gguf_t *g, const gtensor *t) { return t->own ? (const void *)t->own : g->map + g->data_off + t->off; }
 
 static int get_mat(const gguf_t *g, const char *name, int rows, int cols, mat16 *out) {
     const gtensor *t = gfind(g, name);
@@ -1518,6 +1583,19 @@ static int64_t full_len(const q3o_model *m, int F) {
     for (int d = 0; d < 4; ++d) { const int s = m->c.rates[d], K = m->c.conv_t_k[d]; T = (T - 1) * s + K - 2 * (K - s); }
     return T;
 }
+int q3o_tensor(const q3o_model *m, const char *name, float *out, int64_t n, int *src_type) {
+    const gguf_t *g = m->gt;
+    const gtensor *t = gfind(g, name);
+    if (!t && m->gk) { g = m->gk; t = gfind(g, name); }
+    if (!t) FAIL("missing tensor %s", name);
+    const int64_t ne = t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
+    if (ne != n || (t->type != 0 && t->type != 1)) FAIL("tensor %s: %lld elements of type %d", name, (long long)ne, t->type);
+    const void *d = tdata(g, t);
+    for (int64_t i = 0; i < n; ++i) out[i] = t->type == 1 ? q3o_f16_to_f32(((const uint16_t *)d)[i]) : ((const float *)d)[i];
+    if (src_type) *src_type = t->src_type;
+    return 1;
+}
+
 int q3o_codebook(const q3o_model *m, int i, float *out) {
     if (!m->c.has_vocoder || i < 0 || i > 15) FAIL("no codebook %d", i);
     const uint16_t *cb = i == 0 ? m->cb_first : m->cb_rest[i - 1];

@@ -92,6 +92,9 @@ int64_t q3o_vocoder_len(const q3o_model *m, int n_frames, int mode);
 int q3o_mel(const q3o_model *m, const float *samples, int n, float *mel, int *n_frames);
 int q3o_speaker_encode(const q3o_model *m, const float *samples, int n, float *embedding);
 int q3o_speaker_dim(const q3o_model *m);
+/* a tensor of either file as the model sees it (F16 weights / F32 vectors; quantised files dequantised at open), f32;
+ * *src_type = the on-disk GGML type */
+int q3o_tensor(const q3o_model *m, const char *name, float *out, int64_t n, int *src_type);
 /* codebook i (0 = vq_first, 1..15 = vq_rest.i-1) as f32 [cb_size][cb_dim], after normalize_codebooks */
 int q3o_codebook(const q3o_model *m, int i, float *out);
 

@@ -68,6 +68,7 @@ def lib():
         L.q3o_mel.argtypes = [P, fp, I, P, C.POINTER(I)]
         L.q3o_speaker_encode.argtypes = [P, fp, I, fp]
         L.q3o_speaker_dim.argtypes = [P]
+        L.q3o_tensor.argtypes = [P, C.c_char_p, fp, C.c_int64, C.POINTER(I)]
         L.q3o_vocoder_len.restype = C.c_int64
         L.q3o_vocoder_len.argtypes = [P, I, I]
         L.q3o_f32_to_f16.restype = C.c_uint16
@@ -220,6 +221,14 @@ class Oracle:
             raise RuntimeError(lib().q3o_error().decode())
         return pcm[:ns.value]
 
+
+    def tensor(self, name, n):
+        """(values as loaded [n] f32, on-disk GGML type)"""
+        out = np.zeros(n, np.float32)
+        st = C.c_int(0)
+        if not lib().q3o_tensor(self.h, name.encode(), out, int(n), C.byref(st)):
+            raise RuntimeError(lib().q3o_error().decode())
+        return out, st.value
 
     # ---- speaker encoder
     def speaker_dim(self):

@@ -108,7 +108,7 @@ def test_cli_single_shot_matches_engine(tmp_path, engine):
     ids = tok.encode_for_tts("Hello. This is a test.")
     codes = eng.generate([ids], speakers=[np.zeros(1024, np.float32)], max_len=FR, temperature=0.9, seed=5)[0]
     want = _pcm16(eng.vocoder(codes))
-    assert got.shape == want.shape and len(got) == codes.shape[0] * 1920
+    assert got.shape == want.shape and len(got) == eng.vocoder_num_samples(codes.shape[0])
     assert np.array_equal(got, want)
 
 

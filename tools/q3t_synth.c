@@ -13,6 +13,11 @@
 // usage: q3t_synth <config: full|tiny> <out_dir> [seed] [usage]
 //   writes <out_dir>/qwen3-tts-0.6b-f16.gguf and <out_dir>/qwen3-tts-tokenizer-f16.gguf
 //   (the fixed file names the reference loads, src/qwen3_tts.cpp:117-118).
+//   "q8_0" / "q4_0" / "q4_k" / "f32": weight dtype policy of the converters' --outtype (convert_tts_to_gguf.py:250-335,
+//   convert_tokenizer_to_gguf.py:265-296; the tokenizer converter knows f32 / f16 / q8_0 only, so q4_* leave that
+//   file F16).  Q8_0 / Q4_0 blocks use ggml's reference quantisers; Q4_K uses a plain min/max fit per 32-value
+//   sub-block (not ggml's iterative make_qkx2_quants: any valid block decodes the same way, which is what the
+//   loaders are tested on).
 //   "usage": the tokenizer file also carries tok_dec.vq_{first.0,rest.N}.usage [cb_size] F32 tensors, as an
 //   unconverted checkpoint would (the converter divides and drops them, convert_tokenizer_to_gguf.py:347-359);
 //   loaders must apply normalize_codebooks (src/audio_tokenizer_decoder.cpp:40-73).
@@ -25,6 +30,9 @@
 
 #define GGML_F32 0
 #define GGML_F16 1
+#define GGML_Q4_0 2
+#define GGML_Q8_0 8
+#define GGML_Q4_K 12
 enum { GV_U32 = 4, GV_F32 = 6, GV_STR = 8, GV_ARR = 9 };
 
 static uint64_t mix64(uint64_t z) {
@@ -352,6 +360,114 @@ static void build_vocab(const cfg_t *c) {
     }
 }
 
+// ---------------------------------------------------------------- weight dtype policy (--outtype)
+static const char *g_outtype = "f16";
+static uint16_t f32_to_f16_rne(float x);
+static int block_of(int type) { return type == GGML_Q4_K ? 256 : (type == GGML_Q8_0 || type == GGML_Q4_0) ? 32 : 1; }
+static uint64_t type_bytes(int type, uint64_t n) {
+    switch (type) {
+        case GGML_F32: return n * 4;
+        case GGML_F16: return n * 2;
+        case GGML_Q8_0: return n / 32 * 34;
+        case GGML_Q4_0: return n / 32 * 18;
+        case GGML_Q4_K: return n / 256 * 144;
+    }
+    return 0;
+}
+static uint32_t file_type(void) {   // llama_ftype of the --outtype
+    return strcmp(g_outtype, "f32") == 0 ? 0 : strcmp(g_outtype, "q4_0") == 0 ? 2 : strcmp(g_outtype, "q8_0") == 0 ? 7
+         : strcmp(g_outtype, "q4_k") == 0 ? 15 : 1;
+}
+static void apply_dtype_policy(int tts_file) {
+    const int want = strcmp(g_outtype, "q8_0") == 0 ? GGML_Q8_0 : strcmp(g_outtype, "q4_0") == 0 ? GGML_Q4_0
+                   : strcmp(g_outtype, "q4_k") == 0 ? GGML_Q4_K : strcmp(g_outtype, "f32") == 0 ? GGML_F32 : GGML_F16;
+    for (int i = 0; i < g_nt; ++i) {
+        tens_t *t = &g_t[i];
+        if (t->ndims <= 1) continue;   // 1-D: always F32
+        if (want == GGML_F32 || want == GGML_F16) { t->type = want; continue; }
+        int keep;
+        if (tts_file)   // _should_quantize (convert_tts_to_gguf.py:250-274)
+            keep = strstr(t->name, "_embd") || strstr(t->name, "codebook") || strstr(t->name, "_norm") ||
+                   strstr(t->name, ".bias") || strstr(t->name, "lm_head") || strstr(t->name, "codec_head");
+        else            // convert_tokenizer_to_gguf.py:283-294 (q8_0 only)
+            keep = want != GGML_Q8_0 || strstr(t->name, "codebook") || strstr(t->name, "_norm") ||
+                   strstr(t->name, "norm.") || strstr(t->name, "scale") || strstr(t->name, "alpha") ||
+                   strstr(t->name, "beta");
+        // gguf.quants.quantize needs whole blocks along the row: otherwise the converter falls back to F16
+        t->type = (keep || t->ne[0] % block_of(want)) ? GGML_F16 : want;
+    }
+}
+// ggml quantize_row_q8_0_ref: d = amax / 127, q = round(x / d)
+static void quant_q8_0(const float *x, uint8_t *o, int64_t n) {
+    for (int64_t b = 0; b < n / 32; ++b, o += 34) {
+        float amax = 0.0f;
+        for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(x[b * 32 + j]));
+        const float d = amax / 127.0f, id = d ? 1.0f / d : 0.0f;
+        const uint16_t dh = f32_to_f16_rne(d);
+        memcpy(o, &dh, 2);
+        for (int j = 0; j < 32; ++j) o[2 + j] = (uint8_t)(int8_t)roundf(x[b * 32 + j] * id);
+    }
+}
+// ggml quantize_row_q4_0_ref: d = (signed max-magnitude value) / -8, q = min(15, (int)(x / d + 8.5))
+static void quant_q4_0(const float *x, uint8_t *o, int64_t n) {
+    for (int64_t b = 0; b < n / 32; ++b, o += 18) {
+        float amax = 0.0f, mx = 0.0f;
+        for (int j = 0; j < 32; ++j) { const float v = x[b * 32 + j]; if (fabsf(v) > amax) { amax = fabsf(v); mx = v; } }
+        const float d = mx / -8.0f, id = d ? 1.0f / d : 0.0f;
+        const uint16_t dh = f32_to_f16_rne(d);
+        memcpy(o, &dh, 2);
+        for (int j = 0; j < 16; ++j) {
+            int q0 = (int)(x[b * 32 + j] * id + 8.5f), q1 = (int)(x[b * 32 + j + 16] * id + 8.5f);
+            q0 = q0 > 15 ? 15 : q0; q1 = q1 > 15 ? 15 : q1;
+            o[2 + j] = (uint8_t)(q0 | (q1 << 4));
+        }
+    }
+}
+// Q4_K super-block of 256: per 32-value sub-block scale = (max - min) / 15 and offset -min, both quantised to 6 bits
+// against the super-block's d / dmin, packed as ggml_get_scale_min_k4 unpacks them
+static void quant_q4_k(const float *x, uint8_t *o, int64_t n) {
+    for (int64_t b = 0; b < n / 256; ++b, o += 144) {
+        const float *v = x + b * 256;
+        float sc[8], mn[8], msc = 0.0f, mmn = 0.0f;
+        for (int s = 0; s < 8; ++s) {
+            float lo = v[s * 32], hi = v[s * 32];
+            for (int j = 1; j < 32; ++j) { lo = fminf(lo, v[s * 32 + j]); hi = fmaxf(hi, v[s * 32 + j]); }
+            if (lo > 0) lo = 0;
+            sc[s] = (hi - lo) / 15.0f;
+            mn[s] = -lo;
+            msc = fmaxf(msc, sc[s]);
+            mmn = fmaxf(mmn, mn[s]);
+        }
+        const float d = msc / 63.0f, dmin = mmn / 63.0f;
+        const uint16_t dh = f32_to_f16_rne(d), mh = f32_to_f16_rne(dmin);
+        memcpy(o, &dh, 2);
+        memcpy(o + 2, &mh, 2);
+        uint8_t ls[8], lm[8];
+        for (int s = 0; s < 8; ++s) {
+            int a = d ? (int)lroundf(sc[s] / d) : 0, c = dmin ? (int)lroundf(mn[s] / dmin) : 0;
+            ls[s] = (uint8_t)(a > 63 ? 63 : a);
+            lm[s] = (uint8_t)(c > 63 ? 63 : c);
+        }
+        uint8_t *S = o + 4;
+        for (int j = 0; j < 4; ++j) {
+            S[j] = (uint8_t)((ls[j] & 63) | ((ls[j + 4] >> 4) << 6));
+            S[j + 4] = (uint8_t)((lm[j] & 63) | ((lm[j + 4] >> 4) << 6));
+            S[j + 8] = (uint8_t)((ls[j + 4] & 15) | ((lm[j + 4] & 15) << 4));
+        }
+        uint8_t *Q = o + 16;
+        for (int s = 0; s < 8; s += 2)
+            for (int l = 0; l < 32; ++l) {
+                int q[2];
+                for (int u = 0; u < 2; ++u) {
+                    const float step = d * ls[s + u], off = dmin * lm[s + u];
+                    int t = step > 0 ? (int)lroundf((v[(s + u) * 32 + l] + off) / step) : 0;
+                    q[u] = t < 0 ? 0 : t > 15 ? 15 : t;
+                }
+                Q[(s / 2) * 32 + l] = (uint8_t)(q[0] | (q[1] << 4));
+            }
+    }
+}
+
 // ---------------------------------------------------------------- GGUF v3 writer
 static void w_u32(FILE *f, uint32_t v) { fwrite(&v, 4, 1, f); }
 static void w_u64(FILE *f, uint64_t v) { fwrite(&v, 8, 1, f); }
@@ -396,7 +512,7 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
         tens_t *t = &g_t[i];
         g_t[i].off = off;
         uint64_t n = (uint64_t)t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
-        off += n * (t->type == GGML_F16 ? 2 : 4);
+        off += type_bytes(t->type, n);
         off = (off + align - 1) / align * align;
     }
     fwrite("GGUF", 1, 4, f);
@@ -439,6 +555,21 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
         fseek(f, (long)(data_start + t->off), SEEK_SET);
         const uint64_t n = (uint64_t)t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3];
         const uint64_t base = mix64(seed ^ fnv1a64(t->name));
+        if (t->type != GGML_F16 && t->type != GGML_F32) {   // block-quantised, one row at a time
+            const int64_t row = t->ne[0];
+            float *x = malloc(sizeof(float) * (size_t)row);
+            uint8_t *q = malloc((size_t)type_bytes(t->type, (uint64_t)row));
+            for (uint64_t r = 0; r < n / (uint64_t)row; ++r) {
+                for (int64_t j = 0; j < row; ++j) x[j] = synth_value(base, r * (uint64_t)row + (uint64_t)j, t->center, t->e);
+                if (t->type == GGML_Q8_0) quant_q8_0(x, q, row);
+                else if (t->type == GGML_Q4_0) quant_q4_0(x, q, row);
+                else quant_q4_k(x, q, row);
+                fwrite(q, 1, (size_t)type_bytes(t->type, (uint64_t)row), f);
+            }
+            free(x);
+            free(q);
+            continue;
+        }
         for (uint64_t s0 = 0; s0 < n; s0 += CH) {
             const uint64_t m = (n - s0) < CH ? (n - s0) : CH;
             if (t->type == GGML_F16) {
@@ -470,14 +601,16 @@ int main(int argc, char **argv) {
     if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
     uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
     g_usage = argc > 4 && strcmp(argv[4], "usage") == 0;
+    if (argc > 4 && !g_usage) g_outtype = argv[4];
     char path[4096];
 
     build_talker(c);
+    apply_dtype_policy(1);
     build_vocab(c);
     kv_t kt[] = {
         {"general.architecture", GV_STR, 0, 0, "qwen3-tts", 0, 0},
         {"general.name", GV_STR, 0, 0, c->name, 0, 0},
-        {"general.file_type", GV_U32, 1, 0, 0, 0, 0},
+        {"general.file_type", GV_U32, file_type(), 0, 0, 0, 0},
         {"qwen3-tts.block_count", GV_U32, (uint32_t)c->n_layers, 0, 0, 0, 0},
         {"qwen3-tts.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
         {"qwen3-tts.feed_forward_length", GV_U32, (uint32_t)c->inter, 0, 0, 0, 0},
@@ -517,6 +650,7 @@ int main(int argc, char **argv) {
 
     g_nt = 0;
     build_tokenizer(c);
+    apply_dtype_policy(0);
     kv_t kk[] = {
         {"general.architecture", GV_STR, 0, 0, "qwen3-tts-tokenizer", 0, 0},
         {"general.name", GV_STR, 0, 0, c->name, 0, 0},
