@@ -19,7 +19,7 @@
 #include <string>
 #include <vector>
 
-#include "qwen3_tts_hip.h"
+#include "qwen3_tts_pipeline.h"
 
 namespace {
 

@@ -6,8 +6,9 @@
 //   qwen3_tts::TRTVocoderDecoder     src/trt_vocoder.h:18-42
 //   qwen3_tts::TextTokenizer         src/text_tokenizer.h:21-86
 //   qwen3_tts::AudioTokenizerEncoder src/audio_tokenizer_encoder.h:95-125
-//   qwen3_tts::Qwen3TTS, tts_params, tts_result, load_audio_file, save_audio_file   src/qwen3_tts.h:17-156
-// so a caller switches by including this header instead of those and linking libqwen3_tts_hip.so + libq3t.so.  Every
+// so a caller switches by including this header instead of those and linking libqwen3_tts_hip.so + libq3t.so
+// (tests/boundary: the reference's own src/qwen3_tts.cpp + src/main.cpp compile and link against it unchanged).
+// The pipeline above them (Qwen3TTS, src/qwen3_tts.h) is qwen3_tts_pipeline.h / libqwen3_tts_pipeline.so.  Every
 // method forwards to q3t_* calls; all weights, KV caches and scratch stay resident in HBM inside a q3t_ctx.  No
 // exceptions cross this surface.
 //
@@ -18,8 +19,9 @@
 //    keeps decoding while the host reads a chunk); returning false stops generation after the frames delivered.
 //  - The KV cache is sized once for prefill + max_len + 8 positions (grown on demand by re-laying out the context
 //    from the resident weights, never from the file), not re-allocated per generate() call.
-//  - TRTVocoderDecoder::load_engine takes the tokenizer GGUF (there is no TensorRT engine on MI355X); fixed_frames
-//    keeps its meaning: the independent chunk length of decode().
+//  - TRTVocoderDecoder::load_engine takes the tokenizer GGUF (there is no TensorRT engine on MI355X); given a path
+//    that is not a GGUF (the reference's <model_dir>/vocoder_decoder_<n>.trt) it loads qwen3-tts-tokenizer-f16.gguf
+//    from the same directory.  fixed_frames keeps its meaning: the independent chunk length of decode().
 //  - TextTokenizer::load_from_gguf takes the GGUF path (the reference takes a ggml gguf_context *: this library has no
 //    ggml); encode / encode_for_tts / decode are token-for-token the reference's (tests/test_tokenizer.py).
 //  - Qwen3TTS keeps talker, code predictor, vocoder and speaker encoder in ONE device context (one weight upload, one
@@ -39,6 +41,7 @@
 #include <vector>
 
 struct q3t_ctx;
+struct q3t_tokenizer;
 
 namespace qwen3_tts {
 
@@ -226,7 +229,7 @@ public:
     int32_t pad_token_id() const { return config_.pad_token_id; }
 
 private:
-    struct q3t_tokenizer *tok_ = nullptr;
+    ::q3t_tokenizer *tok_ = nullptr;
     tokenizer_config config_;
     std::string error_msg_;
 };
@@ -267,93 +270,6 @@ private:
     speaker_encoder_config config_;
     std::string error_msg_;
 };
-
-// ====================================================================================== pipeline (src/qwen3_tts.h)
-struct tts_params {
-    int32_t max_audio_tokens = 4096;
-    float temperature = 0.9f;
-    float top_p = 1.0f;       // accepted, unused (as in the reference: no top-p stage exists in its sampler)
-    int32_t top_k = 50;
-    int32_t n_threads = 4;    // accepted, unused (host threads do no numeric work here)
-    bool print_progress = false;
-    bool print_timing = true;
-    float repetition_penalty = 1.05f;
-};
-
-struct tts_result {
-    std::vector<float> audio;
-    int32_t sample_rate = 24000;
-    bool success = false;
-    std::string error_msg;
-    int64_t t_load_ms = 0;
-    int64_t t_tokenize_ms = 0;
-    int64_t t_encode_ms = 0;
-    int64_t t_generate_ms = 0;
-    int64_t t_decode_ms = 0;
-    int64_t t_total_ms = 0;
-    uint64_t mem_rss_start_bytes = 0;
-    uint64_t mem_rss_end_bytes = 0;
-    uint64_t mem_rss_peak_bytes = 0;
-    uint64_t mem_phys_start_bytes = 0;
-    uint64_t mem_phys_end_bytes = 0;
-    uint64_t mem_phys_peak_bytes = 0;
-};
-
-class Qwen3TTS {
-public:
-    Qwen3TTS();
-    ~Qwen3TTS();
-    Qwen3TTS(const Qwen3TTS &) = delete;
-    Qwen3TTS &operator=(const Qwen3TTS &) = delete;
-
-    // model_dir holds qwen3-tts-0.6b-f16.gguf and qwen3-tts-tokenizer-f16.gguf (qwen3_tts.cpp:117-118)
-    bool load_models(const std::string &model_dir);
-    tts_result synthesize(const std::string &text, const tts_params &params = tts_params());
-    tts_result synthesize_with_voice(const std::string &text, const std::string &reference_audio,
-                                     const tts_params &params = tts_params());
-    tts_result synthesize_with_voice(const std::string &text, const float *ref_samples, int32_t n_ref_samples,
-                                     const tts_params &params = tts_params());
-    bool encode_speaker(const std::string &reference_audio, std::vector<float> &embedding);
-    tts_result synthesize_with_embedding(const std::string &text, const std::vector<float> &speaker_embedding,
-                                         const tts_params &params = tts_params());
-    const std::string &get_error() const { return error_msg_; }
-    bool is_loaded() const { return models_loaded_; }
-
-    // ---- MI355X extensions
-    bool set_device(int device);           // before load_models
-    void set_seed(uint64_t seed) { seed_ = seed; }
-    // 0: whole-utterance vocoder after generation; n > 0: n-frame chunks streamed from the frame callback
-    void set_vocoder_chunk(int32_t frames) { vocoder_chunk_ = frames; }
-    int32_t vocoder_chunk() const { return vocoder_chunk_; }
-    // n utterances decoded together on one GPU (lock-step slots); speaker_embeddings empty or one per text (an empty
-    // vector = no speaker row); results[i] as synthesize_with_embedding's
-    std::vector<tts_result> synthesize_batch(const std::vector<std::string> &texts,
-                                             const std::vector<std::vector<float>> &speaker_embeddings,
-                                             const tts_params &params = tts_params());
-
-private:
-    tts_result synthesize_internal(const std::string &text, const float *speaker_embedding, const tts_params &params,
-                                   tts_result &result);
-    bool ensure_slots(int32_t slots, int32_t max_len);
-
-    TextTokenizer tokenizer_;
-    q3t_ctx *ctx_ = nullptr;
-    int device_ = 0;
-    uint64_t seed_ = 0;
-    int32_t slots_ = 0, n_ctx_ = 0, hidden_ = 1024;
-    int32_t vocoder_chunk_ = 0;
-    bool models_loaded_ = false;
-    std::string error_msg_;
-    std::string tts_model_path_;
-    std::string decoder_model_path_;
-};
-
-// WAV: RIFF PCM16 / PCM32 / IEEE float32, channels averaged to mono (qwen3_tts.cpp:567-706)
-bool load_audio_file(const std::string &path, std::vector<float> &samples, int &sample_rate);
-// WAV PCM16 mono, samples clamped to [-1, 1] and scaled by 32767 (qwen3_tts.cpp:708-759)
-bool save_audio_file(const std::string &path, const std::vector<float> &samples, int sample_rate);
-// linear resampling used for reference audio (qwen3_tts.cpp:83-101)
-void resample_linear(const float *input, int input_len, int input_rate, std::vector<float> &output, int output_rate);
 
 }  // namespace qwen3_tts
 

@@ -13,7 +13,7 @@
 #include <cstring>
 
 #include "q3t_backend.h"
-#include "qwen3_tts_hip.h"
+#include "qwen3_tts_pipeline.h"
 
 namespace qwen3_tts {
 
@@ -127,87 +127,6 @@ int stream_cb(void *user, int32_t /*utt*/, const int32_t *codes, int32_t n_frame
 }
 
 }  // namespace
-
-// ================================================================================================ TextTokenizer
-
-TextTokenizer::TextTokenizer() = default;
-TextTokenizer::~TextTokenizer() {
-    if (tok_) q3t_tokenizer_free(tok_);
-}
-
-bool TextTokenizer::load_from_gguf(const std::string &gguf_path) {
-    if (tok_) { q3t_tokenizer_free(tok_); tok_ = nullptr; }
-    if (q3t_tokenizer_load(gguf_path.c_str(), &tok_) != Q3T_OK) {
-        tok_ = nullptr;
-        error_msg_ = q3t_error();
-        return false;
-    }
-    q3t_tokenizer_info(tok_, &config_.vocab_size, &config_.bos_token_id, &config_.eos_token_id, &config_.pad_token_id);
-    return true;
-}
-
-std::vector<int32_t> TextTokenizer::encode(const std::string &text) const {
-    std::vector<int32_t> ids;
-    int32_t n = 0;
-    if (!tok_ || q3t_tokenizer_encode(tok_, text.data(), (int64_t)text.size(), 0, nullptr, 0, &n) != Q3T_OK) return ids;
-    ids.resize(n);
-    if (n > 0 && q3t_tokenizer_encode(tok_, text.data(), (int64_t)text.size(), 0, ids.data(), n, &n) != Q3T_OK) ids.clear();
-    return ids;
-}
-
-std::vector<int32_t> TextTokenizer::encode_for_tts(const std::string &text) const {
-    std::vector<int32_t> ids;
-    int32_t n = 0;
-    if (!tok_ || q3t_tokenizer_encode(tok_, text.data(), (int64_t)text.size(), 1, nullptr, 0, &n) != Q3T_OK) return ids;
-    ids.resize(n);
-    if (q3t_tokenizer_encode(tok_, text.data(), (int64_t)text.size(), 1, ids.data(), n, &n) != Q3T_OK) ids.clear();
-    return ids;
-}
-
-std::string TextTokenizer::decode(const std::vector<int32_t> &tokens) const {
-    if (!tok_) return "";
-    int64_t nb = 0;
-    if (q3t_tokenizer_decode(tok_, tokens.data(), (int32_t)tokens.size(), nullptr, 0, &nb) != Q3T_OK) return "";
-    std::string s((size_t)nb, '\0');
-    if (nb > 0 && q3t_tokenizer_decode(tok_, tokens.data(), (int32_t)tokens.size(), &s[0], nb, &nb) != Q3T_OK) return "";
-    return s;
-}
-
-std::string TextTokenizer::decode_token(int32_t token_id) const { return decode(std::vector<int32_t>{token_id}); }
-
-// ======================================================================================= AudioTokenizerEncoder
-
-AudioTokenizerEncoder::AudioTokenizerEncoder() = default;
-AudioTokenizerEncoder::~AudioTokenizerEncoder() {
-    if (ctx_) q3t_ctx_destroy(ctx_);
-}
-
-bool AudioTokenizerEncoder::set_device(int device) {
-    if (ctx_) { error_msg_ = "set_device must precede load_model"; return false; }
-    device_ = device;
-    return true;
-}
-
-bool AudioTokenizerEncoder::load_model(const std::string &model_path) {
-    if (ctx_) { q3t_ctx_destroy(ctx_); ctx_ = nullptr; }
-    if (q3t_ctx_create_speaker(model_path.c_str(), device_, &ctx_) != Q3T_OK) {
-        ctx_ = nullptr;
-        error_msg_ = q3t_error();
-        return false;
-    }
-    config_.embedding_dim = q3t_speaker_dim(ctx_);
-    return true;
-}
-
-bool AudioTokenizerEncoder::encode(const float *samples, int32_t n_samples, std::vector<float> &embedding) {
-    if (!ctx_) { error_msg_ = "Model not loaded"; return false; }
-    embedding.resize(config_.embedding_dim);
-    if (q3t_speaker_encode(ctx_, samples, n_samples, embedding.data()) != Q3T_OK) {
-        error_msg_ = q3t_error();
-        return false;
-    }
-    return true;
-}
 
 // ===================================================================================================== Qwen3TTS
 

@@ -11,7 +11,7 @@
 #include <string>
 #include <vector>
 
-#include "qwen3_tts_hip.h"
+#include "qwen3_tts_pipeline.h"
 
 using namespace qwen3_tts;
 
