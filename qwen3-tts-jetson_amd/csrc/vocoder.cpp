@@ -359,6 +359,15 @@ bool Vocoder::conv16(const Conv &c, const uint16_t *xh, int T, int pad, int dil,
 
 bool Vocoder::convT16(const Conv &c, const uint16_t *xh, int T, int st, int trim, float *y, int T_out, uint16_t *y16,
                       const Snake *next, hipStream_t s) {
+    if (c.ic % 32 == 0 && (c.oc % 96 == 0 || c.oc % 64 == 0) && c.k <= st * CONV_MAX_TAPS) {
+        // every output phase in one launch (grid z)
+        ConvParams p;
+        p.xh = xh; p.T_in = T; p.C_in = c.ic;
+        p.ct_w = c.w; p.ct_k = c.k; p.ct_st = st; p.ct_trim = trim; p.T_out = T_out;
+        p.y = y; p.C_out = c.oc; p.bias = c.b; p.y16 = y16;
+        if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
+        return conv(p, s);
+    }
     for (int phi = 0; phi < st; ++phi) {
         ConvParams p;
         p.xh = xh; p.T_in = T; p.C_in = c.ic;
@@ -406,11 +415,23 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     float *qkv = B;                                        // [F][3*LAT]
     uint16_t *att = reinterpret_cast<uint16_t *>(C);       // [F][LAT] f16
     uint16_t *hm = reinterpret_cast<uint16_t *>(C) + (size_t)F * LAT;   // [F][ffn] f16
+    // large-M projections (M = frames or upsampled steps) run as 1-tap convs on the implicit-GEMM conv kernel over
+    // pre-normalised f16 rows (norm_f16 reproduces the GEMM prologue's norm); the decode-shaped GEMM path stays for
+    // the shapes the conv tiles do not cover
+    const bool qkv_conv = VH % 32 == 0 && VH <= 1024 && VH % 4 == 0 && (3 * LAT) % 96 == 0;
     for (const Layer &L : layers_) {
-        GemvParams q;
-        q.W = L.qkv; q.N = 3 * LAT; q.K = VH; q.B = F; q.pro = PRO_RMS; q.x = x; q.ldx = VH; q.nw = L.attn_norm;
-        q.eps = 1e-5f; q.out_f32 = qkv; q.ldo = 3 * LAT;
-        if (!gemv(q, s)) return false;
+        if (qkv_conv) {
+            if (!norm_f16(x, L.attn_norm, nullptr, 1e-5f, 0, xh_, F, VH, s)) return false;
+            ConvParams q;
+            q.xh = xh_; q.T_in = F; q.C_in = VH; q.n_taps = 1; q.taps[0] = ConvTap{L.qkv, 0};
+            q.y = qkv; q.C_out = 3 * LAT; q.M = F;
+            if (!conv(q, s)) return false;
+        } else {
+            GemvParams q;
+            q.W = L.qkv; q.N = 3 * LAT; q.K = VH; q.B = F; q.pro = PRO_RMS; q.x = x; q.ldx = VH; q.nw = L.attn_norm;
+            q.eps = 1e-5f; q.out_f32 = qkv; q.ldo = 3 * LAT;
+            if (!gemv(q, s)) return false;
+        }
         if (!attn_prefill(qkv, rope_, att, F, n_heads_, head_dim_, s)) return false;
         GemvParams o;
         o.W = L.o; o.N = VH; o.K = LAT; o.B = F; o.pro = PRO_F16; o.x = att; o.ldx = LAT;
@@ -445,15 +466,29 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
         if ((size_t)T1 * U.pw_dim / 2 > (size_t)T1 * LAT + (size_t)T * LAT) {
             // cur buffer is sized for the largest activation; pw fits by construction (ensure())
         }
-        GemvParams p1;
-        p1.W = U.pw1; p1.N = U.pw_dim; p1.K = LAT; p1.B = (int)T1; p1.pro = PRO_LN; p1.x = dwo; p1.ldx = LAT;
-        p1.nw = U.norm_w; p1.nb = U.norm_b; p1.eps = 1e-6f; p1.bias = U.pw1_b; p1.act = ACT_GELU;
-        p1.out_f16 = pw; p1.ldo = U.pw_dim;
-        if (!gemv(p1, s)) return false;
-        GemvParams p2;
-        p2.W = U.pw2; p2.N = LAT; p2.K = U.pw_dim; p2.B = (int)T1; p2.pro = PRO_F16; p2.x = pw; p2.ldx = U.pw_dim;
-        p2.bias = U.pw2_b; p2.scale = U.gamma; p2.resid = h; p2.ldr = LAT; p2.out_f32 = h; p2.ldo = LAT;
-        if (!gemv(p2, s)) return false;
+        const bool pw_conv = LAT % 32 == 0 && LAT <= 1024 && U.pw_dim % 64 == 0 && U.pw_dim % 32 == 0 && LAT % 64 == 0;
+        if (pw_conv) {
+            // LayerNorm -> f16 rows, pw1 + bias + GELU -> f16, pw2 + bias, x gamma, + residual (in place)
+            if (!norm_f16(dwo, U.norm_w, U.norm_b, 1e-6f, 1, xh_, (int)T1, LAT, s)) return false;
+            ConvParams c1;
+            c1.xh = xh_; c1.T_in = (int)T1; c1.C_in = LAT; c1.n_taps = 1; c1.taps[0] = ConvTap{U.pw1, 0};
+            c1.C_out = U.pw_dim; c1.M = (int)T1; c1.bias = U.pw1_b; c1.act = 4; c1.y16 = pw;
+            if (!conv(c1, s)) return false;
+            ConvParams c2;
+            c2.xh = pw; c2.T_in = (int)T1; c2.C_in = U.pw_dim; c2.n_taps = 1; c2.taps[0] = ConvTap{U.pw2, 0};
+            c2.C_out = LAT; c2.M = (int)T1; c2.bias = U.pw2_b; c2.scale = U.gamma; c2.resid = h; c2.y = h;
+            if (!conv(c2, s)) return false;
+        } else {
+            GemvParams p1;
+            p1.W = U.pw1; p1.N = U.pw_dim; p1.K = LAT; p1.B = (int)T1; p1.pro = PRO_LN; p1.x = dwo; p1.ldx = LAT;
+            p1.nw = U.norm_w; p1.nb = U.norm_b; p1.eps = 1e-6f; p1.bias = U.pw1_b; p1.act = ACT_GELU;
+            p1.out_f16 = pw; p1.ldo = U.pw_dim;
+            if (!gemv(p1, s)) return false;
+            GemvParams p2;
+            p2.W = U.pw2; p2.N = LAT; p2.K = U.pw_dim; p2.B = (int)T1; p2.pro = PRO_F16; p2.x = pw; p2.ldx = U.pw_dim;
+            p2.bias = U.pw2_b; p2.scale = U.gamma; p2.resid = h; p2.ldr = LAT; p2.out_f32 = h; p2.ldo = LAT;
+            if (!gemv(p2, s)) return false;
+        }
         float *nxt = h;
         f0 = cur; cur = nxt; T = T1;
     }
@@ -484,6 +519,11 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
         }
     }
     // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790): ha holds f16(snake(dec5)) of the stream
+    if (dec6_.oc == 1 && dec6_.ic % 8 == 0 && dec6_.ic <= 112 && dec6_.k <= 8) {
+        if (!conv_out1(ha, dec6_.w, dec6_.b, pcm_dev, (int)T, dec6_.ic, dec6_.k, s)) return false;
+        *n_out = T;
+        return true;
+    }
     ConvParams p6;
     p6.xh = ha; p6.T_in = (int)T; p6.C_in = dec6_.ic;
     p6.n_taps = dec6_.k;

@@ -20,18 +20,31 @@ struct ConvParams {
     int C_out = 0, M = 0, so = 1, ob = 0;
     int ldy = 0;                    // row stride of y and resid (0: C_out)
     const float *bias = nullptr, *resid = nullptr;
-    int act = 0;   // 1 = tanh, 2 = ReLU, 3 = tanh(ReLU)
+    const float *scale = nullptr;   // per output channel, applied after the bias and before the residual
+    int act = 0;   // 1 = tanh, 2 = ReLU, 3 = tanh(ReLU), 4 = GELU (ggml tanh form, f16 table); after the residual
     // optional f16 output of the same elements: y16[t][co] = f16(snake(v)) with exp(alpha) / exp(-beta) per output
     // channel (y16_a null: plain rounding) -- the NEXT conv's input, so no separate snake/round pass reads y back
     uint16_t *y16 = nullptr;
     const float *y16_a = nullptr, *y16_ib = nullptr;
+    // transposed conv in one launch (multi-tile kernel): grid z = output phase phi of a stride-ct_st transposed conv
+    // with ct_k taps [ct_k][C_out][C_in] at ct_w, trimmed by ct_trim; phase phi writes rows ct_st*m + phi < T_out
+    // from taps k = (phi + trim) % st + j*st at input offset (phi + trim - k) / st.  taps/dmin/dmax/M/so/ob unused
+    const uint16_t *ct_w = nullptr;
+    int ct_k = 0, ct_st = 0, ct_trim = 0, T_out = 0;
 };
 bool conv(const ConvParams &p, hipStream_t s);
 // out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
 // the conv input computed ONCE per element instead of once per (output tile, tap window) inside k_conv
 bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, int64_t T, int C, hipStream_t s);
+// out[t][:] = f16(norm(x[t][:])): mode 0 RMSNorm (x * scale) * w, mode 1 LayerNorm ((x - mean) * scale) * w + b;
+// double sums as gemm_mfma's PRO_RMS / PRO_LN prologues (the input of a 1-tap conv used as a large-M GEMM)
+bool norm_f16(const float *x, const float *w, const float *b, float eps, int mode, uint16_t *out, int T, int C,
+              hipStream_t s);
+// y[t] = tanh(bias + sum_j sum_ci w[j][ci] * xh[t + j - (K - 1)][ci]): the decoder's last conv (C_out = 1, K <= 8)
+bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s);
 bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s);
-bool attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s);
+// RoPE is applied to qkv's q and k columns in place
+bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s);
 bool codes_cols(const int32_t *codes, int *cols, int F, int ncb, hipStream_t s);
 
 }  // namespace q3t

@@ -19,6 +19,7 @@ __device__ __forceinline__ float conv_act(float v, int act) {
     if (act == 1) return tanhf(v);
     if (act == 2) return fmaxf(v, 0.0f);
     if (act == 3) return tanhf(fmaxf(v, 0.0f));
+    if (act == 4) return gelu_ggml(v);
     return v;
 }
 constexpr int CT_MAXWIN = CT_M + 64;
@@ -122,6 +123,7 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
         const size_t t = (size_t)m * p.so + p.ob;
         const int ldy = p.ldy ? p.ldy : p.C_out;
         float v = acc[reg] + b;
+        if (p.scale) v *= p.scale[co];
         if (p.resid) v = p.resid[t * ldy + co] + v;
         v = conv_act(v, p.act);
         if (p.y) p.y[t * ldy + co] = v;
@@ -145,23 +147,41 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
 // Input: f16 rows (snake already applied).  Epilogue: bias, residual, tanh, f32 and/or f16(snake_next) outputs.
 constexpr int MT_KC = 32, MT_LDK = MT_KC + 8;   // LDS row: 32 f16 + 16 B pad (conflict-free ds_read_b128)
 
-template <int RB, int NT>
-__global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
+template <int RB, int NT, int MINB = 2>
+__global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     constexpr int MT = 128 * RB, CB = NT / 32;
     extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
     // the tap table in LDS: indexing the by-value kernel argument with a runtime tap index makes the compiler copy
     // the whole ConvParams to scratch memory
     __shared__ const uint16_t *tapw[CONV_MAX_TAPS];
     __shared__ int tapdj[CONV_MAX_TAPS];
-    const int win = MT + p.dmax - p.dmin;
+    // launch geometry of this workgroup's conv: the params' own, or output phase blockIdx.z of a transposed conv
+    int n_taps = p.n_taps, dmin = p.dmin, dmax = p.dmax, M = p.M, so = p.so, ob = p.ob;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (p.ct_st) {
+        const int phi = blockIdx.z, st = p.ct_st, k0 = (phi + p.ct_trim) % st;
+        n_taps = 0;
+        for (int k = k0; k < p.ct_k && n_taps < CONV_MAX_TAPS; k += st) {
+            const int dj = (phi + p.ct_trim - k) / st;
+            if (tid == n_taps) { tapw[n_taps] = p.ct_w + (size_t)k * p.C_out * p.C_in; tapdj[n_taps] = dj; }
+            dmin = n_taps == 0 ? dj : min(dmin, dj);
+            dmax = n_taps == 0 ? dj : max(dmax, dj);
+            ++n_taps;
+        }
+        M = (p.T_out - phi + st - 1) / st;
+        so = st;
+        ob = phi;
+    } else {
+#pragma unroll
+        for (int j = 0; j < CONV_MAX_TAPS; ++j)
+            if (tid == j) { tapw[j] = p.taps[j].w; tapdj[j] = p.taps[j].dj; }
+    }
+    const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
+    if (m0 >= M || n_taps == 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
+    __syncthreads();
+    const int win = MT + dmax - dmin;
     uint16_t *xs = sm;                          // [win][MT_LDK]
     uint16_t *ws = sm + (size_t)win * MT_LDK;   // [taps][NT][MT_LDK]
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int j = 0; j < CONV_MAX_TAPS; ++j)
-        if (tid == j) { tapw[j] = p.taps[j].w; tapdj[j] = p.taps[j].dj; }
-    __syncthreads();
-    const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
     const int r = lane & 31, h = lane >> 5;
     f32x16_t acc[RB][CB];
 #pragma unroll
@@ -174,12 +194,12 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
     // the chunk's weights (L2-resident: every workgroup reads the same ones) are loaded all at once and stored
     constexpr int XR = (MT + 64) * (MT_KC / 8) / 256;              // window rows <= MT + 64
     constexpr int WR = (CONV_MAX_TAPS * NT * (MT_KC / 8) + 255) / 256;
-    const int nx = win * (MT_KC / 8), nw = p.n_taps * NT * (MT_KC / 8);
+    const int nx = win * (MT_KC / 8), nw = n_taps * NT * (MT_KC / 8);
     uint4 xr[XR];
 #define Q3T_CONV_XLOAD(C0)                                                                                            \
     do {                                                                                                              \
         _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                              \
-            const int e = tid + q * 256, row = e >> 2, c8 = (e & 3) * 8, i = m0 + p.dmin + row;                       \
+            const int e = tid + q * 256, row = e >> 2, c8 = (e & 3) * 8, i = m0 + dmin + row;                       \
             const bool in = e < nx && i >= 0 && i < p.T_in;                                                           \
             const int ic = min(max(i, 0), p.T_in - 1);                                                                \
             const uint4 u = ldg16(p.xh + (size_t)ic * p.C_in + (C0) + c8);                                           \
@@ -204,8 +224,8 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
         }
         __syncthreads();
         if (c0 + MT_KC < p.C_in) Q3T_CONV_XLOAD(c0 + MT_KC);
-        for (int j = 0; j < p.n_taps; ++j) {
-            const uint16_t *ab = xs + (wave * 32 * RB + r + (tapdj[j] - p.dmin)) * MT_LDK + 8 * h;
+        for (int j = 0; j < n_taps; ++j) {
+            const uint16_t *ab = xs + (wave * 32 * RB + r + (tapdj[j] - dmin)) * MT_LDK + 8 * h;
             const uint16_t *bb = ws + (j * NT + r) * MT_LDK + 8 * h;
 #pragma unroll
             for (int kk = 0; kk < MT_KC; kk += 16) {
@@ -241,14 +261,18 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
         for (int k = 0; k < 32 * Q / 64; ++k) {
             const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
             const int m = m0 + wave * 32 * RB + i * 32 + row;
-            if (m >= p.M) continue;
-            const size_t t = (size_t)m * p.so + p.ob, o = t * (p.ldy ? p.ldy : p.C_out) + co0 + q4;
+            if (m >= M) continue;
+            const size_t t = (size_t)m * so + ob, o = t * (p.ldy ? p.ldy : p.C_out) + co0 + q4;
             const size_t o16 = t * p.C_out + co0 + q4;
             const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
             float v[4] = {a.x, a.y, a.z, a.w};
             if (p.bias) {
                 const float4 b = *reinterpret_cast<const float4 *>(p.bias + co0 + q4);
                 v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+            }
+            if (p.scale) {
+                const float4 g = *reinterpret_cast<const float4 *>(p.scale + co0 + q4);
+                v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
             }
             if (p.resid) {
                 const float4 rr = *reinterpret_cast<const float4 *>(p.resid + o);
@@ -281,25 +305,42 @@ __global__ void __launch_bounds__(256, 2) k_conv_mt(const ConvParams p) {
     }
 }
 
-template <int RB, int NT>
+template <int RB, int NT, int MINB = 2>
 static bool launch_mt(const ConvParams &p, hipStream_t s) {
     constexpr int MT = 128 * RB;
     // staging area (input window + the chunk's weights of every tap), reused by the epilogue's transposed slices
+    // (transposed launches: p.n_taps / dmin / dmax carry the largest tap count and span over the phases)
     const size_t lds = std::max(((size_t)(MT + p.dmax - p.dmin) + (size_t)p.n_taps * NT) * MT_LDK * 2,
                                 (size_t)4 * 32 * (NT + 4) * 4);
     static bool attr = false;
     if (!attr) {
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_mt<RB, NT>),
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_mt<RB, NT, MINB>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
         attr = true;
     }
-    const dim3 grid((p.M + MT - 1) / MT, p.C_out / NT);
-    hipLaunchKernelGGL((k_conv_mt<RB, NT>), grid, dim3(256), lds, s, p);
+    const dim3 grid((p.M + MT - 1) / MT, p.C_out / NT, p.ct_st ? p.ct_st : 1);
+    hipLaunchKernelGGL((k_conv_mt<RB, NT, MINB>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
 }
 
 bool conv(const ConvParams &p, hipStream_t s) {
+    if (p.ct_st) {   // one launch over every output phase (multi-tile kernel only)
+        const int NT = p.C_out % 96 == 0 ? 96 : p.C_out % 64 == 0 ? 64 : 0;
+        if (!p.xh || !NT || p.C_in % MT_KC != 0 || p.ct_k > p.ct_st * CONV_MAX_TAPS) {
+            set_error("conv: unsupported transposed launch");
+            return false;
+        }
+        ConvParams q = p;
+        q.M = (p.T_out + p.ct_st - 1) / p.ct_st;   // phase 0 has the most rows
+        q.n_taps = (p.ct_k + p.ct_st - 1) / p.ct_st;
+        q.dmin = 0;
+        q.dmax = q.n_taps - 1;                      // taps of one phase are consecutive input rows
+        if (q.M <= 0) return true;
+        const long tiles256 = (long)((q.M + 255) / 256) * (p.C_out / NT) * p.ct_st;
+        if (NT == 96) return tiles256 >= 512 ? launch_mt<2, 96>(q, s) : launch_mt<1, 96>(q, s);
+        return tiles256 >= 512 ? launch_mt<2, 64>(q, s) : launch_mt<1, 64>(q, s);
+    }
     if (p.M <= 0) return true;
     if (p.n_taps < 1 || p.n_taps > CONV_MAX_TAPS || p.dmax - p.dmin > CT_MAXWIN - CT_M) {
         set_error("conv: unsupported tap layout");
@@ -307,9 +348,12 @@ bool conv(const ConvParams &p, hipStream_t s) {
     }
     const int NT = p.C_out % 96 == 0 ? 96 : p.C_out % 64 == 0 ? 64 : 0;
     if (p.xh && NT && p.C_in % MT_KC == 0 && (p.y || p.y16)) {
-        // RB 2 (256-row tiles) unless that leaves fewer than two workgroups per CU to fill the chip
+        // RB 2 (256-row tiles) unless that leaves fewer than two workgroups per CU to fill the chip.  1-tap convs over
+        // narrow channel counts are bound by their epilogue traffic (f32 residual in, f32 + f16 out): 128-row tiles
+        // at three workgroups per CU keep more of it in flight
         const long tiles256 = (long)((p.M + 255) / 256) * (p.C_out / NT);
         const bool big = tiles256 >= 512;
+        if (big && p.n_taps == 1 && p.C_in <= 192) return NT == 96 ? launch_mt<1, 96, 3>(p, s) : launch_mt<1, 64, 3>(p, s);
         if (NT == 96) return big ? launch_mt<2, 96>(p, s) : launch_mt<1, 96>(p, s);
         return big ? launch_mt<2, 64>(p, s) : launch_mt<1, 64>(p, s);
     }
@@ -348,6 +392,95 @@ bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, i
     return true;
 }
 
+// ======================================================================================= row norm -> f16
+__global__ void __launch_bounds__(256) k_norm_f16(const float *x, const float *w, const float *b, float eps, int mode,
+                                                  uint16_t *out, int C) {
+    __shared__ double scr[4];
+    const int t = blockIdx.x, tid = threadIdx.x, k = 4 * tid;
+    const bool ok = k < C;
+    const float *row = x + (size_t)t * C;
+    const float4 v = ok ? *reinterpret_cast<const float4 *>(row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto block_sum = [&](double d) {
+        d = wave_sum_d(d);
+        __syncthreads();
+        if ((tid & 63) == 0) scr[tid >> 6] = d;
+        __syncthreads();
+        return (scr[0] + scr[1]) + (scr[2] + scr[3]);
+    };
+    float y[4] = {v.x, v.y, v.z, v.w};
+    if (mode == 0) {
+        const double ss = block_sum((double)(v.x * v.x) + (double)(v.y * v.y) + (double)(v.z * v.z) + (double)(v.w * v.w));
+        const float scale = 1.0f / sqrtf((float)(ss / C) + eps);
+        if (!ok) return;
+        const float4 g = *reinterpret_cast<const float4 *>(w + k);
+        y[0] = (y[0] * scale) * g.x; y[1] = (y[1] * scale) * g.y; y[2] = (y[2] * scale) * g.z; y[3] = (y[3] * scale) * g.w;
+    } else {
+        const double s1 = block_sum((double)v.x + (double)v.y + (double)v.z + (double)v.w);
+        const float mean = (float)(s1 / C);
+        const float dx = v.x - mean, dy = v.y - mean, dz = v.z - mean, dw = v.w - mean;
+        const double s2 = block_sum(ok ? (double)(dx * dx) + (double)(dy * dy) + (double)(dz * dz) + (double)(dw * dw) : 0.0);
+        const float scale = 1.0f / sqrtf((float)(s2 / C) + eps);
+        if (!ok) return;
+        const float4 g = *reinterpret_cast<const float4 *>(w + k), c = *reinterpret_cast<const float4 *>(b + k);
+        y[0] = (dx * scale) * g.x + c.x; y[1] = (dy * scale) * g.y + c.y;
+        y[2] = (dz * scale) * g.z + c.z; y[3] = (dw * scale) * g.w + c.w;
+    }
+    uint2 hv;
+    hv.x = (uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16);
+    hv.y = (uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16);
+    *reinterpret_cast<uint2 *>(out + (size_t)t * C + k) = hv;
+}
+bool norm_f16(const float *x, const float *w, const float *b, float eps, int mode, uint16_t *out, int T, int C,
+              hipStream_t s) {
+    if (C % 4 != 0 || C > 1024 || (mode == 1 && !b)) { set_error("norm_f16: unsupported shape"); return false; }
+    if (T <= 0) return true;
+    hipLaunchKernelGGL(k_norm_f16, dim3(T), dim3(256), 0, s, x, w, b, eps, mode, out, C);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+// ======================================================================================= single-channel output conv
+// one workgroup per 256 outputs: the input rows [t0 - (K-1), t0 + 256) staged once in LDS, one output per thread
+constexpr int CO1_T = 256, CO1_MAXC = 112, CO1_MAXK = 8;
+__global__ void __launch_bounds__(256) k_conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y,
+                                                   int T, int C, int K) {
+    __shared__ __attribute__((aligned(16))) uint16_t xs[(CO1_T + CO1_MAXK) * CO1_MAXC];
+    __shared__ float ws[CO1_MAXK * CO1_MAXC];
+    const int t0 = blockIdx.x * CO1_T, tid = threadIdx.x;
+    const int rows = CO1_T + K - 1, c8n = C / 8;
+    for (int e = tid; e < rows * c8n; e += 256) {
+        const int r = e / c8n, c8 = (e % c8n) * 8, i = t0 - (K - 1) + r;
+        const uint4 u = (i >= 0 && i < T) ? ldg16(xh + (size_t)i * C + c8) : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4 *>(xs + r * C + c8) = u;
+    }
+    for (int e = tid; e < K * C; e += 256) ws[e] = h2f(w[e]);
+    __syncthreads();
+    const int t = t0 + tid;
+    if (t >= T) return;
+    float acc = 0.0f;
+    for (int j = 0; j < K; ++j) {
+        const uint16_t *xr = xs + (tid + j) * C;
+        const float *wr = ws + j * C;
+        for (int c = 0; c < C; c += 8) {
+            const uint4 u = *reinterpret_cast<const uint4 *>(xr + c);
+            const uint32_t q[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                acc += h2f((uint16_t)(q[e] & 0xffff)) * wr[c + 2 * e];
+                acc += h2f((uint16_t)(q[e] >> 16)) * wr[c + 2 * e + 1];
+            }
+        }
+    }
+    y[t] = tanhf(acc + bias[0]);
+}
+bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s) {
+    if (C % 8 != 0 || C > CO1_MAXC || K > CO1_MAXK) { set_error("conv_out1: unsupported shape"); return false; }
+    if (T <= 0) return true;
+    hipLaunchKernelGGL(k_conv_out1, dim3((T + CO1_T - 1) / CO1_T), dim3(256), 0, s, xh, w, bias, y, T, C, K);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 // ======================================================================================= depthwise causal conv
 // y[t][c] = b[c] + sum_j w[c][j] * f16(x[t + j - (K-1)][c])      (ggml_pad_ext + ggml_conv_1d_dw, im2col F16)
 __global__ void __launch_bounds__(256) k_dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K) {
@@ -372,83 +505,120 @@ bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, 
 // ======================================================================================= pre-transformer attention
 // causal softmax attention over F frames (apply_pre_tfm_layer, audio_tokenizer_decoder.cpp:412-456): NEOX RoPE
 // (theta 1e4) on q,k, f32 scores (ggml mul_mat of two F32 tensors: no rounding), output rounded to f16.
-// grid (query tiles of 16, heads); 16 lanes per query row, 4 keys / 4 dims per lane.
-__global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH) {
-    constexpr int D = 64, QT = 16, KT = 64;
-    __shared__ float qs[QT][D];
-    __shared__ float ks[KT][D + 1];
-    __shared__ float vs[KT][D + 1];
-    __shared__ float ps[QT][KT];
+// Two launches: RoPE applied once, in place, to the q and k columns of the qkv rows (the attention then streams plain
+// rows); then one workgroup per (32 queries, head) walks 64-key chunks: K/V chunk in LDS via coalesced float4 loads,
+// 8 lanes per query (8 keys each for the scores, 8 dims each for P.V), online softmax within the 8-lane group.
+__global__ void k_rope_qk(float *qkv, const float *rope, int F, int nH) {
+    constexpr int D = 64;
+    const int idx = blockIdx.x * 256 + threadIdx.x;   // (pos, q/k, head, pair)
+    const int total = F * 2 * nH * 32;
+    if (idx >= total) return;
+    const int i = idx & 31, hh = (idx >> 5) % (2 * nH), pos = idx / (64 * nH);
+    float *x = qkv + (size_t)pos * 3 * nH * D + hh * D;   // hh < nH: q head, else k head
+    const float c = rope[(size_t)pos * D + 2 * i], sn = rope[(size_t)pos * D + 2 * i + 1];
+    const float x0 = x[i], x1 = x[i + 32];
+    x[i] = x0 * c - x1 * sn;
+    x[i + 32] = x0 * sn + x1 * c;
+}
+
+__global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, uint16_t *out, int F, int nH) {
+    constexpr int D = 64, QT = 32, KT = 64, KP = D + 4;
+    __shared__ __attribute__((aligned(16))) float ks[KT * KP];
+    __shared__ __attribute__((aligned(16))) float vs[KT * KP];
+    __shared__ float ps[QT][KT + 1];
     const int h = blockIdx.y, q0 = blockIdx.x * QT;
-    const int tid = threadIdx.x, qi = tid / 16, l16 = tid % 16;
+    const int tid = threadIdx.x, qi = tid >> 3, g = tid & 7;
     const int LD = 3 * nH * D;
-    auto rope_load = [&](const float *src, int pos, int e) -> float {
-        // NEOX pair (e, e+32)
-        const int i = e & 31;
-        const float c = rope[(size_t)pos * D + 2 * i], sn = rope[(size_t)pos * D + 2 * i + 1];
-        const float x0 = src[i], x1 = src[i + 32];
-        return e < 32 ? x0 * c - x1 * sn : x0 * sn + x1 * c;
-    };
-    for (int e = tid; e < QT * D; e += 256) {
-        const int qq = e / D, d = e % D, pos = q0 + qq;
-        qs[qq][d] = pos < F ? rope_load(qkv + (size_t)pos * LD + h * D, pos, d) : 0.0f;
-    }
-    float m = -INFINITY, l = 0.0f, acc[4] = {0.f, 0.f, 0.f, 0.f};
     const int qpos = q0 + qi;
-    const float scale = 1.0f / sqrtf((float)D);
+    float q[D];
+    {
+        const float *src = qkv + (size_t)min(qpos, F - 1) * LD + h * D;
+#pragma unroll
+        for (int d = 0; d < D; d += 4) {
+            const float4 v = *reinterpret_cast<const float4 *>(src + d);
+            q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
+        }
+    }
+    float m = -INFINITY, l = 0.0f, acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
+    const float scale = 0.125f;   // 1 / sqrt(64)
     const int kend = min(F, q0 + QT);
     for (int k0 = 0; k0 < kend; k0 += KT) {
         __syncthreads();
-        for (int e = tid; e < KT * D; e += 256) {
-            const int kk = e / D, d = e % D, pos = k0 + kk;
-            const float *row = qkv + (size_t)pos * LD;
-            ks[kk][d] = pos < F ? rope_load(row + nH * D + h * D, pos, d) : 0.0f;
-            vs[kk][d] = pos < F ? row[2 * nH * D + h * D + d] : 0.0f;
+        // chunk: 64 keys x 64 dims of K and V, 4 float4 per thread per tensor
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = (u * 256 + tid) * 4, kk = e / D, d = e % D, pos = k0 + kk;
+            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+            if (pos < F) {
+                const float *row = qkv + (size_t)pos * LD;
+                kv = *reinterpret_cast<const float4 *>(row + nH * D + h * D + d);
+                vv = *reinterpret_cast<const float4 *>(row + 2 * nH * D + h * D + d);
+            }
+            *reinterpret_cast<float4 *>(ks + kk * KP + d) = kv;
+            *reinterpret_cast<float4 *>(vs + kk * KP + d) = vv;
         }
         __syncthreads();
-        float s[4];
-        float mt = -INFINITY;
+        float sc[8], mt = -INFINITY;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int kk = l16 * 4 + t, kpos = k0 + kk;
-            float d = 0.0f;
-#pragma unroll 16
-            for (int e = 0; e < D; ++e) d += ks[kk][e] * qs[qi][e];
-            s[t] = (kpos <= qpos && kpos < F) ? d * scale : -INFINITY;
-            mt = fmaxf(mt, s[t]);
+        for (int i = 0; i < 8; ++i) {
+            const int kk = g + 8 * i, kpos = k0 + kk;
+            const float *kr = ks + kk * KP;
+            float dsum = 0.0f;
+#pragma unroll
+            for (int d = 0; d < D; d += 4) {
+                const float4 kv = *reinterpret_cast<const float4 *>(kr + d);
+                dsum += q[d] * kv.x + q[d + 1] * kv.y + q[d + 2] * kv.z + q[d + 3] * kv.w;
+            }
+            sc[i] = (kpos <= qpos && kpos < F) ? dsum * scale : -INFINITY;
+            mt = fmaxf(mt, sc[i]);
         }
-        mt = group_max<16>(mt);
+        mt = fmaxf(mt, __shfl_xor(mt, 1));
+        mt = fmaxf(mt, __shfl_xor(mt, 2));
+        mt = fmaxf(mt, __shfl_xor(mt, 4));
         const float mn = fmaxf(m, mt);
-        const float corr = (m == -INFINITY) ? 0.0f : expf(m - mn);
+        const float corr = m == -INFINITY ? 0.0f : expf(m - mn);
         float ls = 0.0f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float pv = (s[t] == -INFINITY) ? 0.0f : expf(s[t] - mn);
-            ps[qi][l16 * 4 + t] = pv;
+        for (int i = 0; i < 8; ++i) {
+            const float pv = sc[i] == -INFINITY ? 0.0f : expf(sc[i] - mn);
+            ps[qi][g + 8 * i] = pv;
             ls += pv;
         }
-        ls = group_sum<16>(ls);
+        ls += __shfl_xor(ls, 1);
+        ls += __shfl_xor(ls, 2);
+        ls += __shfl_xor(ls, 4);
         l = l * corr + ls;
         m = mn;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] *= corr;
+        for (int e = 0; e < 8; ++e) acc[e] *= corr;
         __syncthreads();
-        for (int kk = 0; kk < KT; ++kk) {
+        const int kn = min(KT, kend - k0);
+        for (int kk = 0; kk < kn; ++kk) {
             const float pv = ps[qi][kk];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] += pv * vs[kk][l16 * 4 + t];
+            const float4 a = *reinterpret_cast<const float4 *>(vs + kk * KP + g * 8);
+            const float4 b = *reinterpret_cast<const float4 *>(vs + kk * KP + g * 8 + 4);
+            acc[0] += pv * a.x; acc[1] += pv * a.y; acc[2] += pv * a.z; acc[3] += pv * a.w;
+            acc[4] += pv * b.x; acc[5] += pv * b.y; acc[6] += pv * b.z; acc[7] += pv * b.w;
         }
     }
     if (qpos < F) {
         const float inv = 1.0f / l;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) out[(size_t)qpos * nH * D + h * D + l16 * 4 + t] = f2h(acc[t] * inv);
+        uint4 o;
+        o.x = (uint32_t)f2h(acc[0] * inv) | ((uint32_t)f2h(acc[1] * inv) << 16);
+        o.y = (uint32_t)f2h(acc[2] * inv) | ((uint32_t)f2h(acc[3] * inv) << 16);
+        o.z = (uint32_t)f2h(acc[4] * inv) | ((uint32_t)f2h(acc[5] * inv) << 16);
+        o.w = (uint32_t)f2h(acc[6] * inv) | ((uint32_t)f2h(acc[7] * inv) << 16);
+        *reinterpret_cast<uint4 *>(out + (size_t)qpos * nH * D + h * D + g * 8) = o;
     }
 }
-bool attn_prefill(const float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s) {
+bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s) {
     if (D != 64) { set_error("attn_prefill: head_dim must be 64"); return false; }
     if (F <= 0) return true;
-    hipLaunchKernelGGL(k_attn_prefill, dim3((F + 15) / 16, nH), dim3(256), 0, s, qkv, rope, out, F, nH);
+    hipLaunchKernelGGL(k_rope_qk, dim3((F * 2 * nH * 32 + 255) / 256), dim3(256), 0, s, qkv, rope, F, nH);
+    Q3T_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_attn_prefill, dim3((F + 31) / 32, nH), dim3(256), 0, s, qkv, out, F, nH);
     Q3T_HIP(hipGetLastError());
     return true;
 }

@@ -39,6 +39,12 @@ def main():
     p = sys.argv[1]
     by_grid = "--by-grid" in sys.argv
     ev = from_db(p) if p.endswith(".db") else from_csv(p)
+    if "--seq" in sys.argv:   # the last N dispatches in time order
+        n = int(sys.argv[sys.argv.index("--seq") + 1])
+        ev.sort(key=lambda x: x[1])
+        for name, s, e, g in ev[-n:]:
+            print(f"{(e - s) / 1e3:9.2f} us  {short(name)} {g}")
+        return
     agg = collections.defaultdict(lambda: [0, 0.0])
     for n, s, e, g in ev:
         a = agg[short(n) + (" " + g if by_grid else "")]
