@@ -31,6 +31,7 @@ KV_BYTES_PER_POS = 114_688         # 28 layers x 2 (K,V) x 8 heads x 128 x 2 B
 CP_PASS_BYTES = 5 * 15_728_640 * 2
 CP_HEAD_BYTES = 2048 * 1024 * 2
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
+MFMA_PEAK_TFLOPS = 2500.0          # dense f16/bf16 MFMA, MI355X_MICROARCH.md (spec; sparsity figures excluded)
 
 
 def log(*a):
@@ -67,7 +68,8 @@ def cpu_baseline(tts, tok, prompt, frames, vocoder_mode):
     [ggml-upstream]; the all-cores figure (OMP_NUM_THREADS) is reported beside it."""
     res = {}
     allc = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    for threads, n in ((4, 24), (allc, 24)):
+    # samples sized to ~10-30 s of CPU work in total (4 threads: ~110 ms/frame; all cores: ~35 ms/frame)
+    for threads, n in ((4, 96), (allc, 128)):
         total, tp, tf, tv, nf, wall = _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n)
         res[threads] = dict(value=round(frames / total, 3), rtf=round(total / (frames * FRAME_SEC), 4),
                             sample=f"prefill + {nf} frames + vocoder of {nf} frames ({wall:.1f} s of CPU work): "
@@ -159,6 +161,13 @@ def pmc_traffic(slots):
     return (round(float(m.group(1)) * 1e6), os.path.relpath(files[-1], REPO)) if m else (None, None)
 
 
+def pmc_file(tag):
+    """newest committed MFMA-utilisation table (tools/dev/gpu_mfma.sh: kernel trace + SQ_INSTS_MFMA / FETCH / WRITE)"""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_mfma_{tag}.txt")))
+    return os.path.relpath(files[-1], REPO) if files else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -244,6 +253,20 @@ def main():
     t_cp = eng.time_stage(1, B, p_mid, max(1, args.stage_iters // 2))
     cp_bytes = 16 * CP_PASS_BYTES + 15 * CP_HEAD_BYTES
 
+    # ---- vocoder (MFMA-bound): algorithmic FLOPs of the loaded conv / projection shapes over the
+    # measured vocoder time of the step; SQ_INSTS_MFMA evidence per kernel in profiles/rNN_pmc_mfma_vocoder.txt
+    voc_flops = eng.vocoder_flops(args.frames) if voc_mode == q3t.VOCODER_FULL else None
+
+    def voc_roofline(voc_ms, n_utt, steps):
+        if not voc_flops or voc_ms <= 0:
+            return None
+        tf = voc_flops * n_utt * steps / (voc_ms * 1e-3) / 1e12
+        return {"bound": "mfma", "kernel": "FULL vocoder of one utterance per call (k_conv_mt implicit-GEMM convs on "
+                                           "v_mfma_f32_32x32x16_f16, transposed convs one launch per conv)",
+                "achieved": round(tf, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "flops_per_decode": round(voc_flops),
+                "ms_per_decode": round(voc_ms / (n_utt * steps), 3), "mfma_pmc": pmc_file("vocoder")}
+
     # ---- secondary: BASELINE configs[2], `batched` concurrent utterances through the matrix-core path
     bres = None
     if batched > 0:
@@ -268,12 +291,15 @@ def main():
                 "breakdown_ms_per_step": {k: round(v, 1) for k, v in stats.items()},
                 "talker_step_ms": round(bt, 4), "cp_frame_ms": round(bc, 4),
                 "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots "
-                                                       "(MFMA f16 GEMMs on hoisted norms, split-K slabs, batched split-K "
-                                                       "attention: 7 launches per layer)",
+                                                       "(MFMA f16 GEMMs on hoisted norms, split-K slabs, k_attn_seq: one "
+                                                       "workgroup per (slot, kv head) streaming the whole context: 7 "
+                                                       "launches per layer)",
                              "achieved": round(b_bytes / (bt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(b_bytes / (bt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": pmc_traffic(batched)[0], "traffic_source": pmc_traffic(batched)[1],
-                             "bytes_per_launch": b_bytes, "launch_ms": round(bt, 4)}}
+                             "bytes_per_launch": b_bytes, "launch_ms": round(bt, 4)},
+                "vocoder_roofline": voc_roofline(stats["vocoder_ms"], batched, 1),
+                "mfma_pmc": pmc_file("talker_b64"), "mfma_pmc_cp": pmc_file("cp_b64")}
 
     if rank == 0:
         res = {
@@ -297,6 +323,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(B)[0],
                          "traffic_source": pmc_traffic(B)[1],
                          "bytes_per_launch": talker_bytes, "launch_ms": round(t_talker, 4)},
+            "vocoder_roofline": voc_roofline(main_stats["vocoder_ms"], B, args.steps),
             "cp_roofline": {"achieved": round(cp_bytes / (t_cp * 1e-3) / 1e9, 1), "unit": "GB/s",
                             "bytes_per_frame": cp_bytes, "note": "157 MB of CP weights re-read 16x per frame "
                             "(Infinity-Cache resident), algorithmic bytes / time"},

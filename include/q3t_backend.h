@@ -114,6 +114,9 @@ int q3t_persist_status(q3t_ctx *ctx);
 
 /* ---- vocoder */
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);
+/* algorithmic FLOPs of one FULL decode of n_frames (sum of 2*M*K*N over the loaded conv / projection shapes and the
+ * causal attention); bench.py's MFMA-utilisation figure.  -1 without a vocoder */
+double q3t_vocoder_flops(const q3t_ctx *ctx, int32_t n_frames);
 int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, int32_t n_frames, int mode,
                        float *pcm /* [q3t_vocoder_num_samples] */, int64_t *n_samples);
 

@@ -228,6 +228,13 @@ int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode) 
     return v->n_samples(n_frames, mode);
 }
 
+double q3t_vocoder_flops(const q3t_ctx *ctx, int32_t n_frames) {
+    if (!ctx) return -1.0;
+    q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();
+    if (!v || !v->loaded()) return -1.0;
+    return v->decode_flops(n_frames);
+}
+
 int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes, int32_t n_frames, int mode, float *pcm, int64_t *n_samples) {
     GUARD_BEGIN
     CHECK_CTX(ctx);

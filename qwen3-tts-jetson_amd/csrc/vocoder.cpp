@@ -247,6 +247,33 @@ int64_t Vocoder::full_len(int F) const {
     for (int d = 0; d < 4; ++d) { const int s = dec_[d].rate, K = dec_[d].ct.k; T = (T - 1) * s + K - 2 * (K - s); }
     return T;
 }
+double Vocoder::decode_flops(int F) const {
+    if (F <= 0 || !loaded_) return 0.0;
+    const double f = F, VH = hidden_, LAT = latent_;
+    auto conv = [](double T_out, const Conv &c) { return 2.0 * T_out * c.ic * c.oc * c.k; };
+    double fl = 16.0 * 2.0 * f * cb_dim_ * VH;                 // RVQ output projections
+    fl += conv(f, pre_conv_) + 2.0 * f * LAT * VH;             // pre-conv, input_proj
+    for (size_t l = 0; l < layers_.size(); ++l)
+        fl += 2.0 * f * VH * 3 * LAT + 2.0 * 2.0 * (f * (f + 1) / 2) * LAT + 2.0 * f * LAT * VH +
+              2.0 * f * VH * 2 * ffn_ + 2.0 * f * ffn_ * VH;
+    fl += 2.0 * f * VH * LAT;                                  // output_proj
+    double T = f;
+    for (int u = 0; u < 2; ++u) {
+        const double T1 = (T - 1) * 2 + up_[u].ct.k;
+        fl += conv(T, up_[u].ct) + 2.0 * T1 * LAT * up_[u].dw_k + 2.0 * 2.0 * T1 * LAT * up_[u].pw_dim;
+        T = T1;
+    }
+    fl += conv(T, dec0_);
+    for (int d = 0; d < 4; ++d) {
+        const Dec &D = dec_[d];
+        const double T2 = (T - 1) * D.rate + D.ct.k - 2 * (D.ct.k - D.rate);
+        fl += conv(T, D.ct);   // every input row meets every tap once (before trimming)
+        for (int r = 0; r < 3; ++r) fl += conv(T2, D.res[r].c1) + conv(T2, D.res[r].c2);
+        T = T2;
+    }
+    return fl + conv(T, dec6_);
+}
+
 int64_t Vocoder::n_samples(int n_frames, int mode) const {
     if (n_frames <= 0) return 0;
     return mode == 0 ? full_len(n_frames) : (int64_t)n_frames * 1920;

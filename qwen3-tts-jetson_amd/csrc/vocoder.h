@@ -23,7 +23,10 @@ public:
     bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s);
     bool ensure(int n_frames);
     bool loaded() const { return loaded_; }
-    int n_usage_normalised() const { return n_usage_; }   // codebooks divided by *.usage at load (0 for converter output)
+    int n_usage_normalised() const { return n_usage_; }
+    // algorithmic FLOPs of one FULL decode of F frames: 2*M*K*N over every conv (per tap), transposed conv, projection
+    // and the causal attention (QK^T + PV over the lower triangle), from the loaded shapes
+    double decode_flops(int n_frames) const;   // codebooks divided by *.usage at load (0 for converter output)
 
 private:
     struct Conv { uint16_t *w = nullptr; float *b = nullptr; int k = 0, ic = 0, oc = 0; };   // w: [k][oc][ic]

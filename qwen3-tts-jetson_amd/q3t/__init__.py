@@ -67,6 +67,8 @@ if hasattr(_lib, "q3t_debug_read"):   # development builds only (make -C csrc DE
     _lib.q3t_debug_read.argtypes = [_P, _I, _P, C.c_size_t]
 _lib.q3t_vocoder_num_samples.restype = C.c_int64
 _lib.q3t_vocoder_num_samples.argtypes = [_P, C.c_int32, _I]
+_lib.q3t_vocoder_flops.restype = C.c_double
+_lib.q3t_vocoder_flops.argtypes = [_P, C.c_int32]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_vocoder_decode_chunked.argtypes = [_P, _ip, C.c_int32, C.c_int32, C.c_int32, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_speaker_dim.argtypes = [_P]
@@ -88,7 +90,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_decode",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
            "q3t_tokenizer_decode", "q3t_talker_forward",
@@ -305,6 +307,10 @@ class Engine:
     # ---- vocoder
     def vocoder_num_samples(self, n_frames, mode=VOCODER_FULL):
         return _lib.q3t_vocoder_num_samples(self.h, int(n_frames), int(mode))
+
+    def vocoder_flops(self, n_frames):
+        """algorithmic FLOPs of one FULL decode of n_frames"""
+        return _lib.q3t_vocoder_flops(self.h, int(n_frames))
 
     def vocoder(self, codes, mode=VOCODER_FULL):
         codes = np.ascontiguousarray(codes, np.int32).reshape(-1, 16)
