@@ -13,6 +13,7 @@
 using namespace q3t;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 static hipStream_t st;
+__global__ void k_empty(int *p) { if (p && threadIdx.x == 999) p[0] = 1; }
 
 template <class T>
 T *dev(size_t n, float fill) {
@@ -51,6 +52,10 @@ int main(int argc, char **argv) {
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     gemm_mfma_set_min_batch(1);
     const int NC = 28;
+    for (int wg : {1, 256, 1024}) {   // floor: an empty kernel per graph node
+        const double us = time_graph(NC, [&](int) { hipLaunchKernelGGL(k_empty, dim3(wg), dim3(256), 0, st, nullptr); return true; });
+        printf("empty kernel, %4d workgroups: %6.2f us per graph node\n", wg, us);
+    }
     float *x = dev<float>((size_t)B * 4096, 1.0f), *nw = dev<float>(4096, 1.0f);
     float *out = dev<float>((size_t)B * 8192, 0.0f), *resid = dev<float>((size_t)B * 4096, 1.0f);
     uint16_t *xh = dev<uint16_t>((size_t)B * 4096, 1.0f), *oh = dev<uint16_t>((size_t)B * 8192, 0.0f);
@@ -59,7 +64,9 @@ int main(int argc, char **argv) {
                             {"gu   N6144 K1024 RMS+SwiGLU", 6144, 1024, PRO_RMS, ACT_SWIGLU},
                             {"o    N1024 K2048 F16+res", 1024, 2048, PRO_F16, ACT_NONE},
                             {"down N1024 K3072 F16+res", 1024, 3072, PRO_F16, ACT_NONE},
-                            {"head N2048 K1024 RMS", 2048, 1024, PRO_RMS, ACT_NONE}};
+                            {"head N2048 K1024 RMS", 2048, 1024, PRO_RMS, ACT_NONE},
+                            {"qkv  N4096 K1024 F16", 4096, 1024, PRO_F16, ACT_NONE},
+                            {"gu   N6144 K1024 F16+SwiGLU", 6144, 1024, PRO_F16, ACT_SWIGLU}};
     for (const Shape &sh : shapes) {
         std::vector<uint16_t *> W(NC);
         for (int c = 0; c < NC; ++c) W[c] = dev<uint16_t>((size_t)sh.N * sh.K, 0.05f);
@@ -68,7 +75,10 @@ int main(int argc, char **argv) {
                 GemvParams p;
                 p.W = W[i % NC]; p.N = sh.N; p.K = sh.K; p.B = B; p.pro = sh.pro; p.act = sh.act; p.dbg = dbg;
                 p.nw = nw; p.eps = 1e-6f;
-                if (sh.pro == PRO_F16) { p.x = xh; p.ldx = sh.K; p.resid = resid; p.ldr = sh.N; p.out_f32 = resid; }
+                if (sh.pro == PRO_F16) {
+                    p.x = xh; p.ldx = sh.K;
+                    if (sh.N == 1024) { p.resid = resid; p.ldr = sh.N; p.out_f32 = resid; }
+                }
                 else { p.x = x; p.ldx = sh.K; }
                 if (sh.act == ACT_SWIGLU) { p.out_f16 = oh; p.ldo = sh.N / 2; }
                 else { if (!p.out_f32) p.out_f32 = out; p.ldo = sh.N; }
