@@ -10,6 +10,8 @@
 // add; the last adder loads the partials with sc1 loads) -- no combine launch, no release/acquire cache flushes.
 #include "kernels.h"
 
+#include <type_traits>
+
 #pragma clang fp contract(off)   // every rounding as written (persist.hip reproduces this kernel bit for bit)
 
 namespace q3t {
@@ -30,6 +32,14 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&f)[8]) {
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) { f[2 * e] = h2f(w[e] & 0xffff); f[2 * e + 1] = h2f(w[e] >> 16); }
+}
+// the same with each converted value materialised: the consumer FMA may not absorb the conversion into a
+// v_fma_mix_f32 (whose f16 operands do not go through v_cvt_f32_f16: k_attn_seq's whole chunks then differed from
+// its masked last chunk, where a select sits between the two)
+__device__ __forceinline__ void unpack8_cvt(const uint4 u, float (&f)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[2 * e] = opaque(h2f(w[e] & 0xffff)); f[2 * e + 1] = opaque(h2f(w[e] >> 16)); }
 }
 
 template <int D, int RMAX, int CHUNK>
@@ -285,8 +295,16 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 // (max, sum, 8-dim accumulator per head) over its 16 positions of every chunk, so no barrier is taken per chunk; the
 // four waves merge once at the end.  Same per-position arithmetic as k_attn (explicit roundings); the rescaling order
 // of the online softmax differs from the split combine (f32).
+//
+// The kernel is issue-bound, not HBM-bound (one wave per SIMD saw every instruction's latency): every chunk but the
+// last is whole (all 64 positions <= pos), so it runs without position masks, without the new-row branch and without
+// the empty-wave test; the new K/V row (pos) is patched into the last chunk's registers once, from LDS (exact: the
+// LDS copy is the f16 value).
+#ifndef Q3T_ATTN_SEQ_MINB
+#define Q3T_ATTN_SEQ_MINB 2
+#endif
 template <int D, int R>
-__global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
+__global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnParams p) {
     constexpr int LPP = D / 8, NP = 4;       // 16 lanes per position, 4 passes of 16 positions per 64-chunk
     static_assert(LPP == 16, "D = 128");
     const int slot = blockIdx.x, g = blockIdx.y;
@@ -294,7 +312,7 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
     const int nch = pos / 64 + 1;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
     __shared__ float q_s[R][D];
-    __shared__ float kn_s[D], vn_s[D];
+    __shared__ __attribute__((aligned(16))) uint16_t kh_s[D], vh_s[D];
     __shared__ float wm[4][R], wl[4][R];
     __shared__ float wa[4][R][D];
 
@@ -317,7 +335,7 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
     for (int v = wave; v < R + 2; v += 4) {
         if (v == R + 1) {
 #pragma unroll
-            for (int e = 0; e < 2; ++e) vn_s[lane + 64 * e] = f16r(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
+            for (int e = 0; e < 2; ++e) vh_s[lane + 64 * e] = f2h(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
             continue;
         }
         const bool isk = v == R;
@@ -334,14 +352,18 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
         const float c = rope[2 * lane], s = rope[2 * lane + 1];
         const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
         const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
-        float *dst = isk ? kn_s : q_s[v];
-        dst[lane] = f16r(y0);
-        dst[lane + 64] = f16r(y1);
+        if (isk) {
+            kh_s[lane] = f2h(y0);
+            kh_s[lane + 64] = f2h(y1);
+        } else {
+            q_s[v][lane] = f16r(y0);
+            q_s[v][lane + 64] = f16r(y1);
+        }
     }
     __syncthreads();
     for (int e = t; e < D; e += 256) {   // KV append at pos
-        p.kc[head_off + (size_t)pos * D + e] = f2h(kn_s[e]);
-        p.vc[head_off + (size_t)pos * D + e] = f2h(vn_s[e]);
+        p.kc[head_off + (size_t)pos * D + e] = kh_s[e];
+        p.vc[head_off + (size_t)pos * D + e] = vh_s[e];
     }
     const float kq_scale = 1.0f / sqrtf((float)D);
     float q8[R][8];
@@ -358,20 +380,16 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
     }
-    auto chunk = [&](int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
+    // one chunk; LAST: positions past pos masked, a wave may hold no live position yet
+    auto chunk = [&](auto last_tag, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
+        constexpr bool LAST = decltype(last_tag)::value;
         float sc[NP][R];
         bool ok[NP];
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
-            const int j = c * 64 + pi * 16 + pg;
-            ok[pi] = j <= pos;
+            ok[pi] = !LAST || c * 64 + pi * 16 + pg <= pos;
             float k8[8];
-            if (j == pos) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) k8[e] = kn_s[li * 8 + e];
-            } else {
-                unpack8(kr[pi], k8);
-            }
+            unpack8_cvt(kr[pi], k8);
 #pragma unroll
             for (int h = 0; h < R; ++h) {
                 float s = 0.0f;
@@ -388,7 +406,7 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
             for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
             mc = rows_max(mc);                      // this wave's 16 positions of the chunk
             const float mn = fmaxf(m[h], mc);
-            if (mn == -INFINITY) continue;          // no live position in this wave yet
+            if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
             const float alpha = expf(__fsub_rn(m[h], mn));
             l[h] *= alpha;
 #pragma unroll
@@ -397,14 +415,8 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
         }
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
-            const int j = c * 64 + pi * 16 + pg;
             float v8[8];
-            if (j == pos) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v8[e] = vn_s[li * 8 + e];
-            } else {
-                unpack8(vr[pi], v8);
-            }
+            unpack8_cvt(vr[pi], v8);
 #pragma unroll
             for (int h = 0; h < R; ++h) {
                 const float pr = ok[pi] ? expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
@@ -414,12 +426,26 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
             }
         }
     };
+    // the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
+    auto patch = [&](uint4 (&kr)[NP], uint4 (&vr)[NP]) {
+        if (pg == (pos & 15)) {
+            const uint4 kn = *reinterpret_cast<const uint4 *>(&kh_s[li * 8]);
+            const uint4 vn = *reinterpret_cast<const uint4 *>(&vh_s[li * 8]);
+#pragma unroll
+            for (int pi = 0; pi < NP; ++pi)
+                if (pi == ((pos & 63) >> 4)) { kr[pi] = kn; vr[pi] = vn; }
+        }
+    };
+    using whole = std::integral_constant<bool, false>;
+    using last = std::integral_constant<bool, true>;
     for (int c = 0; c < nch; c += 2) {
         if (c + 1 < nch) issue(c + 1, kb, vb);
-        chunk(c, ka, va);
+        if (c + 1 < nch) chunk(whole{}, c, ka, va);
+        else { patch(ka, va); chunk(last{}, c, ka, va); }
         if (c + 1 < nch) {
             if (c + 2 < nch) issue(c + 2, ka, va);
-            chunk(c + 1, kb, vb);
+            if (c + 2 < nch) chunk(whole{}, c + 1, kb, vb);
+            else { patch(kb, vb); chunk(last{}, c + 1, kb, vb); }
         }
     }
     // merge the four waves
@@ -448,6 +474,7 @@ __global__ void __launch_bounds__(256) k_attn_seq(const AttnParams p) {
         p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(num / den);
     }
 }
+
 
 bool attn_decode(const AttnParams &p, hipStream_t s) {
     if (p.seqk && p.D == 128 && p.nH == 2 * p.nKV) {
