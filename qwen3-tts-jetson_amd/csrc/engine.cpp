@@ -431,6 +431,21 @@ bool Engine::debug_read(int which, void *dst, size_t bytes) {
 }
 #endif
 
+// test hook (Q3T_PERSIST_FAULT_AT=n): the graph replay that contains the n-th persistent launch of this context runs
+// with the abort word already set, exactly as if one of its hand-off waits had given up.  Host-side on purpose: a
+// device-side launch counter in k_persist's prologue cost 32 us per talker step in code generation alone.
+bool Engine::persist_fault_hook(int S, int n_launches) {
+    if (!opt_.persist_fault_at || S != 1 || !persist_ || !pstate_) return true;
+    const unsigned before = persist_launches_;
+    persist_launches_ += (unsigned)n_launches;
+    if (before < opt_.persist_fault_at && opt_.persist_fault_at <= persist_launches_) {
+        PersistParams p;
+        persist_carve(pstate_, p);
+        Q3T_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.err), 1, 1, stream_));
+    }
+    return true;
+}
+
 bool Engine::persist_error() {
     if (!persist_ || !pstate_) return false;
     PersistParams p;
@@ -622,7 +637,6 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         if (std::getenv("Q3T_PERSIST_DBG")) { p.dbg_qkv = qkv_; p.dbg_attn = attn_; }   // layer-0 intermediates
 #endif
         p.prof = pprof_;
-        p.fault_at = opt_.persist_fault_at;
         return persist_talker_step(p, s);
     }
     StackInput in0;
@@ -675,7 +689,6 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         p.heads = heads_dev_; p.out_norm = cp_out_norm_; p.logits = cp_logits_;
         p.sel = select_spec(SEL_CP, gp_, 0, 0);
         p.prof = pprof_;
-        p.fault_at = opt_.persist_fault_at;
         return persist_cp_frame(p, s);
     }
     const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
@@ -962,6 +975,7 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     for (int t = 0; t < plen; ++t) {
         Q3T_HIP(hipMemcpy2DAsync(x_, H * 4, prefill_ + (size_t)t * H, (size_t)10 * H * 4, H * 4, S, hipMemcpyDeviceToDevice, stream_));
         Q3T_HIP(hipMemcpyAsync(pos_, cp_pos_ + (size_t)t * max_slots_, S * 4, hipMemcpyDeviceToDevice, stream_));
+        if (!persist_fault_hook(S, 1)) return false;
         Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
     }
     for (int s = 0; s < S; ++s) posv[s] = plen;
@@ -1017,6 +1031,7 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     };
     bool all_done = false;
     for (int f = 0; f < gp.max_len && !all_done && n_live > 0; ++f) {
+        if (!persist_fault_hook(S, persist_cp_ ? 2 : 1)) return false;
         Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
         if (dbg) { fprintf(stderr, "[q3t] frame %d launched\n", f); fflush(stderr); }
         if (stream_cb && (f + 1) % interval == 0) {

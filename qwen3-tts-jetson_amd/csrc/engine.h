@@ -112,6 +112,8 @@ public:
     bool time_stage(int stage, int S, int pos, int iters, double *ms);
 
     // true if a persistent launch gave up waiting on a hand-off (never expected: a protocol fault)
+    bool persist_fault_hook(int S, int n_launches);   // Q3T_PERSIST_FAULT_AT test hook (host side)
+    unsigned persist_launches_ = 0;
     bool persist_error();
     bool persist_enabled() const { return persist_; }
     bool persist_fell_back() const { return persist_fallback_; }

@@ -51,9 +51,6 @@ struct PersistParams {
     uint16_t *dbg_attn = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
-    unsigned *launches = nullptr;  // device launch counter (fault injection)
-    unsigned spin_limit = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
-    unsigned fault_at = 0;         // test hook: the fault_at-th launch of this state block flags a fault (0 = never)
 };
 
 // shapes the persistent step supports: H 1024, 16 q / 8 kv heads of 128, I 3072, V 3072, one workgroup per CU on a

@@ -24,6 +24,7 @@ constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, IN
 constexpr int G = 256;          // workgroups (one per CU)
 constexpr int MAXSPLIT = G / NKV;
 constexpr int R = NH / NKV;     // q heads per kv head
+constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
 constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
 
@@ -64,11 +65,10 @@ __device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two 
 
 struct Ctl {
     unsigned *err;
-    unsigned limit;   // polls before giving up (PersistParams::spin_limit)
     bool abort;
 };
 
-// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after c.limit polls (or once any
+// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
 // workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
 template <int N>
 __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
@@ -83,7 +83,7 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
         if (ok || c.abort) break;
         ++it;
         if ((it & 255u) == 0) {
-            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= c.limit) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
                 c.abort = true;
                 __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
@@ -174,12 +174,8 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     constexpr int NP = CH / 16;   // positions per lane group pass (16 lanes per position, 16 positions per pass)
     const int w = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15, grp = t >> 4;
     const int grp4 = lane >> 4;   // row of a KS = 4 GEMV
-    Ctl c{p.err, p.spin_limit, false};
+    Ctl c{p.err, false};
     const unsigned seq = __hip_atomic_load(p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (p.fault_at && w == 0 && t == 0) {   // test hook: this launch flags a protocol fault (every wait then gives up)
-        const unsigned n = __hip_atomic_fetch_add(p.launches, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-        if (n == p.fault_at) __hip_atomic_fetch_or(p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     auto TAG = [&](int ph) -> uint32_t { return ((seq * 1024u + (unsigned)ph) << 1) | 1u; };
     int pos = MODE == 0 ? p.pos[0] : 0;
     const int nsplit = MODE == 0 ? pos / CH + 1 : 1;
@@ -724,7 +720,6 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.head_ticket = ctr + 16;  // own 64-B line
     p.err = ctr + 32;
     p.ticket = ctr + 48;       // [8]
-    p.launches = ctr + 56;
 }
 
 template <int MODE, int CH>
