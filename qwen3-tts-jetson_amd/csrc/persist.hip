@@ -26,7 +26,8 @@ constexpr int MAXSPLIT = G / NKV;
 constexpr int R = NH / NKV;     // q heads per kv head
 constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
-constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
+constexpr int PSLOT = 264;
+constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgroup only at 32 splits)      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
 
 template <class V>
 __device__ __forceinline__ V ldgv(const void *p) {
@@ -55,7 +56,6 @@ __device__ __forceinline__ void g_put(uint64_t *p, uint32_t payload, uint32_t ta
 __device__ __forceinline__ uint64_t g_ld(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_sc1f(float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two agent-scope (L1-bypassing) 8-B loads
     uint64_t *q = reinterpret_cast<uint64_t *>(const_cast<uint16_t *>(p));
     const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -623,27 +623,33 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         for (int tt = 4; tt < 8; ++tt) a1 = dot8(wh[tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a1);
         a0 = group_sum<16>(a0);
         a1 = group_sum<16>(a1);
-        if (l16 == 0 && grp < RPW) st_sc1f(p.logits + w * RPW + grp, a0 + a1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (l16 == 0 && grp < RPW) {
+            const float lg = a0 + a1;
+            p.logits[w * RPW + grp] = lg;   // read after the launch only (host, tests)
+            g_put(p.glog + w * RPW + grp, __float_as_uint(lg), TAG(hph));
+        }
         PROF(hph, 2);
-        if (t == 0) S.last = __hip_atomic_fetch_add(p.head_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(G - 1);
-        __syncthreads();
-        if (S.last) {
+        // one fixed workgroup gathers the logits granules and selects: no arrival ticket, no store drain and no
+        // reload of the logits row on the chain (the last 256 -> 1 fan-in of the step)
+        if (w == SELW) {
             int tok = -1;
             SelectSpec sp = p.sel;
             if (MODE == 1) sp.step = pass - 1;
             if (p.prof && t == 0) p.prof[((size_t)w * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection start
-            if (sp.mode != SEL_NONE) tok = select_token<true>(sp, p.logits, 0, S.sel);
+            if (sp.mode != SEL_NONE) {
+                constexpr int VPT = MODE == 0 ? VOC / G : 2048 / G;
+                uint32_t u[VPT];
+                g_wait<VPT>(p.glog + t * VPT, TAG(hph), u, c);
+                float v[SEL_VPT_MAX];
+#pragma unroll
+                for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = e < VPT ? __uint_as_float(u[e]) : -INFINITY;
+                tok = select_token_regs<MODE == 0 ? SEL_CB0 : SEL_CP>(sp, v, 0, S.sel);
+            }
             if (p.prof && t == 0) p.prof[((size_t)0 * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection end (row 0)
             if (t == 0) {
                 if (tok >= 0) select_commit(sp, 0, tok);
-                __hip_atomic_store(p.head_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (pass + 1 == npass) __hip_atomic_store(p.seq, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (MODE == 1 && pass + 1 < npass) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // ticket reset lands before the token
-                    g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
-                }
+                if (MODE == 1 && pass + 1 < npass) g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
             }
         }
     }
@@ -651,7 +657,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 }
 
 struct StateLayout {
-    size_t gx, gx2, gqkv, gattn, gh, part, gpart, gtok, ctr, total;
+    size_t gx, gx2, gqkv, gattn, gh, part, gpart, gtok, glog, ctr, total;
     StateLayout() {
         size_t o = 0;
         auto take = [&](size_t b) { const size_t r = o; o += (b + 255) & ~(size_t)255; return r; };
@@ -663,6 +669,7 @@ struct StateLayout {
         part = take((size_t)NKV * MAXSPLIT * R * (D + 2) * 4);
         gpart = take((size_t)NKV * MAXSPLIT * PSLOT * 8);
         gtok = take(16 * 8);
+        glog = take(VOC * 8);
         ctr = take(64 * 4);
         total = o;
     }
@@ -715,6 +722,7 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.part = reinterpret_cast<float *>(base + L.part);
     p.gpart = reinterpret_cast<uint64_t *>(base + L.gpart);
     p.gtok = reinterpret_cast<uint64_t *>(base + L.gtok);
+    p.glog = reinterpret_cast<uint64_t *>(base + L.glog);
     unsigned *ctr = reinterpret_cast<unsigned *>(base + L.ctr);
     p.seq = ctr;               // [0]
     p.head_ticket = ctr + 16;  // own 64-B line
