@@ -13,6 +13,8 @@
  *   q3t_generate          TTSTransformer::generate (src/tts_transformer.h:233-241, .cpp:2342-2574)
  *   q3t_generate_stream   the same with frame_callback_t on_frames / callback_interval (src/tts_transformer.h:224,
  *                         .cpp:2517-2523, 2563-2570; caller qwen3_tts.cpp:437-463: the TRT streaming vocoder)
+ *   q3t_generate_queue    continuous batching over the same path (no reference counterpart: SURVEY §7 step 9,
+ *                         the serving extension of TTSTransformer::generate to more utterances than slots)
  *   q3t_comm_unique_id,   SURVEY §8(e) multi-GPU start-up (no reference counterpart: the reference is one process
  *   q3t_ctx_create_shared on one Jetson): RCCL broadcast of rank 0's packed weight blobs over xGMI
  *   q3t_ctx_create_replica, q3t_comm_allreduce_max
@@ -93,6 +95,14 @@ typedef int (*q3t_frame_cb)(void *user, int32_t utterance, const int32_t *codes,
 int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                         const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
                         q3t_frame_cb on_frames, void *user, int32_t interval);
+/* continuous batching: n_utt utterances (any number; codes [n_utt][max_len][16], n_frames [n_utt]) through
+ * min(max_slots, n_utt) slots with at most max_active (<= 0: all slots) in flight.  When an utterance ends (EOS or
+ * max_len) its slot is refilled with the next one between two frames (prefill of the newcomer on that slot only).
+ * Sampling is keyed by the utterance's index in the call, so an utterance's codes do not depend on its slot, on when
+ * it was admitted or on its neighbours.  A newcomer's prefill runs on the single-slot kernels. */
+int q3t_generate_queue(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
+                       const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
+                       int32_t max_active);
 /* tuning knob (process-wide): batches of >= min_batch slots run the projections on the matrix cores (MFMA GEMM,
  * gemm_mfma.hip) instead of the weight-streaming GEMV; 0 disables the matrix-core path.  Default 4 (env
  * Q3T_MFMA_MIN_B).  Applies to graphs captured afterwards (create contexts after changing it). */

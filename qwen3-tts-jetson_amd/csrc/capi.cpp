@@ -176,6 +176,17 @@ int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, c
     GUARD_END
 }
 
+int q3t_generate_queue(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
+                       const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
+                       int32_t max_active) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
+    if (n_utt < 0 || (n_utt > 0 && (!tokens || !n_tokens || !codes || !n_frames))) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.generate_queue(n_utt, tokens, n_tokens, speaker, to_gp(p), codes, n_frames, max_active) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
 int q3t_synchronize(q3t_ctx *ctx) {
     GUARD_BEGIN
     CHECK_CTX(ctx);

@@ -52,6 +52,7 @@ Engine::~Engine() {
     if (device_ >= 0) hipSetDevice(device_);
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_slot_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     voc_.reset();
     for (void *p : allocs_) hipFree(p);
@@ -323,6 +324,7 @@ bool Engine::alloc_state() {
     force_ = dalloc<int>(S);
     trailing_len_ = dalloc<int>(S);
     cp_pos_ = dalloc<int>((size_t)16 * S);
+    slot_pos_ = dalloc<int>(S);
     seen_ = dalloc<uint8_t>((size_t)S * c_.codec_vocab);
     utt_ = dalloc<uint64_t>(S);
     trailing_ = dalloc<float>((size_t)S * max_trailing_ * H);
@@ -392,7 +394,8 @@ bool Engine::persist_recover() {
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
-    g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
+    for (auto &kv : g_slot_) hipGraphExecDestroy(kv.second);
+    g_talker_.clear(); g_frame_.clear(); g_cp_.clear(); g_slot_.clear();
     persist_ = persist_cp_ = false;
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
     // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
@@ -745,7 +748,7 @@ bool Engine::enqueue_frame(int S, hipStream_t s) {
     if (!fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, s)) return false;
     if (!enqueue_cp_frame(S, s)) return false;
     if (!enqueue_talker(S, s, true, fused_select_)) return false;
-    return advance(pos_, frame_, S, s);
+    return advance(pos_, frame_, done_, S, s);
 }
 
 bool Engine::graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t)) {
@@ -1102,6 +1105,216 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     last_prefill_ms = ms1;
     last_frames_ms = ms2;
     release();
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------ continuous batching
+// the talker step of ONE slot (slot k of the batch buffers: its x / hidden / logits rows and its KV region, position
+// slot_pos_[k]) on the launch-per-op kernels; the prefill of an admitted utterance replays it token by token
+bool Engine::enqueue_slot_step(int k, hipStream_t s) {
+    const int H = c_.hidden;
+    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
+    const size_t kv_slot = (size_t)k * c_.n_kv * max_ctx_ * c_.head_dim;
+    const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
+    float *x = x_ + (size_t)k * H;
+    if (!decoder_stack(c_, L_, 1, x, qkv_, attn_, hmlp_, kc_ + kv_slot, vc_ + kv_slot, kv_layer, max_ctx_, max_splits,
+                       slot_pos_ + k, rope_, part_, ticket_, s))
+        return false;
+    GemvParams h;   // final RMSNorm (hidden side output) + codec head, as enqueue_talker
+    h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = 1;
+    h.pro = PRO_RMS; h.x = x; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_ + (size_t)k * H;
+    h.out_f32 = logits_ + (size_t)k * c_.codec_vocab; h.ldo = c_.codec_vocab;
+    return gemv(h, s);
+}
+
+// admit utterance `utt` into slot k between two frames: text projection, prefill / trailing / pad rows (the recipe
+// of generate_once for one slot), the slot's state, plen single-slot prefill steps and the CB0 selection of its first
+// frame.  state_h: pinned [8] ints of this slot (alive until the stream has passed these copies)
+bool Engine::admit_slot(int k, uint64_t utt, const int32_t *tok, int n, const float *spk, const GenParams &gp, int plen,
+                        int *state_h) {
+    const int H = c_.hidden, NCB = 16;
+    const int32_t *tk[1] = {tok};
+    std::vector<int> idx;
+    std::vector<SlotPlan> plan;
+    if (!plan_rows(c_, 1, tk, &n, max_trailing_, idx, plan)) return false;
+    Q3T_HIP(hipMemcpyAsync(proj_idx_, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_));
+    if (!enqueue_text_projection((int)idx.size(), stream_)) return false;
+    float *spk_dev = cp_in1_ + (size_t)k * H;
+    if (spk) Q3T_HIP(hipMemcpyAsync(spk_dev, spk, H * 4, hipMemcpyHostToDevice, stream_));
+    const SlotPlan &p = plan[0];
+    const float *P = proj_out_;
+    auto prow = [&](int i) { return RowTerm{P + (size_t)i * H, 0}; };
+    auto crow = [&](int id) { return RowTerm{codec_embd_ + (size_t)id * H, 1}; };
+    std::vector<RowTerm> cin;
+    if (gp.language_id < 0) cin = {crow(c_.nothink), crow(c_.think_bos), crow(c_.think_eos)};
+    else cin = {crow(c_.think), crow(c_.think_bos), crow(gp.language_id), crow(c_.think_eos)};
+    if (spk) cin.push_back(RowTerm{spk_dev, 0});
+    cin.push_back(crow(c_.codec_pad));
+    cin.push_back(crow(c_.codec_bos));
+    const int ol = (int)cin.size() - 1;
+    if (3 + ol + 1 != plen) { set_error("admit_slot: prefill length mismatch"); return false; }
+    std::vector<RowRecipe> rec;
+    float *out = prefill_ + (size_t)k * 10 * H;
+    for (int r = 0; r < 3; ++r) rec.push_back(RowRecipe{out + (size_t)r * H, {prow(3 + r), {nullptr, 0}, {nullptr, 0}}});
+    for (int t = 0; t < ol; ++t) rec.push_back(RowRecipe{out + (size_t)(3 + t) * H, {t == ol - 1 ? prow(0) : prow(2), cin[t], {nullptr, 0}}});
+    rec.push_back(RowRecipe{out + (size_t)(plen - 1) * H, {prow(6), cin.back(), {nullptr, 0}}});
+    float *tr = trailing_ + (size_t)k * max_trailing_ * H;
+    for (int i = 0; i < p.tcount; ++i) rec.push_back(RowRecipe{tr + (size_t)i * H, {prow(7 + i), {nullptr, 0}, {nullptr, 0}}});
+    rec.push_back(RowRecipe{tr + (size_t)p.tcount * H, {prow(1), {nullptr, 0}, {nullptr, 0}}});
+    rec.push_back(RowRecipe{tts_pad_ + (size_t)k * H, {prow(2), {nullptr, 0}, {nullptr, 0}}});
+    if ((int)rec.size() > recipe_cap_) { set_error("recipe overflow"); return false; }
+    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
+    if (!rows_recipe(recipe_, (int)rec.size(), H, stream_)) return false;
+    // slot state (pinned staging: [0] trailing_len [1] n_tokens [2] force [3] done [4] pos [5] frame [6..7] utt)
+    state_h[0] = p.tcount + 1; state_h[1] = p.n; state_h[2] = gp.force_frames; state_h[3] = -1;
+    state_h[4] = plen; state_h[5] = 0;
+    std::memcpy(state_h + 6, &utt, 8);
+    Q3T_HIP(hipMemcpyAsync(trailing_len_ + k, state_h + 0, 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(n_tokens_ + k, state_h + 1, 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(force_ + k, state_h + 2, 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(utt_ + k, state_h + 6, 8, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemsetAsync(seen_ + (size_t)k * c_.codec_vocab, 0, c_.codec_vocab, stream_));
+    Q3T_HIP(hipMemsetAsync(codes_ + (size_t)k * codes_max_len_ * NCB, 0, (size_t)codes_max_len_ * NCB * 4, stream_));
+    // prefill: plen single-slot steps on slot k (its graph captured once per slot)
+    if (!g_slot_.count(k)) {
+        hipGraph_t graph = nullptr;
+        Q3T_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+        const bool ok = enqueue_slot_step(k, stream_);
+        hipError_t e = hipStreamEndCapture(stream_, &graph);
+        if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
+        if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
+        hipGraphExec_t exec = nullptr;
+        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
+        g_slot_[k] = exec;
+    }
+    for (int t = 0; t < plen; ++t) {
+        Q3T_HIP(hipMemcpyAsync(x_ + (size_t)k * H, prefill_ + ((size_t)k * 10 + t) * H, H * 4, hipMemcpyDeviceToDevice, stream_));
+        Q3T_HIP(hipMemcpyAsync(slot_pos_ + k, cp_pos_ + (size_t)t * max_slots_, 4, hipMemcpyDeviceToDevice, stream_));
+        Q3T_HIP(hipGraphLaunch(g_slot_[k], stream_));
+    }
+    Q3T_HIP(hipMemcpyAsync(pos_ + k, state_h + 4, 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(frame_ + k, state_h + 5, 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(done_ + k, state_h + 3, 4, hipMemcpyHostToDevice, stream_));
+    // CB0 of the slot's first frame from its last prefill logits (the slot's rows of every per-slot array)
+    SelectSpec sp = select_spec(SEL_CB0, gp_, 0, 0);
+    sp.tokens += (size_t)k * 16; sp.codes += (size_t)k * codes_max_len_ * NCB; sp.frame += k; sp.done += k; sp.utt += k;
+    sp.seen += (size_t)k * c_.codec_vocab; sp.n_tokens += k; sp.force_frames += k;
+    if (sp.ticket) sp.ticket += k;
+    return select_tokens(sp, logits_ + (size_t)k * c_.codec_vocab, 1, stream_);
+}
+
+bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                            const GenParams &gp, int32_t *codes, int *n_frames, int max_active) {
+    if (n_utt <= 0) return true;
+    const int S = std::min(max_slots_, n_utt), NCB = 16;
+    if (max_active <= 0 || max_active > S) max_active = S;
+    for (int u = 0; u < n_utt; ++u) n_frames[u] = 0;
+    if (gp.max_len <= 0) return true;
+    if (gp.language_id >= c_.codec_vocab) { set_error("language id out of range"); return false; }
+    const bool has_spk = speaker && speaker[0];
+    for (int u = 0; u < n_utt; ++u)
+        if ((speaker && speaker[u]) != has_spk) { set_error("speaker embedding must be given for all or none of the utterances"); return false; }
+    {   // validate every prompt before anything runs
+        std::vector<int> idx;
+        std::vector<SlotPlan> plan;
+        if (!plan_rows(c_, n_utt, tokens, n_tokens, max_trailing_, idx, plan)) return false;
+    }
+    const int n_pre = gp.language_id < 0 ? 3 : 4;
+    const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
+    if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
+    if (gp.max_len > codes_max_len_) { set_error("max_len exceeds the code buffer"); return false; }
+    auto lk = persist_lock(persist_, device_);
+    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty && gp.seed == gp_.seed)) {
+        for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
+        g_frame_.clear();
+    }
+    gp_ = gp;
+    // device arena for the finished utterances' codes (copied to the caller once at the end)
+    int32_t *out_dev = nullptr;
+    Q3T_HIP(hipMalloc(&out_dev, (size_t)n_utt * gp.max_len * NCB * 4));
+    int *pin = nullptr;   // [S][8] admission staging + [S] done flags + one constant 0 (parking a slot)
+    if (hipHostMalloc(&pin, ((size_t)S * 9 + 1) * 4, hipHostMallocDefault) != hipSuccess) {
+        hipFree(out_dev);
+        set_error("hipHostMalloc failed");
+        return false;
+    }
+    int *done_h = pin + (size_t)S * 8, *park = pin + (size_t)S * 9;
+    *park = 0;
+    hipEvent_t ev = nullptr;
+    auto cleanup = [&]() {
+        if (ev) hipEventDestroy(ev);
+        hipFree(out_dev);
+        hipHostFree(pin);
+    };
+    Q3T_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // every slot starts idle: done = 0 (no selection, no advance), position / frame 0, valid code ids for the gathers
+    // an idle slot still runs through, no trailing text
+    Q3T_HIP(hipMemsetAsync(done_, 0, S * 4, stream_));
+    Q3T_HIP(hipMemsetAsync(pos_, 0, S * 4, stream_));
+    Q3T_HIP(hipMemsetAsync(frame_, 0, S * 4, stream_));
+    Q3T_HIP(hipMemsetAsync(tokens_, 0, (size_t)S * 16 * 4, stream_));
+    Q3T_HIP(hipMemsetAsync(trailing_len_, 0, S * 4, stream_));
+    std::vector<int> slot_utt(S, -1), started(S, 0);
+    int next = 0, f = 0, n_fin = 0;
+    auto admit = [&](int k) -> bool {
+        const int u = next++;
+        if (!admit_slot(k, (uint64_t)u, tokens[u], n_tokens[u], has_spk ? speaker[u] : nullptr, gp, plen, pin + (size_t)k * 8))
+            return false;
+        slot_utt[k] = u;
+        started[k] = f;
+        return true;
+    };
+    for (int k = 0; k < max_active && next < n_utt; ++k)
+        if (!admit(k)) { cleanup(); return false; }
+    if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) { cleanup(); return false; }
+    // frame loop, one frame in flight: frame f is launched before frame f-1's done flags are read
+    bool pending = false;
+    while (n_fin < n_utt) {
+        Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
+        ++f;
+        if (pending) {
+            Q3T_HIP(hipEventSynchronize(ev));
+            // done_h is frame f-1's: a slot done there (or at max_len) ran at most this one extra, harmless frame
+            bool refill = false;
+            for (int k = 0; k < S; ++k) {
+                if (slot_utt[k] < 0) continue;
+                const int ran = f - 1 - started[k];   // frames completed by the read-back
+                const int d = done_h[k];
+                if (d < 0 && ran < gp.max_len) continue;
+                const int u = slot_utt[k];
+                n_frames[u] = d >= 0 ? std::min(d, gp.max_len) : gp.max_len;
+                Q3T_HIP(hipMemcpyAsync(out_dev + (size_t)u * gp.max_len * NCB, codes_ + (size_t)k * codes_max_len_ * NCB,
+                                       (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToDevice, stream_));
+                slot_utt[k] = -1;
+                ++n_fin;
+                if (d < 0)   // stopped at max_len: park the slot (no selection, no advance)
+                    Q3T_HIP(hipMemcpyAsync(done_ + k, park, 4, hipMemcpyHostToDevice, stream_));
+                refill = true;
+            }
+            if (refill) {
+                int active = 0;
+                for (int k = 0; k < S; ++k) active += slot_utt[k] >= 0;
+                for (int k = 0; k < S && next < n_utt && active < max_active; ++k)
+                    if (slot_utt[k] < 0) {
+                        if (!admit(k)) { cleanup(); return false; }
+                        ++active;
+                    }
+            }
+        }
+        Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
+        Q3T_HIP(hipEventRecord(ev, stream_));
+        pending = true;
+        if (f > (n_utt + 1) * (gp.max_len + 2)) { cleanup(); set_error("generate_queue: no progress"); return false; }
+    }
+    for (int u = 0; u < n_utt; ++u)
+        Q3T_HIP(hipMemcpyAsync(codes + (size_t)u * gp.max_len * NCB, out_dev + (size_t)u * gp.max_len * NCB,
+                               (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    const bool fault = persist_error();
+    cleanup();
+    if (fault) { set_error("persistent kernel: an in-launch hand-off timed out"); return false; }
     return true;
 }
 

@@ -94,6 +94,15 @@ public:
     bool generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
                   const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames = nullptr,
                   void *user = nullptr, int interval = 40);
+    // continuous batching: n_utt utterances (any number) through min(max_slots, n_utt) slots, at
+    // most max_active of them at a time.  A slot whose utterance ended (EOS or max_len) is refilled with the next
+    // queued utterance between two frames: its text rows are projected, its prefill rows assembled and replayed
+    // token by token through a single-slot talker step on that slot's KV region while the other slots wait, and its
+    // state (position, frame, EOS, repetition set, codes) is reset.  Sampling streams are keyed by the utterance's
+    // index in the call (utt id), so an utterance's codes do not depend on its slot, its admission frame or the
+    // other utterances in flight (the S-slot decode step never mixes tokens).
+    bool generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                        const GenParams &gp, int32_t *codes, int *n_frames, int max_active);
     // fill this context's weight arenas (laid out with recv_weights) from another context's, device to device
     bool copy_weights_from(Engine &src);
 
@@ -146,6 +155,12 @@ private:
     bool enqueue_text_projection(int n_rows, hipStream_t s);
     bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));
     bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
+    // continuous batching: the single-slot prefill step of slot cur_slot_ (graph per slot) and slot admission
+    bool enqueue_slot_step(int slot, hipStream_t s);
+    bool admit_slot(int slot, uint64_t utt, const int32_t *tok, int n, const float *spk, const GenParams &gp, int plen,
+                    int *state_h);
+    std::map<int, hipGraphExec_t> g_slot_;
+    int *slot_pos_ = nullptr;      // [max_slots] position of the single-slot prefill step
 
     Config c_;
     std::string tts_path_, tok_path_;

@@ -143,7 +143,7 @@ constexpr int ATTN_MAX_SPLITS = 160;   // n_ctx <= 10240
 
 
 // pos[s]++, frame[s]++
-bool advance(int *pos, int *frame, int S, hipStream_t s);
+bool advance(int *pos, int *frame, const int *done, int S, hipStream_t s);   // done: slots with done >= 0 stay (may be null)
 
 // *out = t[0] + t[1] + t[2] (f32 rows or f16 table rows; null terms skipped); recipe built on the host
 struct RowTerm { const void *ptr; int is_f16; };

@@ -65,12 +65,14 @@ bool gather_sum(const GatherSum &gs, int nt, int S, int K, float *out, int ldo, 
     return true;
 }
 
-__global__ void k_advance(int *pos, int *frame, int S) {
+// a slot whose utterance ended (done >= 0) stays where it is: its position never runs past the context reserved
+// for it, however long the other slots (or a continuous-batching queue) keep the frame loop going
+__global__ void k_advance(int *pos, int *frame, const int *done, int S) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < S) { pos[s] += 1; frame[s] += 1; }
+    if (s < S && !(done && done[s] >= 0)) { pos[s] += 1; frame[s] += 1; }
 }
-bool advance(int *pos, int *frame, int S, hipStream_t s) {
-    hipLaunchKernelGGL(k_advance, dim3((S + 63) / 64), dim3(64), 0, s, pos, frame, S);
+bool advance(int *pos, int *frame, const int *done, int S, hipStream_t s) {
+    hipLaunchKernelGGL(k_advance, dim3((S + 63) / 64), dim3(64), 0, s, pos, frame, done, S);
     Q3T_HIP(hipGetLastError());
     return true;
 }

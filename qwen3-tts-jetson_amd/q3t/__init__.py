@@ -50,6 +50,8 @@ _lib.q3t_ctx_destroy.argtypes = [_P]
 _lib.q3t_get_config.argtypes = [_P, C.POINTER(Config)]
 _lib.q3t_generate.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
                               C.POINTER(GenParams), _ip, _ip]
+_lib.q3t_generate_queue.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
+                                    C.POINTER(GenParams), _ip, _ip, C.c_int32]
 FRAME_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_int32)
 _lib.q3t_generate_stream.argtypes = [_P, _I, C.POINTER(C.POINTER(C.c_int32)), _ip, C.POINTER(C.POINTER(C.c_float)),
                                      C.POINTER(GenParams), _ip, _ip, FRAME_CB, C.c_void_p, C.c_int32]
@@ -89,7 +91,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
-           "q3t_generate", "q3t_generate_stream", "q3t_comm_unique_id", "q3t_ctx_create_shared",
+           "q3t_generate", "q3t_generate_stream", "q3t_generate_queue", "q3t_comm_unique_id", "q3t_ctx_create_shared",
            "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
@@ -245,6 +247,26 @@ class Engine:
         codes = np.zeros((n, p.max_len, 16), np.int32)
         nf = np.zeros(n, np.int32)
         _check(_lib.q3t_generate(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf))
+        del keep
+        return [codes[i, :nf[i]].copy() for i in range(n)]
+
+    def generate_queue(self, prompts, speakers=None, max_active=0, **params):
+        """continuous batching (q3t_generate_queue): any number of prompts through the context's slots, a finished
+        utterance's slot refilled with the next prompt.  Returns list of [n_frames][16] int32 arrays."""
+        p = default_params(**params)
+        n = len(prompts)
+        toks = [np.ascontiguousarray(t, np.int32) for t in prompts]
+        tarr = (C.POINTER(C.c_int32) * n)(*[t.ctypes.data_as(C.POINTER(C.c_int32)) for t in toks])
+        ntok = np.array([len(t) for t in toks], np.int32)
+        sarr = None
+        keep = []
+        if speakers is not None:
+            sp = [np.ascontiguousarray(s, np.float32) for s in speakers]
+            keep = sp
+            sarr = (C.POINTER(C.c_float) * n)(*[s.ctypes.data_as(C.POINTER(C.c_float)) for s in sp])
+        codes = np.zeros((n, p.max_len, 16), np.int32)
+        nf = np.zeros(n, np.int32)
+        _check(_lib.q3t_generate_queue(self.h, n, tarr, ntok, sarr, C.byref(p), codes, nf, int(max_active)))
         del keep
         return [codes[i, :nf[i]].copy() for i in range(n)]
 

@@ -1,0 +1,85 @@
+"""Continuous batching (q3t_generate_queue).
+
+More utterances than slots go through one context: a slot whose utterance ended (EOS or max_len) is refilled with
+the next queued utterance between two frames (its prefill runs on that slot alone while the other slots wait).
+
+  invariance   the same queue with 1, 3 and all slots in flight gives every utterance bit-identical codes and
+               lengths: the S-slot decode step never mixes tokens, sampling is keyed by the utterance's index in the
+               call, and a parked / refilled slot leaves its neighbours alone
+  oracle       utterances admitted mid-run (into a slot that had already held two others) are teacher-forced
+               against the CPU oracle with their own utterance id, including their EOS frame
+Prompts of 5..12 text tokens put the EOS ramp (expected = max(20, 4 n_tokens) frames) inside max_len, so the queue
+sees both EOS stops and max_len stops.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from q3t_testutil import REPO, check_decisions, prompt, synth_dir
+
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+pytestmark = pytest.mark.gpu
+MM_MAX_OFF = 0.06   # near-tie decision fraction on the matrix-core path (test_gpu_mfma.py header)
+
+
+@pytest.fixture(scope="module")
+def full():
+    tts, tok = synth_dir("full")
+    orc = Oracle(tts, tok)
+    yield tts, tok, orc
+    orc.close()
+
+
+def _prompts(n, seed):
+    base = prompt("full")
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(5, 13))
+        tail = [(t + 13 * i) % 900 + 20 for t in base[4:]]
+        out.append(base[:4] + tail[:k - 4])
+    return out
+
+
+@pytest.mark.parametrize("slots,n_utt", [(4, 10), (16, 36)])
+def test_queue_is_slot_and_admission_invariant(full, slots, n_utt):
+    import q3t
+    tts, tok, orc = full
+    nf = 48
+    eng = q3t.Engine(tts, None, device=0, max_slots=slots, max_ctx=nf + 40)
+    try:
+        H = eng.cfg["hidden"]
+        prompts = _prompts(n_utt, slots)
+        spk = [np.zeros(H, np.float32)] * n_utt
+        kw = dict(speakers=spk, max_len=nf, temperature=0.9, top_k=50, seed=123)
+        runs = {a: eng.generate_queue(prompts, max_active=a, **kw) for a in (slots, 3, 1)}
+        lens = [len(c) for c in runs[slots]]
+        assert 0 < min(lens) and max(lens) <= nf
+        assert any(n < nf for n in lens), "no utterance stopped at EOS: the refill path after EOS was not exercised"
+        for a in (3, 1):
+            for u in range(n_utt):
+                assert np.array_equal(runs[a][u], runs[slots][u]), (a, u, len(runs[a][u]), len(runs[slots][u]))
+        print(f"{slots} slots, {n_utt} utterances: lengths {lens}")
+    finally:
+        eng.close()
+
+
+def test_queue_admitted_utterances_match_oracle(full):
+    import q3t
+    tts, tok, orc = full
+    nf, slots, n_utt = 40, 4, 12
+    eng = q3t.Engine(tts, None, device=0, max_slots=slots, max_ctx=nf + 40)
+    try:
+        H = eng.cfg["hidden"]
+        prompts = _prompts(n_utt, 7)
+        spk = [np.zeros(H, np.float32)] * n_utt
+        outs = eng.generate_queue(prompts, speakers=spk, max_len=nf, temperature=0.9, top_k=50, seed=5)
+        for u in (0, slots, n_utt - 1):   # first wave, first refill, last admission
+            n_off, n_dec, worst = check_decisions(orc, prompts[u], spk[u], outs[u], max_len=nf, temperature=0.9,
+                                                  top_k=50, seed=5, utt=u, max_off_frac=MM_MAX_OFF)
+            print(f"utterance {u}: {len(outs[u])} frames, {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
+    finally:
+        eng.close()
