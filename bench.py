@@ -184,6 +184,9 @@ def main():
     ap.add_argument("--batched", type=int, default=64,
                     help="secondary measurement: this many concurrent utterances per GPU (BASELINE configs[2] at N=1, "
                          "configs[3] at N>1: weak scaling, value over all ranks); 0 = off")
+    ap.add_argument("--serve", type=int, default=128,
+                    help="serving measurement (N=1): this many utterances with natural EOS (prompt lengths 10..120 "
+                         "tokens) through `batched` slots, lock-step batches vs continuous batching; 0 = off")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -301,6 +304,41 @@ def main():
                 "vocoder_roofline": voc_roofline(stats["vocoder_ms"], batched, 1),
                 "mfma_pmc": pmc_file("talker_b64"), "mfma_pmc_cp": pmc_file("cp_b64")}
 
+    # ---- serving: utterances of different lengths, lock-step batches (every batch runs until its
+    # longest utterance ends) vs continuous batching (a finished slot is refilled between frames); codes only
+    sres = None
+    if args.serve > 0 and batched > 0 and world == 1:
+        rng = np.random.default_rng(2024)
+        sp_prompts = []
+        for i in range(args.serve):
+            n = int(rng.integers(10, 121))
+            sp_prompts.append(prompt[:4] + [(prompt[4 + j % (len(prompt) - 4)] + 13 * i + 7 * j) % 900 + 20
+                                            for j in range(n - 4)])
+        sp_spk = [np.zeros(H, np.float32)] * args.serve
+        kw = dict(max_len=args.frames, temperature=0.9, top_k=50, repetition_penalty=1.05, seed=4242)
+        eng.generate_queue(sp_prompts[:2 * batched], speakers=sp_spk[:2 * batched], max_active=batched,
+                           **dict(kw, max_len=2))   # warm-up: every slot's single-slot prefill graph
+        eng.synchronize()
+        t0 = time.perf_counter()
+        lock = []
+        for b0 in range(0, args.serve, batched):
+            lock += eng.generate(sp_prompts[b0:b0 + batched], speakers=sp_spk[b0:b0 + batched], **kw)
+        eng.synchronize()
+        t_lock = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        queue = eng.generate_queue(sp_prompts, speakers=sp_spk, max_active=batched, **kw)
+        eng.synchronize()
+        t_queue = time.perf_counter() - t0
+        f_lock, f_queue = sum(len(c) for c in lock), sum(len(c) for c in queue)
+        sres = {"config": f"{args.serve} utterances (prompts of 10..120 tokens, natural EOS, max {args.frames} frames) "
+                          f"through {batched} slots, codes only (no vocoder), temp 0.9 top-k 50",
+                "lockstep": {"frames": f_lock, "s": round(t_lock, 3), "value": round(f_lock / t_lock, 1),
+                             "unit": "frames/s"},
+                "continuous": {"frames": f_queue, "s": round(t_queue, 3), "value": round(f_queue / t_queue, 1),
+                               "unit": "frames/s"},
+                "lengths": {"min": min(len(c) for c in queue), "mean": round(f_queue / args.serve, 1),
+                            "max": max(len(c) for c in queue)}}
+
     if rank == 0:
         res = {
             "metric": "audio frames/sec (12 Hz frames) + RTF, Qwen3-TTS-0.6B batch=1 and batch=8xN",
@@ -329,6 +367,9 @@ def main():
                             "(Infinity-Cache resident), algorithmic bytes / time"},
         }
         res["batched"] = bres
+        res["serving"] = sres
+        vr = res["vocoder_roofline"]
+        res["mfma_frac"] = vr["frac"] if vr else None   # the MFMA-bound kernel's fraction (vocoder convs, §8(d))
         if args.cpu_baseline == "on" and world == 1:
             try:
                 res["cpu_baseline"] = cpu_baseline(tts, tok if voc_mode is not None else None, prompt, args.frames,

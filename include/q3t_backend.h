@@ -99,7 +99,8 @@ int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, c
  * min(max_slots, n_utt) slots with at most max_active (<= 0: all slots) in flight.  When an utterance ends (EOS or
  * max_len) its slot is refilled with the next one between two frames (prefill of the newcomer on that slot only).
  * Sampling is keyed by the utterance's index in the call, so an utterance's codes do not depend on its slot, on when
- * it was admitted or on its neighbours.  A newcomer's prefill runs on the single-slot kernels. */
+ * it was admitted or on its neighbours.  A newcomer's prefill runs on its own stream, overlapping the other slots'
+ * decoding, with the batch's kernels (>= 4 slots: the first wave's codes equal q3t_generate's). */
 int q3t_generate_queue(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                        const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,
                        int32_t max_active);

@@ -52,11 +52,12 @@ Engine::~Engine() {
     if (device_ >= 0) hipSetDevice(device_);
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
-    for (auto &kv : g_slot_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_stage_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     voc_.reset();
     for (void *p : allocs_) hipFree(p);
     if (stream_) hipStreamDestroy(stream_);
+    if (astream_) hipStreamDestroy(astream_);
 }
 
 template <class T>
@@ -324,7 +325,6 @@ bool Engine::alloc_state() {
     force_ = dalloc<int>(S);
     trailing_len_ = dalloc<int>(S);
     cp_pos_ = dalloc<int>((size_t)16 * S);
-    slot_pos_ = dalloc<int>(S);
     seen_ = dalloc<uint8_t>((size_t)S * c_.codec_vocab);
     utt_ = dalloc<uint64_t>(S);
     trailing_ = dalloc<float>((size_t)S * max_trailing_ * H);
@@ -394,8 +394,8 @@ bool Engine::persist_recover() {
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
-    for (auto &kv : g_slot_) hipGraphExecDestroy(kv.second);
-    g_talker_.clear(); g_frame_.clear(); g_cp_.clear(); g_slot_.clear();
+    for (auto &kv : g_stage_) hipGraphExecDestroy(kv.second);
+    g_talker_.clear(); g_frame_.clear(); g_cp_.clear(); g_stage_.clear();
     persist_ = persist_cp_ = false;
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
     // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
@@ -484,7 +484,11 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
                              unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
-                             float *final_side) {
+                             float *final_side, int S_main = 0) {
+    // S_main: the batch whose kernel choices this stack reproduces (a continuous-batching admission runs ONE slot
+    // with the S_main-slot kernels, so its per-token arithmetic is the batch's)
+    if (S_main <= 0) S_main = S;
+    const bool force = S < gemm_mfma_min_batch();
     const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
     ResidNorm rn;
     rn.S = S; rn.H = H; rn.eps = c.eps; rn.x = x; rn.xn = xn;
@@ -501,32 +505,32 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         GemvParams g;
         g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
         g.pro = PRO_F16; g.x = xn; g.ldx = H;
-        g.out_f32 = qkv; g.ldo = QKV;
+        g.out_f32 = qkv; g.ldo = QKV; g.force_mm = force;
         if (!gemv(g, s)) return false;
         AttnParams a;
         a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
         a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
         a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
         a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
-        a.seqk = S >= 16 && !attn_split;   // enough (slot, kv head) pairs to fill the chip
+        a.seqk = S_main >= 16 && !attn_split;   // enough (slot, kv head) pairs to fill the chip
         a.part = part; a.ticket = ticket; a.out = attn;
         if (!attn_decode(a, s)) return false;
         GemvParams o;
         o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
         o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
-        o.parts = parts; o.ksplit = splitk_for(H, S, o.K);
+        o.parts = parts; o.ksplit = splitk_for(H, S_main, o.K); o.force_mm = force;
         if (!gemv(o, s)) return false;
         rn.parts = parts; rn.ksplit = o.ksplit; rn.nw = l.ffn_norm; rn.side = nullptr;
         if (!resid_norm(rn, s)) return false;
         GemvParams gu;
         gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
         gu.pro = PRO_F16; gu.x = xn; gu.ldx = H;
-        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter;
+        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter; gu.force_mm = force;
         if (!gemv(gu, s)) return false;
         GemvParams dn;
         dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;
         dn.pro = PRO_F16; dn.x = hmlp; dn.ldx = c.inter;
-        dn.parts = parts; dn.ksplit = splitk_for(H, S, dn.K);
+        dn.parts = parts; dn.ksplit = splitk_for(H, S_main, dn.K); dn.force_mm = force;
         if (!gemv(dn, s)) return false;
         const bool last = il + 1 == layers.size();
         if (last && !final_norm) break;   // code-predictor pass 0: only its K/V caches are read afterwards
@@ -775,16 +779,20 @@ bool Engine::set_slot_state(int S, const std::vector<int> &pos, const std::vecto
 
 // ------------------------------------------------------------------------------------------ prefill pieces
 bool Engine::enqueue_text_projection(int n_rows, hipStream_t s) {
+    return enqueue_text_projection(n_rows, s, proj_idx_, proj_h_, proj_out_);
+}
+
+bool Engine::enqueue_text_projection(int n_rows, hipStream_t s, const int *idx, uint16_t *hbuf, float *out) {
     // text_embd row gather -> fc1 + b -> SiLU -> fc2 + b   (tts_transformer.cpp:1050-1055)
     GemvParams a;
     a.W = fc1_; a.N = c_.text_dim; a.K = c_.text_dim; a.B = n_rows;
-    a.pro = PRO_F16; a.x = text_embd_; a.ldx = c_.text_dim; a.x_idx = proj_idx_;
-    a.bias = fc1_b_; a.act = ACT_SILU; a.out_f16 = proj_h_; a.ldo = c_.text_dim;
+    a.pro = PRO_F16; a.x = text_embd_; a.ldx = c_.text_dim; a.x_idx = idx;
+    a.bias = fc1_b_; a.act = ACT_SILU; a.out_f16 = hbuf; a.ldo = c_.text_dim;
     if (!gemv(a, s)) return false;
     GemvParams b;
     b.W = fc2_; b.N = c_.hidden; b.K = c_.text_dim; b.B = n_rows;
-    b.pro = PRO_F16; b.x = proj_h_; b.ldx = c_.text_dim;
-    b.bias = fc2_b_; b.out_f32 = proj_out_; b.ldo = c_.hidden;
+    b.pro = PRO_F16; b.x = hbuf; b.ldx = c_.text_dim;
+    b.bias = fc2_b_; b.out_f32 = out; b.ldo = c_.hidden;
     return gemv(b, s);
 }
 
@@ -1109,64 +1117,158 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
 }
 
 // ------------------------------------------------------------------------------------------ continuous batching
-// the talker step of ONE slot (slot k of the batch buffers: its x / hidden / logits rows and its KV region, position
-// slot_pos_[k]) on the launch-per-op kernels; the prefill of an admitted utterance replays it token by token
-bool Engine::enqueue_slot_step(int k, hipStream_t s) {
-    const int H = c_.hidden;
-    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
-    const size_t kv_slot = (size_t)k * c_.n_kv * max_ctx_ * c_.head_dim;
-    const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
-    float *x = x_ + (size_t)k * H;
-    if (!decoder_stack(c_, L_, 1, x, qkv_, attn_, hmlp_, kc_ + kv_slot, vc_ + kv_slot, kv_layer, max_ctx_, max_splits,
-                       slot_pos_ + k, rope_, part_, ticket_, s))
+// Admissions run on their own stream with private scratch, overlapping the frame loop of the other slots (at many
+// slots the decode step leaves most of the chip idle).  The slots freed since the last admission are admitted
+// together: their prompts are projected in one pass and prefilled as a batch of STAGING slots (private x / hidden /
+// logits rows and a 16-position staging KV cache), then k_kv_stage_copy moves the prefill's K/V rows [0, plen) into
+// the target slots.  A target slot is parked in the frame loop meanwhile (done >= 0: no selection, no advance, its
+// position >= plen): the frame graph still runs it, but writes only its own x / hidden / logits rows and the KV row
+// at its parked position, none of which the admission writes.  The slot joins the frame loop (activate_slot, main
+// stream, between two frames) once its admission batch has finished.  On the matrix-core path the staging batch runs
+// the running batch's kernels (S_main), whose per-token arithmetic does not depend on the other tokens: a slot's
+// prefill is what generate()'s batched prefill computes for it, whichever slots were admitted alongside.
+bool Engine::alloc_admission() {
+    if (ax_) return true;
+    const int S = max_slots_, H = c_.hidden, D = c_.head_dim;
+    const int QKV = (c_.n_heads + 2 * c_.n_kv) * D;
+    ax_ = dalloc<float>((size_t)S * H);
+    axn_ = dalloc<uint16_t>((size_t)S * H);
+    aparts_ = dalloc<float>((size_t)4 * S * H);
+    aqkv_ = dalloc<float>((size_t)S * QKV);
+    aattn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
+    ahmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
+    apart_ = dalloc<float>((size_t)S * c_.n_heads * (D + 2));
+    aticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
+    const size_t skv = (size_t)S * c_.n_kv * 16 * D;
+    akc_ = dalloc<uint16_t>(skv * c_.n_layers);
+    avc_ = dalloc<uint16_t>(skv * c_.n_layers);
+    aprefill_ = dalloc<float>((size_t)S * 10 * H);
+    ashid_ = dalloc<float>((size_t)S * H);
+    aslog_ = dalloc<float>((size_t)S * c_.codec_vocab);
+    ahidden_ = dalloc<float>((size_t)S * H);
+    alogits_ = dalloc<float>((size_t)S * c_.codec_vocab);
+    astage_pos_ = dalloc<int>(S);
+    atarget_ = dalloc<int>(S);
+    aproj_cap_ = S * (max_trailing_ + 16);
+    aproj_idx_ = dalloc<int>(aproj_cap_);
+    aproj_h_ = dalloc<uint16_t>((size_t)aproj_cap_ * c_.text_dim);
+    aproj_out_ = dalloc<float>((size_t)aproj_cap_ * H);
+    arecipe_ = dalloc<RowRecipe>(aproj_cap_);
+    if (!ax_ || !akc_ || !avc_ || !aticket_ || !alogits_ || !arecipe_ || !aproj_out_) {
+        set_error("device allocation failed");
         return false;
+    }
+    Q3T_HIP(hipMemset(aticket_, 0, (size_t)S * c_.n_kv * 4));
+    Q3T_HIP(hipStreamCreateWithFlags(&astream_, hipStreamNonBlocking));
+    return true;
+}
+
+// the talker step of staging slots 0..a-1 at position astage_pos_[j] (the prefill of an admission batch), with the
+// kernels of the running q_slots_-slot batch
+bool Engine::enqueue_stage_step(int a, hipStream_t s) {
+    const int H = c_.hidden;
+    const size_t kvl = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
     GemvParams h;   // final RMSNorm (hidden side output) + codec head, as enqueue_talker
-    h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = 1;
-    h.pro = PRO_RMS; h.x = x; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_ + (size_t)k * H;
-    h.out_f32 = logits_ + (size_t)k * c_.codec_vocab; h.ldo = c_.codec_vocab;
+    h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = a;
+    h.out_f32 = aslog_; h.ldo = c_.codec_vocab;
+    if (q_slots_ >= gemm_mfma_min_batch()) {
+        if (!decoder_stack_mm(c_, opt_.attn_split, L_, a, ax_, axn_, aparts_, aqkv_, aattn_, ahmlp_, akc_, avc_, kvl, 16, 1,
+                              astage_pos_, rope_, apart_, aticket_, s, nullptr, out_norm_, ashid_, q_slots_))
+            return false;
+        h.pro = PRO_F16; h.x = axn_; h.ldx = H; h.force_mm = true;
+        return gemv(h, s);
+    }
+    if (!decoder_stack(c_, L_, a, ax_, aqkv_, aattn_, ahmlp_, akc_, avc_, kvl, 16, 1, astage_pos_, rope_, apart_, aticket_, s))
+        return false;
+    h.pro = PRO_RMS; h.x = ax_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = ashid_;
     return gemv(h, s);
 }
 
-// admit utterance `utt` into slot k between two frames: text projection, prefill / trailing / pad rows (the recipe
-// of generate_once for one slot), the slot's state, plen single-slot prefill steps and the CB0 selection of its first
-// frame.  state_h: pinned [8] ints of this slot (alive until the stream has passed these copies)
-bool Engine::admit_slot(int k, uint64_t utt, const int32_t *tok, int n, const float *spk, const GenParams &gp, int plen,
-                        int *state_h) {
-    const int H = c_.hidden, NCB = 16;
-    const int32_t *tk[1] = {tok};
+// admission batch on stream `as`: utterances utt[j] into slots tgt[j] (text projection, prefill / trailing / pad
+// rows, plen staging steps, K/V rows into the target slots, hidden / logits rows per target slot).  tgt_h: pinned
+// copy of tgt (alive until the batch has run); trailing_len[j]: the slot's trailing-text length
+bool Engine::admit_batch(const std::vector<int> &tgt, const std::vector<int> &utt, const int32_t *const *tokens,
+                         const int *n_tokens, const float *const *speaker, const GenParams &gp, int plen, hipStream_t as,
+                         int *tgt_h, std::vector<int> &trailing_len) {
+    const int H = c_.hidden, a = (int)tgt.size();
+    std::vector<const int32_t *> tk(a);
+    std::vector<int> nt(a);
+    for (int j = 0; j < a; ++j) { tk[j] = tokens[utt[j]]; nt[j] = n_tokens[utt[j]]; }
     std::vector<int> idx;
     std::vector<SlotPlan> plan;
-    if (!plan_rows(c_, 1, tk, &n, max_trailing_, idx, plan)) return false;
-    Q3T_HIP(hipMemcpyAsync(proj_idx_, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_));
-    if (!enqueue_text_projection((int)idx.size(), stream_)) return false;
-    float *spk_dev = cp_in1_ + (size_t)k * H;
-    if (spk) Q3T_HIP(hipMemcpyAsync(spk_dev, spk, H * 4, hipMemcpyHostToDevice, stream_));
-    const SlotPlan &p = plan[0];
-    const float *P = proj_out_;
-    auto prow = [&](int i) { return RowTerm{P + (size_t)i * H, 0}; };
-    auto crow = [&](int id) { return RowTerm{codec_embd_ + (size_t)id * H, 1}; };
-    std::vector<RowTerm> cin;
-    if (gp.language_id < 0) cin = {crow(c_.nothink), crow(c_.think_bos), crow(c_.think_eos)};
-    else cin = {crow(c_.think), crow(c_.think_bos), crow(gp.language_id), crow(c_.think_eos)};
-    if (spk) cin.push_back(RowTerm{spk_dev, 0});
-    cin.push_back(crow(c_.codec_pad));
-    cin.push_back(crow(c_.codec_bos));
-    const int ol = (int)cin.size() - 1;
-    if (3 + ol + 1 != plen) { set_error("admit_slot: prefill length mismatch"); return false; }
+    if (!plan_rows(c_, a, tk.data(), nt.data(), max_trailing_, idx, plan)) return false;
+    if ((int)idx.size() > aproj_cap_) { set_error("too many text rows"); return false; }
+    Q3T_HIP(hipMemcpyAsync(aproj_idx_, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, as));
+    if (!enqueue_text_projection((int)idx.size(), as, aproj_idx_, aproj_h_, aproj_out_)) return false;
     std::vector<RowRecipe> rec;
-    float *out = prefill_ + (size_t)k * 10 * H;
-    for (int r = 0; r < 3; ++r) rec.push_back(RowRecipe{out + (size_t)r * H, {prow(3 + r), {nullptr, 0}, {nullptr, 0}}});
-    for (int t = 0; t < ol; ++t) rec.push_back(RowRecipe{out + (size_t)(3 + t) * H, {t == ol - 1 ? prow(0) : prow(2), cin[t], {nullptr, 0}}});
-    rec.push_back(RowRecipe{out + (size_t)(plen - 1) * H, {prow(6), cin.back(), {nullptr, 0}}});
-    float *tr = trailing_ + (size_t)k * max_trailing_ * H;
-    for (int i = 0; i < p.tcount; ++i) rec.push_back(RowRecipe{tr + (size_t)i * H, {prow(7 + i), {nullptr, 0}, {nullptr, 0}}});
-    rec.push_back(RowRecipe{tr + (size_t)p.tcount * H, {prow(1), {nullptr, 0}, {nullptr, 0}}});
-    rec.push_back(RowRecipe{tts_pad_ + (size_t)k * H, {prow(2), {nullptr, 0}, {nullptr, 0}}});
-    if ((int)rec.size() > recipe_cap_) { set_error("recipe overflow"); return false; }
-    Q3T_HIP(hipMemcpyAsync(recipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, stream_));
-    if (!rows_recipe(recipe_, (int)rec.size(), H, stream_)) return false;
-    // slot state (pinned staging: [0] trailing_len [1] n_tokens [2] force [3] done [4] pos [5] frame [6..7] utt)
-    state_h[0] = p.tcount + 1; state_h[1] = p.n; state_h[2] = gp.force_frames; state_h[3] = -1;
+    auto crow = [&](int id) { return RowTerm{codec_embd_ + (size_t)id * H, 1}; };
+    for (int j = 0; j < a; ++j) {
+        const int k = tgt[j];
+        const float *spk = speaker ? speaker[utt[j]] : nullptr;
+        float *spk_dev = cp_in1_ + (size_t)k * H;
+        if (spk) Q3T_HIP(hipMemcpyAsync(spk_dev, spk, H * 4, hipMemcpyHostToDevice, as));
+        const SlotPlan &p = plan[j];
+        const float *P = aproj_out_ + (size_t)p.rb * H;
+        auto prow = [&](int i) { return RowTerm{P + (size_t)i * H, 0}; };
+        std::vector<RowTerm> cin;
+        if (gp.language_id < 0) cin = {crow(c_.nothink), crow(c_.think_bos), crow(c_.think_eos)};
+        else cin = {crow(c_.think), crow(c_.think_bos), crow(gp.language_id), crow(c_.think_eos)};
+        if (spk) cin.push_back(RowTerm{spk_dev, 0});
+        cin.push_back(crow(c_.codec_pad));
+        cin.push_back(crow(c_.codec_bos));
+        const int ol = (int)cin.size() - 1;
+        if (3 + ol + 1 != plen) { set_error("admit_batch: prefill length mismatch"); return false; }
+        float *out = aprefill_ + (size_t)j * 10 * H;
+        for (int r = 0; r < 3; ++r) rec.push_back(RowRecipe{out + (size_t)r * H, {prow(3 + r), {nullptr, 0}, {nullptr, 0}}});
+        for (int t = 0; t < ol; ++t) rec.push_back(RowRecipe{out + (size_t)(3 + t) * H, {t == ol - 1 ? prow(0) : prow(2), cin[t], {nullptr, 0}}});
+        rec.push_back(RowRecipe{out + (size_t)(plen - 1) * H, {prow(6), cin.back(), {nullptr, 0}}});
+        float *tr = trailing_ + (size_t)k * max_trailing_ * H;
+        for (int i = 0; i < p.tcount; ++i) rec.push_back(RowRecipe{tr + (size_t)i * H, {prow(7 + i), {nullptr, 0}, {nullptr, 0}}});
+        rec.push_back(RowRecipe{tr + (size_t)p.tcount * H, {prow(1), {nullptr, 0}, {nullptr, 0}}});
+        rec.push_back(RowRecipe{tts_pad_ + (size_t)k * H, {prow(2), {nullptr, 0}, {nullptr, 0}}});
+        trailing_len[j] = p.tcount + 1;
+    }
+    if ((int)rec.size() > aproj_cap_) { set_error("recipe overflow"); return false; }
+    Q3T_HIP(hipMemcpyAsync(arecipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, as));
+    if (!rows_recipe(arecipe_, (int)rec.size(), H, as)) return false;
+    const int gkey = q_slots_ * 4096 + a;
+    if (!g_stage_.count(gkey)) {   // the staging step for (batch size, admission size), captured once
+        hipGraph_t graph = nullptr;
+        Q3T_HIP(hipStreamBeginCapture(as, hipStreamCaptureModeThreadLocal));
+        const bool ok = enqueue_stage_step(a, as);
+        hipError_t e = hipStreamEndCapture(as, &graph);
+        if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
+        if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
+        hipGraphExec_t exec = nullptr;
+        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
+        g_stage_[gkey] = exec;
+    }
+    for (int t = 0; t < plen; ++t) {
+        Q3T_HIP(hipMemcpy2DAsync(ax_, H * 4, aprefill_ + (size_t)t * H, (size_t)10 * H * 4, H * 4, a, hipMemcpyDeviceToDevice, as));
+        Q3T_HIP(hipMemcpyAsync(astage_pos_, cp_pos_ + (size_t)t * max_slots_, a * 4, hipMemcpyDeviceToDevice, as));
+        Q3T_HIP(hipGraphLaunch(g_stage_[gkey], as));
+    }
+    for (int j = 0; j < a; ++j) tgt_h[j] = tgt[j];
+    Q3T_HIP(hipMemcpyAsync(atarget_, tgt_h, a * 4, hipMemcpyHostToDevice, as));
+    const size_t skvl = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim, kvl = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
+    if (!kv_stage_copy(akc_, avc_, kc_, vc_, atarget_, a, c_.n_layers, c_.n_kv, plen, c_.head_dim, skvl, kvl, 16, max_ctx_, as))
+        return false;
+    for (int j = 0; j < a; ++j) {
+        Q3T_HIP(hipMemcpyAsync(ahidden_ + (size_t)tgt[j] * H, ashid_ + (size_t)j * H, H * 4, hipMemcpyDeviceToDevice, as));
+        Q3T_HIP(hipMemcpyAsync(alogits_ + (size_t)tgt[j] * c_.codec_vocab, aslog_ + (size_t)j * c_.codec_vocab,
+                               (size_t)c_.codec_vocab * 4, hipMemcpyDeviceToDevice, as));
+    }
+    return true;
+}
+
+// slot k joins the frame loop (main stream, between two frames, after its admission batch): per-slot state, the
+// last prefill step's hidden state, and the CB0 of its first frame selected from the last prefill logits.
+// state_h: pinned [8]
+bool Engine::activate_slot(int k, uint64_t utt, int trailing_len, int n_tok, const GenParams &gp, int plen, int *state_h) {
+    const int H = c_.hidden, NCB = 16;
+    state_h[0] = trailing_len; state_h[1] = n_tok; state_h[2] = gp.force_frames; state_h[3] = -1;
     state_h[4] = plen; state_h[5] = 0;
     std::memcpy(state_h + 6, &utt, 8);
     Q3T_HIP(hipMemcpyAsync(trailing_len_ + k, state_h + 0, 4, hipMemcpyHostToDevice, stream_));
@@ -1175,34 +1277,15 @@ bool Engine::admit_slot(int k, uint64_t utt, const int32_t *tok, int n, const fl
     Q3T_HIP(hipMemcpyAsync(utt_ + k, state_h + 6, 8, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemsetAsync(seen_ + (size_t)k * c_.codec_vocab, 0, c_.codec_vocab, stream_));
     Q3T_HIP(hipMemsetAsync(codes_ + (size_t)k * codes_max_len_ * NCB, 0, (size_t)codes_max_len_ * NCB * 4, stream_));
-    // prefill: plen single-slot steps on slot k (its graph captured once per slot)
-    if (!g_slot_.count(k)) {
-        hipGraph_t graph = nullptr;
-        Q3T_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-        const bool ok = enqueue_slot_step(k, stream_);
-        hipError_t e = hipStreamEndCapture(stream_, &graph);
-        if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
-        if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
-        hipGraphExec_t exec = nullptr;
-        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
-        g_slot_[k] = exec;
-    }
-    for (int t = 0; t < plen; ++t) {
-        Q3T_HIP(hipMemcpyAsync(x_ + (size_t)k * H, prefill_ + ((size_t)k * 10 + t) * H, H * 4, hipMemcpyDeviceToDevice, stream_));
-        Q3T_HIP(hipMemcpyAsync(slot_pos_ + k, cp_pos_ + (size_t)t * max_slots_, 4, hipMemcpyDeviceToDevice, stream_));
-        Q3T_HIP(hipGraphLaunch(g_slot_[k], stream_));
-    }
+    Q3T_HIP(hipMemcpyAsync(hidden_ + (size_t)k * H, ahidden_ + (size_t)k * H, H * 4, hipMemcpyDeviceToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(pos_ + k, state_h + 4, 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_ + k, state_h + 5, 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(done_ + k, state_h + 3, 4, hipMemcpyHostToDevice, stream_));
-    // CB0 of the slot's first frame from its last prefill logits (the slot's rows of every per-slot array)
-    SelectSpec sp = select_spec(SEL_CB0, gp_, 0, 0);
+    SelectSpec sp = select_spec(SEL_CB0, gp_, 0, 0);   // the slot's rows of every per-slot array
     sp.tokens += (size_t)k * 16; sp.codes += (size_t)k * codes_max_len_ * NCB; sp.frame += k; sp.done += k; sp.utt += k;
     sp.seen += (size_t)k * c_.codec_vocab; sp.n_tokens += k; sp.force_frames += k;
     if (sp.ticket) sp.ticket += k;
-    return select_tokens(sp, logits_ + (size_t)k * c_.codec_vocab, 1, stream_);
+    return select_tokens(sp, alogits_ + (size_t)k * c_.codec_vocab, 1, stream_);
 }
 
 bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
@@ -1226,87 +1309,124 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
     if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
     if (gp.max_len > codes_max_len_) { set_error("max_len exceeds the code buffer"); return false; }
     auto lk = persist_lock(persist_, device_);
+    if (!alloc_admission()) return false;
+    q_slots_ = S;
+    // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
+    hipStream_t as = (S == 1 && persist_) ? stream_ : astream_;
     if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty && gp.seed == gp_.seed)) {
         for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
         g_frame_.clear();
     }
     gp_ = gp;
-    // device arena for the finished utterances' codes (copied to the caller once at the end)
-    int32_t *out_dev = nullptr;
+    int32_t *out_dev = nullptr;   // the finished utterances' codes, copied to the caller once at the end
     Q3T_HIP(hipMalloc(&out_dev, (size_t)n_utt * gp.max_len * NCB * 4));
-    int *pin = nullptr;   // [S][8] admission staging + [S] done flags + one constant 0 (parking a slot)
-    if (hipHostMalloc(&pin, ((size_t)S * 9 + 1) * 4, hipHostMallocDefault) != hipSuccess) {
+    int *pin = nullptr;   // [S][8] activation staging, [S] done flags, [S] admission targets, one constant 0 (parking)
+    if (hipHostMalloc(&pin, ((size_t)S * 10 + 1) * 4, hipHostMallocDefault) != hipSuccess) {
         hipFree(out_dev);
         set_error("hipHostMalloc failed");
         return false;
     }
-    int *done_h = pin + (size_t)S * 8, *park = pin + (size_t)S * 9;
+    int *done_h = pin + (size_t)S * 8, *tgt_h = pin + (size_t)S * 9, *park = pin + (size_t)S * 10;
     *park = 0;
-    hipEvent_t ev = nullptr;
+    hipEvent_t aev = nullptr, pev = nullptr;
     auto cleanup = [&]() {
-        if (ev) hipEventDestroy(ev);
+        hipStreamSynchronize(as);
+        hipStreamSynchronize(stream_);
+        if (aev) hipEventDestroy(aev);
+        if (pev) hipEventDestroy(pev);
         hipFree(out_dev);
         hipHostFree(pin);
+        std::vector<uint64_t> ident(max_slots_);   // generate() keys sampling by slot index again
+        for (int k = 0; k < max_slots_; ++k) ident[k] = (uint64_t)k;
+        hipMemcpy(utt_, ident.data(), max_slots_ * 8, hipMemcpyHostToDevice);
     };
-    Q3T_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    // every slot starts idle: done = 0 (no selection, no advance), position / frame 0, valid code ids for the gathers
-    // an idle slot still runs through, no trailing text
-    Q3T_HIP(hipMemsetAsync(done_, 0, S * 4, stream_));
-    Q3T_HIP(hipMemsetAsync(pos_, 0, S * 4, stream_));
-    Q3T_HIP(hipMemsetAsync(frame_, 0, S * 4, stream_));
-    Q3T_HIP(hipMemsetAsync(tokens_, 0, (size_t)S * 16 * 4, stream_));
-    Q3T_HIP(hipMemsetAsync(trailing_len_, 0, S * 4, stream_));
-    std::vector<int> slot_utt(S, -1), started(S, 0);
-    int next = 0, f = 0, n_fin = 0;
-    auto admit = [&](int k) -> bool {
-        const int u = next++;
-        if (!admit_slot(k, (uint64_t)u, tokens[u], n_tokens[u], has_spk ? speaker[u] : nullptr, gp, plen, pin + (size_t)k * 8))
-            return false;
-        slot_utt[k] = u;
-        started[k] = f;
+    Q3T_HIP(hipEventCreateWithFlags(&aev, hipEventDisableTiming));
+    Q3T_HIP(hipEventCreateWithFlags(&pev, hipEventDisableTiming));
+    // every slot starts parked: done = 0 (no selection, no advance), position plen (above the rows a prefill writes),
+    // valid code ids for the gathers it still runs through, no trailing text
+    {
+        std::vector<int> pl(S, plen);
+        Q3T_HIP(hipMemsetAsync(done_, 0, S * 4, stream_));
+        Q3T_HIP(hipMemcpyAsync(pos_, pl.data(), S * 4, hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipMemsetAsync(frame_, 0, S * 4, stream_));
+        Q3T_HIP(hipMemsetAsync(tokens_, 0, (size_t)S * 16 * 4, stream_));
+        Q3T_HIP(hipMemsetAsync(trailing_len_, 0, S * 4, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+    }
+    enum { FREE, PENDING, ACTIVE };
+    std::vector<int> state(S, FREE), slot_utt(S, -1), started(S, 0), tl(S, 0);
+    std::vector<int> batch_tgt, batch_tl;   // the admission batch in flight (at most one)
+    int next = 0, f = 0, n_fin = 0, n_busy = 0;
+    auto admit = [&]() -> bool {   // every free slot, up to max_active busy, one batch
+        std::vector<int> tgt, utt;
+        for (int k = 0; k < S && next + (int)tgt.size() < n_utt && n_busy + (int)tgt.size() < max_active; ++k)
+            if (state[k] == FREE) { tgt.push_back(k); utt.push_back(next + (int)tgt.size() - 1); }
+        if (tgt.empty()) return true;
+        batch_tl.assign(tgt.size(), 0);
+        if (!admit_batch(tgt, utt, tokens, n_tokens, has_spk ? speaker : nullptr, gp, plen, as, tgt_h, batch_tl)) return false;
+        Q3T_HIP(hipEventRecord(aev, as));
+        for (size_t j = 0; j < tgt.size(); ++j) {
+            state[tgt[j]] = PENDING;
+            slot_utt[tgt[j]] = utt[j];
+            tl[tgt[j]] = batch_tl[j];
+        }
+        next += (int)tgt.size();
+        n_busy += (int)tgt.size();
+        batch_tgt = tgt;
         return true;
     };
-    for (int k = 0; k < max_active && next < n_utt; ++k)
-        if (!admit(k)) { cleanup(); return false; }
+    auto activate = [&]() -> bool {   // the batch in flight has finished: its slots join the frame loop
+        if (as != stream_) Q3T_HIP(hipStreamWaitEvent(stream_, aev, 0));
+        for (int k : batch_tgt) {
+            const int u = slot_utt[k];
+            if (!activate_slot(k, (uint64_t)u, tl[k], n_tokens[u], gp, plen, pin + (size_t)k * 8)) return false;
+            state[k] = ACTIVE;
+            started[k] = f;
+        }
+        batch_tgt.clear();
+        return true;
+    };
+    if (!admit() || !activate()) { cleanup(); return false; }
     if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) { cleanup(); return false; }
-    // frame loop, one frame in flight: frame f is launched before frame f-1's done flags are read
-    bool pending = false;
+    bool polled = false;   // one frame in flight: frame f is launched before frame f-1's done flags are read
     while (n_fin < n_utt) {
+        int n_active = 0;
+        for (int k = 0; k < S; ++k) n_active += state[k] == ACTIVE;
+        if (n_active == 0) {   // only an admission in flight: wait for it instead of running empty frames
+            if (batch_tgt.empty() && !admit()) { cleanup(); return false; }
+            Q3T_HIP(hipEventSynchronize(aev));
+            if (!activate()) { cleanup(); return false; }
+            polled = false;
+            continue;
+        }
         Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
         ++f;
-        if (pending) {
-            Q3T_HIP(hipEventSynchronize(ev));
-            // done_h is frame f-1's: a slot done there (or at max_len) ran at most this one extra, harmless frame
-            bool refill = false;
-            for (int k = 0; k < S; ++k) {
-                if (slot_utt[k] < 0) continue;
-                const int ran = f - 1 - started[k];   // frames completed by the read-back
+        if (polled) {
+            Q3T_HIP(hipEventSynchronize(pev));
+            for (int k = 0; k < S; ++k) {   // done_h: after frame f-1
+                if (state[k] != ACTIVE) continue;
+                const int ran = f - 1 - started[k];
                 const int d = done_h[k];
                 if (d < 0 && ran < gp.max_len) continue;
                 const int u = slot_utt[k];
                 n_frames[u] = d >= 0 ? std::min(d, gp.max_len) : gp.max_len;
                 Q3T_HIP(hipMemcpyAsync(out_dev + (size_t)u * gp.max_len * NCB, codes_ + (size_t)k * codes_max_len_ * NCB,
                                        (size_t)gp.max_len * NCB * 4, hipMemcpyDeviceToDevice, stream_));
-                slot_utt[k] = -1;
-                ++n_fin;
                 if (d < 0)   // stopped at max_len: park the slot (no selection, no advance)
                     Q3T_HIP(hipMemcpyAsync(done_ + k, park, 4, hipMemcpyHostToDevice, stream_));
-                refill = true;
-            }
-            if (refill) {
-                int active = 0;
-                for (int k = 0; k < S; ++k) active += slot_utt[k] >= 0;
-                for (int k = 0; k < S && next < n_utt && active < max_active; ++k)
-                    if (slot_utt[k] < 0) {
-                        if (!admit(k)) { cleanup(); return false; }
-                        ++active;
-                    }
+                state[k] = FREE;
+                slot_utt[k] = -1;
+                --n_busy;
+                ++n_fin;
             }
         }
+        if (!batch_tgt.empty() && (as == stream_ || hipEventQuery(aev) == hipSuccess) && !activate()) { cleanup(); return false; }
+        if (batch_tgt.empty() && next < n_utt && !admit()) { cleanup(); return false; }
+        if (as == stream_ && !batch_tgt.empty() && !activate()) { cleanup(); return false; }
         Q3T_HIP(hipMemcpyAsync(done_h, done_, S * 4, hipMemcpyDeviceToHost, stream_));
-        Q3T_HIP(hipEventRecord(ev, stream_));
-        pending = true;
-        if (f > (n_utt + 1) * (gp.max_len + 2)) { cleanup(); set_error("generate_queue: no progress"); return false; }
+        Q3T_HIP(hipEventRecord(pev, stream_));
+        polled = true;
+        if (f > (n_utt + 1) * (gp.max_len + plen + 2)) { cleanup(); set_error("generate_queue: no progress"); return false; }
     }
     for (int u = 0; u < n_utt; ++u)
         Q3T_HIP(hipMemcpyAsync(codes + (size_t)u * gp.max_len * NCB, out_dev + (size_t)u * gp.max_len * NCB,

@@ -100,7 +100,8 @@ public:
     // token by token through a single-slot talker step on that slot's KV region while the other slots wait, and its
     // state (position, frame, EOS, repetition set, codes) is reset.  Sampling streams are keyed by the utterance's
     // index in the call (utt id), so an utterance's codes do not depend on its slot, its admission frame or the
-    // other utterances in flight (the S-slot decode step never mixes tokens).
+    // other utterances in flight (the S-slot decode step never mixes tokens); on the matrix-core path (>= 4 slots) the
+    // admission prefill runs the batch's kernels for its one slot, so the first wave's codes equal generate()'s.
     bool generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
                         const GenParams &gp, int32_t *codes, int *n_frames, int max_active);
     // fill this context's weight arenas (laid out with recv_weights) from another context's, device to device
@@ -155,12 +156,25 @@ private:
     bool enqueue_text_projection(int n_rows, hipStream_t s);
     bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));
     bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
-    // continuous batching: the single-slot prefill step of slot cur_slot_ (graph per slot) and slot admission
-    bool enqueue_slot_step(int slot, hipStream_t s);
-    bool admit_slot(int slot, uint64_t utt, const int32_t *tok, int n, const float *spk, const GenParams &gp, int plen,
-                    int *state_h);
-    std::map<int, hipGraphExec_t> g_slot_;
-    int *slot_pos_ = nullptr;      // [max_slots] position of the single-slot prefill step
+    // continuous batching: admission batches on their own stream and scratch (staging slots + staging KV), then
+    // activation of each slot on the main stream between two frames
+    bool alloc_admission();
+    bool enqueue_stage_step(int a, hipStream_t s);
+    bool admit_batch(const std::vector<int> &tgt, const std::vector<int> &utt, const int32_t *const *tokens,
+                     const int *n_tokens, const float *const *speaker, const GenParams &gp, int plen, hipStream_t as,
+                     int *tgt_h, std::vector<int> &trailing_len);
+    bool activate_slot(int slot, uint64_t utt, int trailing_len, int n_tok, const GenParams &gp, int plen, int *state_h);
+    bool enqueue_text_projection(int n_rows, hipStream_t s, const int *idx, uint16_t *hbuf, float *out);
+    std::map<int, hipGraphExec_t> g_stage_;
+    hipStream_t astream_ = nullptr;
+    float *ax_ = nullptr, *aqkv_ = nullptr, *aparts_ = nullptr, *apart_ = nullptr, *aprefill_ = nullptr;
+    float *ashid_ = nullptr, *aslog_ = nullptr, *ahidden_ = nullptr, *alogits_ = nullptr, *aproj_out_ = nullptr;
+    uint16_t *axn_ = nullptr, *aattn_ = nullptr, *ahmlp_ = nullptr, *aproj_h_ = nullptr, *akc_ = nullptr, *avc_ = nullptr;
+    unsigned *aticket_ = nullptr;
+    int *astage_pos_ = nullptr, *atarget_ = nullptr, *aproj_idx_ = nullptr;
+    RowRecipe *arecipe_ = nullptr;
+    int aproj_cap_ = 0;
+    int q_slots_ = 0;              // slot count of the running queue (the batch the admissions reproduce)
 
     Config c_;
     std::string tts_path_, tok_path_;

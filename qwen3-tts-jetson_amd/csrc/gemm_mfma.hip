@@ -558,7 +558,7 @@ static int nch_of(int K) {
 }
 
 bool gemm_mfma_supported(const GemvParams &p) {
-    if (p.B < gemm_mfma_min_batch() || p.sel.mode != SEL_NONE || p.N % MM_ROWS != 0) return false;
+    if ((p.B < gemm_mfma_min_batch() && !p.force_mm) || p.sel.mode != SEL_NONE || p.N % MM_ROWS != 0) return false;
     const int nch = nch_of(p.K);
     if (!nch) return false;
     const bool swiglu = p.act == ACT_SWIGLU;

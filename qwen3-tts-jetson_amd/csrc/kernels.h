@@ -107,6 +107,8 @@ struct GemvParams {
     // to parts[z][b][n] (no epilogue); resid_norm() folds them into the residual stream
     float *parts = nullptr;
     int ksplit = 1;
+    bool force_mm = false;   // matrix-core path even below gemm_mfma_min_batch() (a single slot reproducing the
+                             // per-token arithmetic of a batch that runs there)
 };
 bool gemv(const GemvParams &p, hipStream_t s);   // routes wide batches to gemm_mfma (gemm_mfma.hip)
 // matrix-core path for B >= gemm_mfma_min_batch() tokens (Q3T_MFMA_MIN_B, default 4; 0 = off): F16 / F32 / RMS / LN
@@ -149,6 +151,11 @@ bool advance(int *pos, int *frame, const int *done, int S, hipStream_t s);   // 
 struct RowTerm { const void *ptr; int is_f16; };
 struct RowRecipe { float *out; RowTerm t[3]; };
 bool rows_recipe(const RowRecipe *recipe_dev, int n_rows, int H, hipStream_t s);
+// K/V rows [0, rows) of staging slots 0..n-1 (cache [layer][slot][kv][src_ctx][D]) -> slots dst_slot[0..n) of a
+// [layer][slot][kv][dst_ctx][D] cache (continuous-batching admissions)
+bool kv_stage_copy(const uint16_t *sk, const uint16_t *sv, uint16_t *dk, uint16_t *dv, const int *dst_slot, int n,
+                   int n_layers, int nkv, int rows, int D, size_t src_layer, size_t dst_layer, int src_ctx, int dst_ctx,
+                   hipStream_t s);
 
 // batched residual + RMSNorm between the matrix-core projections (one workgroup per token, H <= 1024):
 //   x[b] = xin[b] + parts[0][b] + ... + parts[ksplit-1][b]   (written to x when parts or xin != x)

@@ -6,6 +6,8 @@ the next queued utterance between two frames (its prefill runs on that slot alon
   invariance   the same queue with 1, 3 and all slots in flight gives every utterance bit-identical codes and
                lengths: the S-slot decode step never mixes tokens, sampling is keyed by the utterance's index in the
                call, and a parked / refilled slot leaves its neighbours alone
+  generate     on the matrix-core path (>= 4 slots) an admission runs the batch's kernels for its one slot: the first
+               wave's codes equal generate()'s exactly
   oracle       utterances admitted mid-run (into a slot that had already held two others) are teacher-forced
                against the CPU oracle with their own utterance id, including their EOS frame
 Prompts of 5..12 text tokens put the EOS ramp (expected = max(20, 4 n_tokens) frames) inside max_len, so the queue
@@ -63,6 +65,28 @@ def test_queue_is_slot_and_admission_invariant(full, slots, n_utt):
             for u in range(n_utt):
                 assert np.array_equal(runs[a][u], runs[slots][u]), (a, u, len(runs[a][u]), len(runs[slots][u]))
         print(f"{slots} slots, {n_utt} utterances: lengths {lens}")
+    finally:
+        eng.close()
+
+
+def test_queue_first_wave_equals_generate(full):
+    """on the matrix-core path an admission runs the batch's own kernels for its one slot, so the utterances of the
+    first wave (slot u = utterance u) get exactly generate()'s codes, refills of the other slots notwithstanding"""
+    import q3t
+    tts, tok, orc = full
+    nf, slots, n_utt = 40, 8, 20
+    eng = q3t.Engine(tts, None, device=0, max_slots=slots, max_ctx=nf + 40)
+    try:
+        H = eng.cfg["hidden"]
+        prompts = _prompts(n_utt, 11)
+        spk = [np.zeros(H, np.float32)] * n_utt
+        kw = dict(max_len=nf, temperature=0.9, top_k=50, seed=31)
+        q = eng.generate_queue(prompts, speakers=spk, **kw)
+        g = eng.generate(prompts[:slots], speakers=spk[:slots], **kw)
+        for u in range(slots):
+            assert np.array_equal(q[u], g[u]), (u, len(q[u]), len(g[u]))
+        # generate() after a queue run keys sampling by slot again
+        assert all(np.array_equal(a, b) for a, b in zip(eng.generate(prompts[:slots], speakers=spk[:slots], **kw), g))
     finally:
         eng.close()
 
