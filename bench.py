@@ -184,7 +184,7 @@ def main():
     ap.add_argument("--batched", type=int, default=64,
                     help="secondary measurement: this many concurrent utterances per GPU (BASELINE configs[2] at N=1, "
                          "configs[3] at N>1: weak scaling, value over all ranks); 0 = off")
-    ap.add_argument("--serve", type=int, default=128,
+    ap.add_argument("--serve", type=int, default=256,
                     help="serving measurement (N=1): this many utterances with natural EOS (prompt lengths 10..120 "
                          "tokens) through `batched` slots, lock-step batches vs continuous batching; 0 = off")
     args = ap.parse_args()

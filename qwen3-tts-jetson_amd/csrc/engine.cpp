@@ -656,7 +656,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
     const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
     if (mm) {
         if (!decoder_stack_mm(c_, opt_.attn_split, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
-                              rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_))
+                              rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_, policy_slots_))
             return false;
     } else if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_,
                               ticket_, s, gather_input ? &in0 : nullptr)) {
@@ -718,7 +718,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
         if (mm) {
             if (!decoder_stack_mm(c_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
-                                  p == 0 ? nullptr : cp_out_norm_, nullptr))
+                                  p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_))
                 return false;
         } else if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0, cp_fused_attn_)) {
@@ -756,7 +756,11 @@ bool Engine::enqueue_frame(int S, hipStream_t s) {
 }
 
 bool Engine::graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t)) {
-    if (cache.count(S)) return true;
+    return graph_for_key(cache, S, S, fn);
+}
+
+bool Engine::graph_for_key(std::map<int, hipGraphExec_t> &cache, int key, int S, bool (Engine::*fn)(int, hipStream_t)) {
+    if (cache.count(key)) return true;
     hipGraph_t graph = nullptr;
     Q3T_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
     const bool ok = (this->*fn)(S, stream_);
@@ -767,7 +771,7 @@ bool Engine::graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     hipGraphDestroy(graph);
     if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
-    cache[S] = exec;
+    cache[key] = exec;
     return true;
 }
 
@@ -1336,6 +1340,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
         if (pev) hipEventDestroy(pev);
         hipFree(out_dev);
         hipHostFree(pin);
+        policy_slots_ = 0;
         std::vector<uint64_t> ident(max_slots_);   // generate() keys sampling by slot index again
         for (int k = 0; k < max_slots_; ++k) ident[k] = (uint64_t)k;
         hipMemcpy(utt_, ident.data(), max_slots_ * 8, hipMemcpyHostToDevice);
@@ -1387,7 +1392,19 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
         return true;
     };
     if (!admit() || !activate()) { cleanup(); return false; }
-    if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) { cleanup(); return false; }
+    // frame graph over slots [0, S_eff): S_eff = the highest busy slot + 1, rounded up to 8, never below the smallest
+    // batch that keeps the S-slot kernel family (matrix cores from 4 slots, k_attn_seq from 16), whose per-token
+    // arithmetic the graph reproduces (policy_slots_ = S): a draining queue stops paying for parked slots
+    const int fam = S >= 16 ? 16 : S >= gemm_mfma_min_batch() ? gemm_mfma_min_batch() : S;
+    policy_slots_ = S;
+    auto frame_graph = [&](hipGraphExec_t *g) -> bool {
+        int hi = 0;
+        for (int k = 0; k < S; ++k) if (state[k] != FREE) hi = k + 1;
+        int se = fam < S ? std::max(fam, std::min(S, (hi + 7) / 8 * 8)) : S;
+        if (!graph_for_key(g_frame_, se + 65536 * S, se, &Engine::enqueue_frame)) return false;
+        *g = g_frame_[se + 65536 * S];
+        return true;
+    };
     bool polled = false;   // one frame in flight: frame f is launched before frame f-1's done flags are read
     while (n_fin < n_utt) {
         int n_active = 0;
@@ -1399,7 +1416,9 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
             polled = false;
             continue;
         }
-        Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
+        hipGraphExec_t fg = nullptr;
+        if (!frame_graph(&fg)) { cleanup(); return false; }
+        Q3T_HIP(hipGraphLaunch(fg, stream_));
         ++f;
         if (polled) {
             Q3T_HIP(hipEventSynchronize(pev));

@@ -155,6 +155,8 @@ private:
     bool enqueue_frame(int S, hipStream_t s);
     bool enqueue_text_projection(int n_rows, hipStream_t s);
     bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));
+    bool graph_for_key(std::map<int, hipGraphExec_t> &cache, int key, int S, bool (Engine::*fn)(int, hipStream_t));
+    int policy_slots_ = 0;         // > 0: the batched stacks choose kernels as for this many slots (queue graphs)
     bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
     // continuous batching: admission batches on their own stream and scratch (staging slots + staging KV), then
     // activation of each slot on the main stream between two frames

@@ -5,7 +5,8 @@ the next queued utterance between two frames (its prefill runs on that slot alon
 
   invariance   the same queue with 1, 3 and all slots in flight gives every utterance bit-identical codes and
                lengths: the S-slot decode step never mixes tokens, sampling is keyed by the utterance's index in the
-               call, and a parked / refilled slot leaves its neighbours alone
+               call, and a parked / refilled slot leaves its neighbours alone; at 12 and 24 slots the frame graph
+               also shrinks to the busy slots (8 / 16 of them with 1 or 3 in flight) within the same kernel family
   generate     on the matrix-core path (>= 4 slots) an admission runs the batch's kernels for its one slot: the first
                wave's codes equal generate()'s exactly
   oracle       utterances admitted mid-run (into a slot that had already held two others) are teacher-forced
@@ -46,7 +47,7 @@ def _prompts(n, seed):
     return out
 
 
-@pytest.mark.parametrize("slots,n_utt", [(4, 10), (16, 36)])
+@pytest.mark.parametrize("slots,n_utt", [(4, 10), (12, 20), (24, 40)])
 def test_queue_is_slot_and_admission_invariant(full, slots, n_utt):
     import q3t
     tts, tok, orc = full
