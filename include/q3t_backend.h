@@ -136,6 +136,18 @@ int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes /* [n_frames][16] */, 
 int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes /* [n_frames][n_codebooks] */, int32_t n_frames,
                                int32_t n_codebooks, int32_t chunk_frames, float *pcm, int64_t *n_samples);
 
+/* Several utterances through shared launches (the batched counterpart of q3t_vocoder_decode /
+ * q3t_vocoder_decode_chunked; the reference decodes one utterance per call, qwen3_tts.cpp:518 /
+ * trt_vocoder.cpp:98-170).  FULL: utterances run as batches of up to q3t_vocoder_set_batch_frames frames (default
+ * 4096), each padded to its batch's longest; the decoder is causal end to end, so pcm[u] is exactly
+ * q3t_vocoder_decode(codes[u]).  CHUNK40: every chunk_frames-long chunk of every utterance is one independent sequence
+ * of the batch; pcm[u] equals q3t_vocoder_decode_chunked(codes[u]).  codes[u]: [n_frames[u]][16];
+ * pcm[u]: capacity q3t_vocoder_num_samples(n_frames[u], mode); n_samples[u] receives its length. */
+int q3t_vocoder_decode_batch(q3t_ctx *ctx, int32_t n_utt, const int32_t *const *codes, const int32_t *n_frames,
+                             int mode, int32_t chunk_frames, float *const *pcm, int64_t *n_samples);
+/* frames (utterances x frames) per batched vocoder launch sequence; scratch grows to ~3 MB per frame */
+int q3t_vocoder_set_batch_frames(q3t_ctx *ctx, int32_t frames);
+
 /* ---- speaker encoder (ECAPA-TDNN; the TTS GGUF's spk_enc.* tensors)
  * q3t_speaker_dim: embedding length, 0 when the model has no speaker encoder.
  * q3t_speaker_encode: AudioTokenizerEncoder::encode (src/audio_tokenizer_encoder.h:107-108): samples in [-1, 1] at

@@ -270,6 +270,32 @@ int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes, int32_t n_fra
     GUARD_END
 }
 
+int q3t_vocoder_decode_batch(q3t_ctx *ctx, int32_t n_utt, const int32_t *const *codes, const int32_t *n_frames,
+                             int mode, int32_t chunk_frames, float *const *pcm, int64_t *n_samples) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::Vocoder *v = ctx->engine.vocoder();
+    if (!v || !v->loaded()) { q3t::set_error("vocoder not loaded (no tokenizer GGUF given)"); return Q3T_ERR; }
+    if (mode != Q3T_VOCODER_FULL && mode != Q3T_VOCODER_CHUNK40) { q3t::set_error("bad vocoder mode"); return Q3T_ERR; }
+    if (n_utt < 0 || (n_utt > 0 && (!codes || !n_frames || !pcm || !n_samples))) { q3t::set_error("null argument"); return Q3T_ERR; }
+    for (int u = 0; u < n_utt; ++u)
+        if (n_frames[u] > 0 && (!codes[u] || !pcm[u])) { q3t::set_error("null argument"); return Q3T_ERR; }
+    if (mode == Q3T_VOCODER_CHUNK40 && chunk_frames <= 0) { q3t::set_error("chunk_frames must be > 0"); return Q3T_ERR; }
+    std::vector<int> nf(n_frames, n_frames + n_utt);
+    return v->decode_batch(n_utt, codes, nf.data(), mode, pcm, n_samples, chunk_frames) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
+int q3t_vocoder_set_batch_frames(q3t_ctx *ctx, int32_t frames) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    q3t::Vocoder *v = ctx->engine.vocoder();
+    if (!v || !v->loaded()) { q3t::set_error("vocoder not loaded (no tokenizer GGUF given)"); return Q3T_ERR; }
+    v->set_batch_frames(frames);
+    return Q3T_OK;
+    GUARD_END
+}
+
 int q3t_ctx_create_speaker(const char *tts_gguf, int device, q3t_ctx **out) {
     GUARD_BEGIN
     if (!out || !tts_gguf) { q3t::set_error("null argument"); return Q3T_ERR; }

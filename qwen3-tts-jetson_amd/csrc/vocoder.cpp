@@ -279,18 +279,10 @@ int64_t Vocoder::n_samples(int n_frames, int mode) const {
     return mode == 0 ? full_len(n_frames) : (int64_t)n_frames * 1920;
 }
 
-bool Vocoder::ensure(int F) {
-    if (F <= cap_frames_) return true;
-    for (void *p : scratch_) hipFree(p);
-    scratch_.clear();
-    auto alloc = [&](size_t bytes) -> void * {
-        void *p = nullptr;
-        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
-        scratch_.push_back(p);
-        return p;
-    };
-    // largest [T][C] activation over the stages
-    size_t big = 0;
+// scratch for nb utterances of F frames: sized by the totals (largest activation x nb, frames x nb), so a batch of
+// short utterances reuses the scratch of one long one
+bool Vocoder::ensure(int F, int nb) {
+    size_t big = 0;   // largest [T][C] activation of one utterance over the stages
     int64_t T = F;
     big = std::max(big, (size_t)F * std::max(latent_, 3 * latent_));
     for (int u = 0; u < 2; ++u) { T = (T - 1) * 2 + up_[u].ct.k; big = std::max(big, (size_t)T * up_[u].pw_dim / 2 + (size_t)T * latent_); }
@@ -300,11 +292,28 @@ bool Vocoder::ensure(int F) {
         T = (T - 1) * s + K - 2 * (K - s);
         big = std::max(big, (size_t)T * dec_[d].ct.oc);
     }
+    big *= (size_t)nb;
+    const size_t frames = (size_t)F * nb;
+    const size_t pcm = (size_t)nb * std::max<int64_t>(full_len(F), (int64_t)F * 1920);
+    if (big <= cap_big_ && frames <= cap_ftot_ && pcm <= cap_pcm_ && F <= cap_frames_) return true;
+    big = std::max(big, cap_big_);
+    const size_t fr = std::max(frames, cap_ftot_), pc = std::max(pcm, cap_pcm_);
+    F = std::max(F, cap_frames_);
+    for (void *p : scratch_) hipFree(p);
+    scratch_.clear();
+    cap_big_ = cap_ftot_ = cap_pcm_ = 0;
+    cap_frames_ = 0;
+    auto alloc = [&](size_t bytes) -> void * {
+        void *p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        scratch_.push_back(p);
+        return p;
+    };
     for (int i = 0; i < 3; ++i) if (!(buf_[i] = (float *)alloc(big * 4))) { set_error("vocoder scratch alloc"); return false; }
     if (!(xh_ = (uint16_t *)alloc(big * 2)) || !(xh2_ = (uint16_t *)alloc(big * 2))) { set_error("vocoder scratch alloc"); return false; }
-    codes_ = (int32_t *)alloc((size_t)F * 16 * 4);
-    cols_ = (int *)alloc((size_t)F * 16 * 4);
-    pcm_ = (float *)alloc((size_t)std::max<int64_t>(full_len(F), (int64_t)F * 1920) * 4);
+    codes_ = (int32_t *)alloc(fr * 16 * 4);
+    cols_ = (int *)alloc(fr * 16 * 4);
+    pcm_ = (float *)alloc(pc * 4);
     // RoPE cos/sin table (theta 1e4, head_dim 64) with the ggml_rope_cache_init recurrence
     std::vector<float> rope((size_t)F * head_dim_);
     const float theta_scale = powf(10000.0f, -2.0f / (float)head_dim_);
@@ -319,6 +328,7 @@ bool Vocoder::ensure(int F) {
     rope_ = (float *)alloc(rope.size() * 4);
     if (!codes_ || !cols_ || !pcm_ || !rope_) { set_error("vocoder scratch alloc"); return false; }
     Q3T_HIP(hipMemcpy(rope_, rope.data(), rope.size() * 4, hipMemcpyHostToDevice));
+    cap_big_ = big; cap_ftot_ = fr; cap_pcm_ = pc;
     cap_frames_ = F;
     return true;
 }
@@ -329,7 +339,7 @@ bool Vocoder::run_conv(const Conv &c, const float *x, int T, int pad, int dil, c
     ConvParams p;
     p.x = x; p.T_in = T; p.C_in = c.ic;
     if (c.ic % 8 == 0) {   // SnakeBeta + f16 rounding once per element, not once per output tile and tap window
-        if (!snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, T, c.ic, s)) return false;
+        if (!snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, (int64_t)T * nb_, c.ic, s)) return false;
         p.xh = xh_;
     } else if (sn) {
         p.snake_a = sn->a; p.snake_ib = sn->ib;
@@ -339,6 +349,7 @@ bool Vocoder::run_conv(const Conv &c, const float *x, int T, int pad, int dil, c
     p.dmin = -pad; p.dmax = (c.k - 1) * dil - pad;
     p.y = y; p.C_out = c.oc; p.M = T + pad - dil * (c.k - 1); p.so = 1; p.ob = 0;
     p.bias = c.b; p.resid = resid; p.act = act;
+    p.nb = nb_; p.xbs = T; p.ybs = p.M;
     return conv(p, s);
 }
 
@@ -347,7 +358,7 @@ bool Vocoder::run_conv(const Conv &c, const float *x, int T, int pad, int dil, c
 bool Vocoder::run_convT(const Conv &c, const float *x, int T, int st, int trim, const Snake *sn, float *y, int T_out,
                         hipStream_t s) {
     const bool pre = c.ic % 8 == 0;   // one snake/f16 pass shared by the st output phases
-    if (pre && !snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, T, c.ic, s)) return false;
+    if (pre && !snake_f16(x, sn ? sn->a : nullptr, sn ? sn->ib : nullptr, xh_, (int64_t)T * nb_, c.ic, s)) return false;
     for (int phi = 0; phi < st; ++phi) {
         ConvParams p;
         p.x = x; p.T_in = T; p.C_in = c.ic;
@@ -365,6 +376,7 @@ bool Vocoder::run_convT(const Conv &c, const float *x, int T, int st, int trim, 
         p.n_taps = n; p.dmin = dmin; p.dmax = dmax;
         p.y = y; p.C_out = c.oc; p.M = (T_out - phi + st - 1) / st; p.so = st; p.ob = phi;
         p.bias = c.b;
+        p.nb = nb_; p.xbs = T; p.ybs = T_out;
         if (!conv(p, s)) return false;
     }
     return true;
@@ -381,6 +393,7 @@ bool Vocoder::conv16(const Conv &c, const uint16_t *xh, int T, int pad, int dil,
     p.bias = c.b; p.resid = resid;
     p.y16 = y16;
     if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
+    p.nb = nb_; p.xbs = T; p.ybs = p.M;
     return conv(p, s);
 }
 
@@ -393,6 +406,7 @@ bool Vocoder::convT16(const Conv &c, const uint16_t *xh, int T, int st, int trim
         p.ct_w = c.w; p.ct_k = c.k; p.ct_st = st; p.ct_trim = trim; p.T_out = T_out;
         p.y = y; p.C_out = c.oc; p.bias = c.b; p.y16 = y16;
         if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
+        p.nb = nb_; p.xbs = T; p.ybs = T_out;
         return conv(p, s);
     }
     for (int phi = 0; phi < st; ++phi) {
@@ -412,20 +426,32 @@ bool Vocoder::convT16(const Conv &c, const uint16_t *xh, int T, int st, int trim
         p.bias = c.b;
         p.y16 = y16;
         if (next) { p.y16_a = next->a; p.y16_ib = next->ib; }
+        p.nb = nb_; p.xbs = T; p.ybs = T_out;
         if (!conv(p, s)) return false;
     }
     return true;
 }
 
-bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int64_t *n_out, hipStream_t s) {
+bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int64_t *n_out, hipStream_t s, int nb) {
+    if (nb < 1 || F > cap_frames_ || (size_t)F * nb > cap_ftot_) { set_error("vocoder: decode larger than ensure()"); return false; }
+    nb_ = nb;
+    const bool ok = decode_rows(codes_dev, F, pcm_dev, n_out, s);
+    nb_ = 1;
+    return ok;
+}
+
+// one decode of nb_ utterances of F frames: row-wise stages (RVQ, projections, norms, 1-tap convs) run over all
+// nb_*F rows, sequence stages (causal convs, transposed convs, attention) carry the utterance as grid z
+bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64_t *n_out, hipStream_t s) {
     const int VH = hidden_, LAT = latent_;
+    const int FR = F * nb_;   // frame rows of the batch
     float *A = buf_[0], *B = buf_[1], *C = buf_[2];
     // 1) RVQ: latent = W_first . cb_first[c0] + sum_k W_rest . cb_rest_k[c_{k+1}]   (:650-703)
-    if (!codes_cols(codes_dev, cols_, F, 16, s)) return false;
+    if (!codes_cols(codes_dev, cols_, FR, 16, s)) return false;
     GemvParams g;
-    g.N = VH; g.K = cb_dim_; g.B = F; g.pro = PRO_F16; g.ldx = cb_dim_; g.ldo = VH;
+    g.N = VH; g.K = cb_dim_; g.B = FR; g.pro = PRO_F16; g.ldx = cb_dim_; g.ldo = VH;
     for (int k = 0; k < 15; ++k) {
-        g.W = vq_rest_out_; g.x = cb_rest_[k]; g.x_idx = cols_ + (size_t)(k + 1) * F;
+        g.W = vq_rest_out_; g.x = cb_rest_[k]; g.x_idx = cols_ + (size_t)(k + 1) * FR;
         g.resid = k == 0 ? nullptr : B; g.ldr = VH; g.out_f32 = B;
         if (!gemv(g, s)) return false;
     }
@@ -435,47 +461,47 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     if (!run_conv(pre_conv_, A, F, 2, 1, nullptr, C, nullptr, 0, s)) return false;
     // 3) input_proj + bias -> x [F][VH]
     GemvParams ip;
-    ip.W = in_proj_; ip.N = VH; ip.K = LAT; ip.B = F; ip.pro = PRO_F32; ip.x = C; ip.ldx = LAT;
+    ip.W = in_proj_; ip.N = VH; ip.K = LAT; ip.B = FR; ip.pro = PRO_F32; ip.x = C; ip.ldx = LAT;
     ip.bias = in_proj_b_; ip.out_f32 = A; ip.ldo = VH;
     if (!gemv(ip, s)) return false;
     float *x = A;
     float *qkv = B;                                        // [F][3*LAT]
     uint16_t *att = reinterpret_cast<uint16_t *>(C);       // [F][LAT] f16
-    uint16_t *hm = reinterpret_cast<uint16_t *>(C) + (size_t)F * LAT;   // [F][ffn] f16
+    uint16_t *hm = reinterpret_cast<uint16_t *>(C) + (size_t)FR * LAT;   // [F][ffn] f16
     // large-M projections (M = frames or upsampled steps) run as 1-tap convs on the implicit-GEMM conv kernel over
     // pre-normalised f16 rows (norm_f16 reproduces the GEMM prologue's norm); the decode-shaped GEMM path stays for
     // the shapes the conv tiles do not cover
     const bool qkv_conv = VH % 32 == 0 && VH <= 1024 && VH % 4 == 0 && (3 * LAT) % 96 == 0;
     for (const Layer &L : layers_) {
         if (qkv_conv) {
-            if (!norm_f16(x, L.attn_norm, nullptr, 1e-5f, 0, xh_, F, VH, s)) return false;
+            if (!norm_f16(x, L.attn_norm, nullptr, 1e-5f, 0, xh_, FR, VH, s)) return false;
             ConvParams q;
-            q.xh = xh_; q.T_in = F; q.C_in = VH; q.n_taps = 1; q.taps[0] = ConvTap{L.qkv, 0};
-            q.y = qkv; q.C_out = 3 * LAT; q.M = F;
+            q.xh = xh_; q.T_in = FR; q.C_in = VH; q.n_taps = 1; q.taps[0] = ConvTap{L.qkv, 0};
+            q.y = qkv; q.C_out = 3 * LAT; q.M = FR;
             if (!conv(q, s)) return false;
         } else {
             GemvParams q;
-            q.W = L.qkv; q.N = 3 * LAT; q.K = VH; q.B = F; q.pro = PRO_RMS; q.x = x; q.ldx = VH; q.nw = L.attn_norm;
+            q.W = L.qkv; q.N = 3 * LAT; q.K = VH; q.B = FR; q.pro = PRO_RMS; q.x = x; q.ldx = VH; q.nw = L.attn_norm;
             q.eps = 1e-5f; q.out_f32 = qkv; q.ldo = 3 * LAT;
             if (!gemv(q, s)) return false;
         }
-        if (!attn_prefill(qkv, rope_, att, F, n_heads_, head_dim_, s)) return false;
+        if (!attn_prefill(qkv, rope_, att, F, n_heads_, head_dim_, s, nb_)) return false;
         GemvParams o;
-        o.W = L.o; o.N = VH; o.K = LAT; o.B = F; o.pro = PRO_F16; o.x = att; o.ldx = LAT;
+        o.W = L.o; o.N = VH; o.K = LAT; o.B = FR; o.pro = PRO_F16; o.x = att; o.ldx = LAT;
         o.scale = L.attn_scale; o.resid = x; o.ldr = VH; o.out_f32 = x; o.ldo = VH;
         if (!gemv(o, s)) return false;
         GemvParams gu;
-        gu.W = L.gu; gu.N = 2 * ffn_; gu.K = VH; gu.B = F; gu.pro = PRO_RMS; gu.x = x; gu.ldx = VH; gu.nw = L.ffn_norm;
+        gu.W = L.gu; gu.N = 2 * ffn_; gu.K = VH; gu.B = FR; gu.pro = PRO_RMS; gu.x = x; gu.ldx = VH; gu.nw = L.ffn_norm;
         gu.eps = 1e-5f; gu.act = ACT_SWIGLU; gu.out_f16 = hm; gu.ldo = ffn_;
         if (!gemv(gu, s)) return false;
         GemvParams dn;
-        dn.W = L.down; dn.N = VH; dn.K = ffn_; dn.B = F; dn.pro = PRO_F16; dn.x = hm; dn.ldx = ffn_;
+        dn.W = L.down; dn.N = VH; dn.K = ffn_; dn.B = FR; dn.pro = PRO_F16; dn.x = hm; dn.ldx = ffn_;
         dn.scale = L.ffn_scale; dn.resid = x; dn.ldr = VH; dn.out_f32 = x; dn.ldo = VH;
         if (!gemv(dn, s)) return false;
     }
     // final RMSNorm + output_proj + bias -> [F][LAT]   (:740-744)
     GemvParams op;
-    op.W = out_proj_; op.N = LAT; op.K = VH; op.B = F; op.pro = PRO_RMS; op.x = x; op.ldx = VH; op.nw = pre_norm_;
+    op.W = out_proj_; op.N = LAT; op.K = VH; op.B = FR; op.pro = PRO_RMS; op.x = x; op.ldx = VH; op.nw = pre_norm_;
     op.eps = 1e-5f; op.bias = out_proj_b_; op.out_f32 = B; op.ldo = LAT;
     if (!gemv(op, s)) return false;
     float *cur = B;
@@ -488,31 +514,28 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
         float *h = f0;                                   // conv-transpose output = residual [T1][LAT]
         if (!run_convT(U.ct, cur, (int)T, 2, 0, nullptr, h, (int)T1, s)) return false;
         float *dwo = f1;                                 // [T1][LAT]
-        if (!dwconv(h, U.dw, U.dw_b, dwo, (int)T1, LAT, U.dw_k, s)) return false;
-        uint16_t *pw = reinterpret_cast<uint16_t *>(cur);  // [T1][pw_dim] f16, cur is dead now
-        if ((size_t)T1 * U.pw_dim / 2 > (size_t)T1 * LAT + (size_t)T * LAT) {
-            // cur buffer is sized for the largest activation; pw fits by construction (ensure())
-        }
+        if (!dwconv(h, U.dw, U.dw_b, dwo, (int)T1, LAT, U.dw_k, s, nb_)) return false;
+        uint16_t *pw = reinterpret_cast<uint16_t *>(cur);  // [T1][pw_dim] f16, cur is dead now (ensure() sizes it)
         const bool pw_conv = LAT % 32 == 0 && LAT <= 1024 && U.pw_dim % 64 == 0 && U.pw_dim % 32 == 0 && LAT % 64 == 0;
         if (pw_conv) {
             // LayerNorm -> f16 rows, pw1 + bias + GELU -> f16, pw2 + bias, x gamma, + residual (in place)
-            if (!norm_f16(dwo, U.norm_w, U.norm_b, 1e-6f, 1, xh_, (int)T1, LAT, s)) return false;
+            if (!norm_f16(dwo, U.norm_w, U.norm_b, 1e-6f, 1, xh_, (int)T1 * nb_, LAT, s)) return false;
             ConvParams c1;
-            c1.xh = xh_; c1.T_in = (int)T1; c1.C_in = LAT; c1.n_taps = 1; c1.taps[0] = ConvTap{U.pw1, 0};
-            c1.C_out = U.pw_dim; c1.M = (int)T1; c1.bias = U.pw1_b; c1.act = 4; c1.y16 = pw;
+            c1.xh = xh_; c1.T_in = (int)T1 * nb_; c1.C_in = LAT; c1.n_taps = 1; c1.taps[0] = ConvTap{U.pw1, 0};
+            c1.C_out = U.pw_dim; c1.M = (int)T1 * nb_; c1.bias = U.pw1_b; c1.act = 4; c1.y16 = pw;
             if (!conv(c1, s)) return false;
             ConvParams c2;
-            c2.xh = pw; c2.T_in = (int)T1; c2.C_in = U.pw_dim; c2.n_taps = 1; c2.taps[0] = ConvTap{U.pw2, 0};
-            c2.C_out = LAT; c2.M = (int)T1; c2.bias = U.pw2_b; c2.scale = U.gamma; c2.resid = h; c2.y = h;
+            c2.xh = pw; c2.T_in = (int)T1 * nb_; c2.C_in = U.pw_dim; c2.n_taps = 1; c2.taps[0] = ConvTap{U.pw2, 0};
+            c2.C_out = LAT; c2.M = (int)T1 * nb_; c2.bias = U.pw2_b; c2.scale = U.gamma; c2.resid = h; c2.y = h;
             if (!conv(c2, s)) return false;
         } else {
             GemvParams p1;
-            p1.W = U.pw1; p1.N = U.pw_dim; p1.K = LAT; p1.B = (int)T1; p1.pro = PRO_LN; p1.x = dwo; p1.ldx = LAT;
+            p1.W = U.pw1; p1.N = U.pw_dim; p1.K = LAT; p1.B = (int)T1 * nb_; p1.pro = PRO_LN; p1.x = dwo; p1.ldx = LAT;
             p1.nw = U.norm_w; p1.nb = U.norm_b; p1.eps = 1e-6f; p1.bias = U.pw1_b; p1.act = ACT_GELU;
             p1.out_f16 = pw; p1.ldo = U.pw_dim;
             if (!gemv(p1, s)) return false;
             GemvParams p2;
-            p2.W = U.pw2; p2.N = LAT; p2.K = U.pw_dim; p2.B = (int)T1; p2.pro = PRO_F16; p2.x = pw; p2.ldx = U.pw_dim;
+            p2.W = U.pw2; p2.N = LAT; p2.K = U.pw_dim; p2.B = (int)T1 * nb_; p2.pro = PRO_F16; p2.x = pw; p2.ldx = U.pw_dim;
             p2.bias = U.pw2_b; p2.scale = U.gamma; p2.resid = h; p2.ldr = LAT; p2.out_f32 = h; p2.ldo = LAT;
             if (!gemv(p2, s)) return false;
         }
@@ -523,7 +546,7 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     // SnakeBeta of its predecessor's output, written by that conv's epilogue (snake + rounding once per element,
     // the f32 tensor itself only where a residual needs it): ha / hb ping-pong
     uint16_t *ha = xh_, *hb = xh2_;
-    if (!snake_f16(cur, nullptr, nullptr, ha, T, dec0_.ic, s)) return false;
+    if (!snake_f16(cur, nullptr, nullptr, ha, T * nb_, dec0_.ic, s)) return false;
     if (!conv16(dec0_, ha, (int)T, 6, 1, nullptr, nullptr, hb, &dec_[0].snake, s)) return false;   // snake(dec0) only
     std::swap(ha, hb);
     // 6) decoder blocks: SnakeBeta -> conv-transpose (trim K-s both sides) + bias -> 3 residual units (:551-620)
@@ -547,7 +570,7 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     }
     // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790): ha holds f16(snake(dec5)) of the stream
     if (dec6_.oc == 1 && dec6_.ic % 8 == 0 && dec6_.ic <= 112 && dec6_.k <= 8) {
-        if (!conv_out1(ha, dec6_.w, dec6_.b, pcm_dev, (int)T, dec6_.ic, dec6_.k, s)) return false;
+        if (!conv_out1(ha, dec6_.w, dec6_.b, pcm_dev, (int)T, dec6_.ic, dec6_.k, s, nb_)) return false;
         *n_out = T;
         return true;
     }
@@ -557,6 +580,7 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     for (int j = 0; j < dec6_.k; ++j) p6.taps[j] = ConvTap{dec6_.w + (size_t)j * dec6_.oc * dec6_.ic, j - 6};
     p6.dmin = -6; p6.dmax = dec6_.k - 1 - 6;
     p6.y = pcm_dev; p6.C_out = dec6_.oc; p6.M = (int)T + 6 - (dec6_.k - 1); p6.bias = dec6_.b; p6.act = 1;
+    p6.nb = nb_; p6.xbs = T; p6.ybs = p6.M;
     if (!conv(p6, s)) return false;
     *n_out = T;
     return true;
@@ -575,28 +599,56 @@ bool Vocoder::decode(const int32_t *codes, int F, int mode, float *pcm, int64_t 
         *n_out = n;
         return true;
     }
-    // CHUNK40 (trt_vocoder.cpp:98-170): independent fixed-length chunks (40 frames unless the caller names the
-    // engine's fixed_frames), zero-padded codes, chunk_frames*1920 kept
-    if (chunk_frames <= 0) { set_error("vocoder: chunk_frames must be > 0"); return false; }
-    const int FIX = chunk_frames;
-    if (!ensure(FIX)) return false;
-    std::vector<int32_t> cc((size_t)FIX * 16);
-    const int64_t full = full_len(FIX);
-    int64_t out = 0;
-    for (int off = 0; off < F; off += FIX) {
-        const int cf = std::min(FIX, F - off);
-        std::fill(cc.begin(), cc.end(), 0);
-        std::memcpy(cc.data(), codes + (size_t)off * 16, (size_t)cf * 16 * 4);
-        Q3T_HIP(hipMemcpyAsync(codes_, cc.data(), cc.size() * 4, hipMemcpyHostToDevice, stream_));
-        int64_t n = 0;
-        if (!decode_device(codes_, FIX, pcm_, &n, stream_)) return false;
-        const int64_t want = (int64_t)cf * 1920, have = std::min(want, full);
-        Q3T_HIP(hipMemcpyAsync(pcm + out, pcm_, (size_t)have * 4, hipMemcpyDeviceToHost, stream_));
-        Q3T_HIP(hipStreamSynchronize(stream_));
-        for (int64_t i = have; i < want; ++i) pcm[out + i] = 0.0f;
-        out += want;
+    // CHUNK40: every chunk of the utterance in shared launches
+    return decode_batch(1, &codes, &F, mode, &pcm, n_out, chunk_frames);
+}
+
+bool Vocoder::decode_batch(int n_utt, const int32_t *const *codes, const int *n_frames, int mode, float *const *pcm,
+                           int64_t *n_out, int chunk_frames) {
+    // a sequence = one utterance (FULL) or one chunk_frames-long chunk of one (CHUNK40, trt_vocoder.cpp:98-170:
+    // independent fixed-length chunks, zero-padded codes, chunk_frames*1920 samples kept)
+    struct Seq { int u, off, nf; };
+    std::vector<Seq> seqs;
+    if (mode != 0 && chunk_frames <= 0) { set_error("vocoder: chunk_frames must be > 0"); return false; }
+    for (int u = 0; u < n_utt; ++u) {
+        const int nf = std::max(n_frames[u], 0);
+        n_out[u] = n_samples(nf, mode);
+        if (mode == 0) {
+            if (nf > 0) seqs.push_back({u, 0, nf});
+        } else {
+            for (int off = 0; off < nf; off += chunk_frames) seqs.push_back({u, off, std::min(chunk_frames, nf - off)});
+        }
     }
-    *n_out = out;
+    // FULL: longest first, so each batch pads its utterances to a similar length (the decoder is causal end to end:
+    // frames appended after an utterance change none of its samples)
+    if (mode == 0) std::stable_sort(seqs.begin(), seqs.end(), [](const Seq &a, const Seq &b) { return a.nf > b.nf; });
+    std::vector<int32_t> hc;
+    for (size_t i = 0; i < seqs.size();) {
+        const int F = mode == 0 ? seqs[i].nf : chunk_frames;
+        const int nb = (int)std::min<size_t>(seqs.size() - i, (size_t)std::max(1, batch_frames_ / F));
+        if (!ensure(F, nb)) return false;
+        hc.assign((size_t)nb * F * 16, 0);
+        for (int j = 0; j < nb; ++j) {
+            const Seq &q = seqs[i + j];
+            std::memcpy(hc.data() + (size_t)j * F * 16, codes[q.u] + (size_t)q.off * 16, (size_t)q.nf * 16 * 4);
+        }
+        Q3T_HIP(hipMemcpyAsync(codes_, hc.data(), hc.size() * 4, hipMemcpyHostToDevice, stream_));
+        int64_t per = 0;   // samples per sequence of this batch
+        if (!decode_device(codes_, F, pcm_, &per, stream_, nb)) return false;
+        for (int j = 0; j < nb; ++j) {
+            const Seq &q = seqs[i + j];
+            const float *src = pcm_ + (size_t)j * per;
+            if (mode == 0) {
+                Q3T_HIP(hipMemcpyAsync(pcm[q.u], src, (size_t)n_out[q.u] * 4, hipMemcpyDeviceToHost, stream_));
+            } else {
+                const int64_t want = (int64_t)q.nf * 1920, have = std::min(want, per);
+                Q3T_HIP(hipMemcpyAsync(pcm[q.u] + (size_t)q.off * 1920, src, (size_t)have * 4, hipMemcpyDeviceToHost, stream_));
+                for (int64_t k = have; k < want; ++k) pcm[q.u][(size_t)q.off * 1920 + k] = 0.0f;
+            }
+        }
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        i += nb;
+    }
     return true;
 }
 

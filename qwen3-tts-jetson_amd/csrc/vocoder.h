@@ -19,9 +19,18 @@ public:
     int64_t n_samples(int n_frames, int mode) const;
     // chunk_frames: the fixed chunk length of the chunked mode (TRTVocoderDecoder::load_engine's fixed_frames)
     bool decode(const int32_t *codes_host, int n_frames, int mode, float *pcm_host, int64_t *n_out, int chunk_frames = 40);
-    // FULL decode of device-resident codes [F][16] into pcm_dev (capacity >= n_samples(F, 0)); ensure(F) first
-    bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s);
-    bool ensure(int n_frames);
+    // n_utt utterances through shared launches: FULL decodes run as utterance batches (every conv / attention launch
+    // covers up to batch_frames() frames of utterances padded to the batch's longest; the decoder is causal end to end,
+    // so each utterance's samples are exactly its own decode's); CHUNK40 decodes every chunk of every utterance as one
+    // batch of independent chunk_frames-long sequences.  pcm[u] capacity >= n_samples(n_frames[u], mode)
+    bool decode_batch(int n_utt, const int32_t *const *codes_host, const int *n_frames, int mode, float *const *pcm_host,
+                      int64_t *n_out, int chunk_frames = 40);
+    // FULL decode of device-resident codes [nb][F][16] into pcm_dev [nb][n_samples(F, 0)]; ensure(F, nb) first
+    bool decode_device(const int32_t *codes_dev, int n_frames, float *pcm_dev, int64_t *n_out, hipStream_t s, int nb = 1);
+    bool ensure(int n_frames, int nb = 1);
+    // frames per batched launch sequence (utterances x frames); scratch grows to this (~3 MB per frame)
+    int batch_frames() const { return batch_frames_; }
+    void set_batch_frames(int f) { batch_frames_ = f > 0 ? f : 4096; }
     bool loaded() const { return loaded_; }
     int n_usage_normalised() const { return n_usage_; }
     // algorithmic FLOPs of one FULL decode of F frames: 2*M*K*N over every conv (per tap), transposed conv, projection
@@ -56,6 +65,7 @@ private:
                 const Snake *next, hipStream_t s);
     bool convT16(const Conv &c, const uint16_t *xh, int T, int stride, int trim, float *y, int T_out, uint16_t *y16,
                  const Snake *next, hipStream_t s);
+    bool decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64_t *n_out, hipStream_t s);
 
     bool loaded_ = false;
     hipStream_t stream_ = nullptr;
@@ -72,7 +82,9 @@ private:
     Dec dec_[4];
     Snake dec5_;
     // scratch (grown by ensure)
-    int cap_frames_ = 0;
+    int cap_frames_ = 0, batch_frames_ = 4096;
+    size_t cap_big_ = 0, cap_ftot_ = 0, cap_pcm_ = 0;
+    int nb_ = 1;   // utterances of the decode in flight (conv launches carry it as grid z)
     float *buf_[3] = {nullptr, nullptr, nullptr};
     uint16_t *xh_ = nullptr;   // f16 (snake'd) conv input, one activation
     uint16_t *xh2_ = nullptr;  // second f16 activation: the decoder blocks ping-pong conv inputs written by epilogues

@@ -31,6 +31,11 @@ struct ConvParams {
     // from taps k = (phi + trim) % st + j*st at input offset (phi + trim - k) / st.  taps/dmin/dmax/M/so/ob unused
     const uint16_t *ct_w = nullptr;
     int ct_k = 0, ct_st = 0, ct_trim = 0, T_out = 0;
+    // utterance batch (grid z = nb x phases): nb independent sequences of the same length; utterance u's input rows
+    // start xbs rows after u-1's (x / xh), its output rows (y, resid, y16) ybs rows after.  Causal padding stays
+    // inside each utterance (rows outside [0, T_in) of its own segment read as 0)
+    int nb = 1;
+    int64_t xbs = 0, ybs = 0;
 };
 bool conv(const ConvParams &p, hipStream_t s);
 // out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
@@ -41,10 +46,12 @@ bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, i
 bool norm_f16(const float *x, const float *w, const float *b, float eps, int mode, uint16_t *out, int T, int C,
               hipStream_t s);
 // y[t] = tanh(bias + sum_j sum_ci w[j][ci] * xh[t + j - (K - 1)][ci]): the decoder's last conv (C_out = 1, K <= 8)
-bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s);
-bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s);
-// RoPE is applied to qkv's q and k columns in place
-bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s);
+// nb utterances of T rows each, back to back (xh [nb][T][C], y [nb][T])
+bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s,
+               int nb = 1);
+bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s, int nb = 1);
+// RoPE is applied to qkv's q and k columns in place; nb utterances of F frames each, causal within each
+bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s, int nb = 1);
 bool codes_cols(const int32_t *codes, int *cols, int F, int ncb, hipStream_t s);
 
 }  // namespace q3t

@@ -15,6 +15,16 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 // Tile 64 (m) x 64 (co); 4 waves as 2 x 2 of 32 x 32; K-chunk = 32 input channels.
 constexpr int CT_M = 64, CT_N = 64, CT_K = 32, CT_LD = CT_K + 8;   // LDS row: 32 f16 + 16 B pad
 
+// sin for SnakeBeta: reduce to [-0.5, 0.5] revolutions (v_rndne) and use the hardware v_sin_f32.  ocml's sinf is
+// ~30 VALU instructions with a range-reduction branch; the vocoder evaluates it twice per activation element of every
+// residual unit (~190 M per unit at 512 frames), which made it a quarter of the narrow blocks' time.  Its result is
+// rounded to f16 right after (x + sin^2 * ib), so the ~1e-6 absolute difference flips an f16 rounding only rarely
+// (PCM parity vs the oracle's sinf stays within the test's 1e-2 / RMS bar).
+__device__ __forceinline__ float snake_sin(float v) {
+    const float r = v * 0.15915494309189535f;   // 1 / (2 pi)
+    return __builtin_amdgcn_sinf(r - __builtin_rintf(r));
+}
+
 __device__ __forceinline__ float conv_act(float v, int act) {
     if (act == 1) return tanhf(v);
     if (act == 2) return fmaxf(v, 0.0f);
@@ -31,23 +41,30 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
     const int wm = wave >> 1, wn = wave & 1;
     const int m0 = blockIdx.x * CT_M, co0 = blockIdx.y * CT_N;
     const int win = CT_M + p.dmax - p.dmin;
+    const int ldy = p.ldy ? p.ldy : p.C_out;
+    const size_t ub = blockIdx.z;   // utterance
+    const float *px = p.x ? p.x + ub * p.xbs * p.C_in : nullptr;
+    const uint16_t *pxh = p.xh ? p.xh + ub * p.xbs * p.C_in : nullptr;
+    float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
+    const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
+    uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
     f32x16_t acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
     const int r = lane & 31, h = lane >> 5;
     for (int c0 = 0; c0 < p.C_in; c0 += CT_K) {
         // ---- stage the input window: f16 rows as they are (snake applied by snake_f16), or snake + f16 rounding here
-        if (p.xh) {
+        if (pxh) {
             for (int e = tid; e < win * (CT_K / 8); e += 256) {
                 const int row = e / (CT_K / 8), c8 = (e % (CT_K / 8)) * 8;
                 const int i = m0 + p.dmin + row;
                 uint4 u = make_uint4(0, 0, 0, 0);
                 if (i >= 0 && i < p.T_in && c0 + c8 < p.C_in) {
                     if ((p.C_in & 7) == 0) {
-                        u = *reinterpret_cast<const uint4 *>(p.xh + (size_t)i * p.C_in + c0 + c8);
+                        u = *reinterpret_cast<const uint4 *>(pxh + (size_t)i * p.C_in + c0 + c8);
                     } else {   // narrow channel counts (tiny test configs): element-wise, zero past C_in
                         uint16_t t8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                        for (int q = 0; q < 8; ++q) if (c0 + c8 + q < p.C_in) t8[q] = p.xh[(size_t)i * p.C_in + c0 + c8 + q];
+                        for (int q = 0; q < 8; ++q) if (c0 + c8 + q < p.C_in) t8[q] = pxh[(size_t)i * p.C_in + c0 + c8 + q];
                         u = *reinterpret_cast<const uint4 *>(t8);
                     }
                 }
@@ -61,16 +78,16 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
             if (i >= 0 && i < p.T_in) {
                 const int ci = c0 + cq;
                 if (ci + 3 < p.C_in && (p.C_in & 3) == 0) {
-                    const float4 u = *reinterpret_cast<const float4 *>(p.x + (size_t)i * p.C_in + ci);
+                    const float4 u = *reinterpret_cast<const float4 *>(px + (size_t)i * p.C_in + ci);
                     v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
                 } else {
-                    for (int q = 0; q < 4; ++q) if (ci + q < p.C_in) v[q] = p.x[(size_t)i * p.C_in + ci + q];
+                    for (int q = 0; q < 4; ++q) if (ci + q < p.C_in) v[q] = px[(size_t)i * p.C_in + ci + q];
                 }
                 if (p.snake_a) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if (ci + q < p.C_in) {
-                            const float sn = sinf(v[q] * p.snake_a[ci + q]);
+                            const float sn = snake_sin(v[q] * p.snake_a[ci + q]);
                             v[q] = v[q] + (sn * sn) * p.snake_ib[ci + q];
                         }
                     }
@@ -121,19 +138,18 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
         const int m = m0 + wm * 32 + row;
         if (m >= p.M) continue;
         const size_t t = (size_t)m * p.so + p.ob;
-        const int ldy = p.ldy ? p.ldy : p.C_out;
         float v = acc[reg] + b;
         if (p.scale) v *= p.scale[co];
-        if (p.resid) v = p.resid[t * ldy + co] + v;
+        if (pres) v = pres[t * ldy + co] + v;
         v = conv_act(v, p.act);
-        if (p.y) p.y[t * ldy + co] = v;
-        if (p.y16) {
+        if (py) py[t * ldy + co] = v;
+        if (py16) {
             float z = v;
             if (p.y16_a) {
-                const float sn = sinf(z * sa);
+                const float sn = snake_sin(z * sa);
                 z = z + (sn * sn) * sib;
             }
-            p.y16[t * p.C_out + co] = f2h(z);
+            py16[t * p.C_out + co] = f2h(z);
         }
     }
 }
@@ -158,8 +174,16 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     // launch geometry of this workgroup's conv: the params' own, or output phase blockIdx.z of a transposed conv
     int n_taps = p.n_taps, dmin = p.dmin, dmax = p.dmax, M = p.M, so = p.so, ob = p.ob;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nz = p.ct_st ? p.ct_st : 1;
+    const int ubi = blockIdx.z / nz;   // utterance; blockIdx.z % nz = output phase of a transposed conv
+    const size_t ub = ubi;
+    const int ldy = p.ldy ? p.ldy : p.C_out;
+    const uint16_t *pxh = p.xh + ub * p.xbs * p.C_in;
+    float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
+    const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
+    uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
     if (p.ct_st) {
-        const int phi = blockIdx.z, st = p.ct_st, k0 = (phi + p.ct_trim) % st;
+        const int phi = blockIdx.z - ubi * nz, st = p.ct_st, k0 = (phi + p.ct_trim) % st;
         n_taps = 0;
         for (int k = k0; k < p.ct_k && n_taps < CONV_MAX_TAPS; k += st) {
             const int dj = (phi + p.ct_trim - k) / st;
@@ -202,7 +226,7 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
             const int e = tid + q * 256, row = e >> 2, c8 = (e & 3) * 8, i = m0 + dmin + row;                       \
             const bool in = e < nx && i >= 0 && i < p.T_in;                                                           \
             const int ic = min(max(i, 0), p.T_in - 1);                                                                \
-            const uint4 u = ldg16(p.xh + (size_t)ic * p.C_in + (C0) + c8);                                           \
+            const uint4 u = ldg16(pxh + (size_t)ic * p.C_in + (C0) + c8);                                           \
             xr[q] = in ? u : make_uint4(0, 0, 0, 0);                                                                  \
         }                                                                                                             \
     } while (0)
@@ -262,7 +286,7 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
             const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
             const int m = m0 + wave * 32 * RB + i * 32 + row;
             if (m >= M) continue;
-            const size_t t = (size_t)m * so + ob, o = t * (p.ldy ? p.ldy : p.C_out) + co0 + q4;
+            const size_t t = (size_t)m * so + ob, o = t * ldy + co0 + q4;
             const size_t o16 = t * p.C_out + co0 + q4;
             const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
             float v[4] = {a.x, a.y, a.z, a.w};
@@ -274,16 +298,16 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
                 const float4 g = *reinterpret_cast<const float4 *>(p.scale + co0 + q4);
                 v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
             }
-            if (p.resid) {
-                const float4 rr = *reinterpret_cast<const float4 *>(p.resid + o);
+            if (pres) {
+                const float4 rr = *reinterpret_cast<const float4 *>(pres + o);
                 v[0] = rr.x + v[0]; v[1] = rr.y + v[1]; v[2] = rr.z + v[2]; v[3] = rr.w + v[3];
             }
             if (p.act) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) v[q] = conv_act(v[q], p.act);
             }
-            if (p.y) *reinterpret_cast<float4 *>(p.y + o) = make_float4(v[0], v[1], v[2], v[3]);
-            if (p.y16) {
+            if (py) *reinterpret_cast<float4 *>(py + o) = make_float4(v[0], v[1], v[2], v[3]);
+            if (py16) {
                 float z[4] = {v[0], v[1], v[2], v[3]};
                 if (p.y16_a) {   // the k_snake_f16 expression, term for term
                     const float4 sa = *reinterpret_cast<const float4 *>(p.y16_a + co0 + q4);
@@ -291,14 +315,14 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
                     const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const float sn = sinf(z[q] * av[q]);
+                        const float sn = snake_sin(z[q] * av[q]);
                         z[q] = z[q] + (sn * sn) * bv[q];
                     }
                 }
                 uint2 hv;
                 hv.x = (uint32_t)f2h(z[0]) | ((uint32_t)f2h(z[1]) << 16);
                 hv.y = (uint32_t)f2h(z[2]) | ((uint32_t)f2h(z[3]) << 16);
-                *reinterpret_cast<uint2 *>(p.y16 + o16) = hv;
+                *reinterpret_cast<uint2 *>(py16 + o16) = hv;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -318,7 +342,7 @@ static bool launch_mt(const ConvParams &p, hipStream_t s) {
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
         attr = true;
     }
-    const dim3 grid((p.M + MT - 1) / MT, p.C_out / NT, p.ct_st ? p.ct_st : 1);
+    const dim3 grid((p.M + MT - 1) / MT, p.C_out / NT, (p.ct_st ? p.ct_st : 1) * p.nb);
     hipLaunchKernelGGL((k_conv_mt<RB, NT, MINB>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
@@ -331,17 +355,20 @@ bool conv(const ConvParams &p, hipStream_t s) {
             set_error("conv: unsupported transposed launch");
             return false;
         }
+        if (p.nb <= 0) return true;
+        if (p.nb > 1 && (p.xbs < p.T_in || p.ybs < p.T_out)) { set_error("conv: bad utterance strides"); return false; }
         ConvParams q = p;
         q.M = (p.T_out + p.ct_st - 1) / p.ct_st;   // phase 0 has the most rows
         q.n_taps = (p.ct_k + p.ct_st - 1) / p.ct_st;
         q.dmin = 0;
         q.dmax = q.n_taps - 1;                      // taps of one phase are consecutive input rows
         if (q.M <= 0) return true;
-        const long tiles256 = (long)((q.M + 255) / 256) * (p.C_out / NT) * p.ct_st;
+        const long tiles256 = (long)((q.M + 255) / 256) * (p.C_out / NT) * p.ct_st * p.nb;
         if (NT == 96) return tiles256 >= 512 ? launch_mt<2, 96>(q, s) : launch_mt<1, 96>(q, s);
         return tiles256 >= 512 ? launch_mt<2, 64>(q, s) : launch_mt<1, 64>(q, s);
     }
-    if (p.M <= 0) return true;
+    if (p.M <= 0 || p.nb <= 0) return true;
+    if (p.nb > 1 && (p.xbs < p.T_in || p.ybs <= 0)) { set_error("conv: bad utterance strides"); return false; }
     if (p.n_taps < 1 || p.n_taps > CONV_MAX_TAPS || p.dmax - p.dmin > CT_MAXWIN - CT_M) {
         set_error("conv: unsupported tap layout");
         return false;
@@ -351,14 +378,14 @@ bool conv(const ConvParams &p, hipStream_t s) {
         // RB 2 (256-row tiles) unless that leaves fewer than two workgroups per CU to fill the chip.  1-tap convs over
         // narrow channel counts are bound by their epilogue traffic (f32 residual in, f32 + f16 out): 128-row tiles
         // at three workgroups per CU keep more of it in flight
-        const long tiles256 = (long)((p.M + 255) / 256) * (p.C_out / NT);
+        const long tiles256 = (long)((p.M + 255) / 256) * (p.C_out / NT) * p.nb;
         const bool big = tiles256 >= 512;
         if (big && p.n_taps == 1 && p.C_in <= 192) return NT == 96 ? launch_mt<1, 96, 3>(p, s) : launch_mt<1, 64, 3>(p, s);
         if (NT == 96) return big ? launch_mt<2, 96>(p, s) : launch_mt<1, 96>(p, s);
         return big ? launch_mt<2, 64>(p, s) : launch_mt<1, 64>(p, s);
     }
     if (!p.y && !p.y16) { set_error("conv: no output"); return false; }
-    const dim3 grid((p.M + CT_M - 1) / CT_M, (p.C_out + CT_N - 1) / CT_N);
+    const dim3 grid((p.M + CT_M - 1) / CT_M, (p.C_out + CT_N - 1) / CT_N, p.nb);
     hipLaunchKernelGGL(k_conv, grid, dim3(256), 0, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
@@ -373,7 +400,7 @@ __global__ void __launch_bounds__(256) k_snake_f16(const float *x, const float *
     if (a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {   // the k_conv staging expression, term for term
-            const float sn = sinf(y[q] * a[c + q]);
+            const float sn = snake_sin(y[q] * a[c + q]);
             y[q] = y[q] + (sn * sn) * ib[c + q];
         }
     }
@@ -447,6 +474,8 @@ __global__ void __launch_bounds__(256) k_conv_out1(const uint16_t *xh, const uin
     __shared__ __attribute__((aligned(16))) uint16_t xs[(CO1_T + CO1_MAXK) * CO1_MAXC];
     __shared__ float ws[CO1_MAXK * CO1_MAXC];
     const int t0 = blockIdx.x * CO1_T, tid = threadIdx.x;
+    xh += (size_t)blockIdx.y * T * C;   // utterance
+    y += (size_t)blockIdx.y * T;
     const int rows = CO1_T + K - 1, c8n = C / 8;
     for (int e = tid; e < rows * c8n; e += 256) {
         const int r = e / c8n, c8 = (e % c8n) * 8, i = t0 - (K - 1) + r;
@@ -473,10 +502,11 @@ __global__ void __launch_bounds__(256) k_conv_out1(const uint16_t *xh, const uin
     }
     y[t] = tanhf(acc + bias[0]);
 }
-bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s) {
+bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y, int T, int C, int K, hipStream_t s,
+               int nb) {
     if (C % 8 != 0 || C > CO1_MAXC || K > CO1_MAXK) { set_error("conv_out1: unsupported shape"); return false; }
-    if (T <= 0) return true;
-    hipLaunchKernelGGL(k_conv_out1, dim3((T + CO1_T - 1) / CO1_T), dim3(256), 0, s, xh, w, bias, y, T, C, K);
+    if (T <= 0 || nb <= 0) return true;
+    hipLaunchKernelGGL(k_conv_out1, dim3((T + CO1_T - 1) / CO1_T, nb), dim3(256), 0, s, xh, w, bias, y, T, C, K);
     Q3T_HIP(hipGetLastError());
     return true;
 }
@@ -486,6 +516,8 @@ bool conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *
 __global__ void __launch_bounds__(256) k_dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K) {
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (size_t)T * C) return;
+    x += (size_t)blockIdx.y * T * C;   // utterance
+    y += (size_t)blockIdx.y * T * C;
     const int t = (int)(idx / C), c = (int)(idx % C);
     float acc = 0.0f;
     for (int j = 0; j < K; ++j) {
@@ -494,10 +526,10 @@ __global__ void __launch_bounds__(256) k_dwconv(const float *x, const uint16_t *
     }
     y[idx] = acc + b[c];
 }
-bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s) {
+bool dwconv(const float *x, const uint16_t *w, const float *b, float *y, int T, int C, int K, hipStream_t s, int nb) {
     const size_t n = (size_t)T * C;
-    if (!n) return true;
-    hipLaunchKernelGGL(k_dwconv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, w, b, y, T, C, K);
+    if (!n || nb <= 0) return true;
+    hipLaunchKernelGGL(k_dwconv, dim3((unsigned)((n + 255) / 256), nb), dim3(256), 0, s, x, w, b, y, T, C, K);
     Q3T_HIP(hipGetLastError());
     return true;
 }
@@ -514,7 +546,7 @@ __global__ void k_rope_qk(float *qkv, const float *rope, int F, int nH) {
     const int total = F * 2 * nH * 32;
     if (idx >= total) return;
     const int i = idx & 31, hh = (idx >> 5) % (2 * nH), pos = idx / (64 * nH);
-    float *x = qkv + (size_t)pos * 3 * nH * D + hh * D;   // hh < nH: q head, else k head
+    float *x = qkv + ((size_t)blockIdx.y * F + pos) * 3 * nH * D + hh * D;   // utterance y; hh < nH: q head, else k
     const float c = rope[(size_t)pos * D + 2 * i], sn = rope[(size_t)pos * D + 2 * i + 1];
     const float x0 = x[i], x1 = x[i + 32];
     x[i] = x0 * c - x1 * sn;
@@ -529,6 +561,8 @@ __global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, uint16_t
     const int h = blockIdx.y, q0 = blockIdx.x * QT;
     const int tid = threadIdx.x, qi = tid >> 3, g = tid & 7;
     const int LD = 3 * nH * D;
+    qkv += (size_t)blockIdx.z * F * LD;   // utterance
+    out += (size_t)blockIdx.z * F * nH * D;
     const int qpos = q0 + qi;
     float q[D];
     {
@@ -613,12 +647,12 @@ __global__ void __launch_bounds__(256) k_attn_prefill(const float *qkv, uint16_t
         *reinterpret_cast<uint4 *>(out + (size_t)qpos * nH * D + h * D + g * 8) = o;
     }
 }
-bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s) {
+bool attn_prefill(float *qkv, const float *rope, uint16_t *out, int F, int nH, int D, hipStream_t s, int nb) {
     if (D != 64) { set_error("attn_prefill: head_dim must be 64"); return false; }
-    if (F <= 0) return true;
-    hipLaunchKernelGGL(k_rope_qk, dim3((F * 2 * nH * 32 + 255) / 256), dim3(256), 0, s, qkv, rope, F, nH);
+    if (F <= 0 || nb <= 0) return true;
+    hipLaunchKernelGGL(k_rope_qk, dim3((F * 2 * nH * 32 + 255) / 256, nb), dim3(256), 0, s, qkv, rope, F, nH);
     Q3T_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_attn_prefill, dim3((F + 31) / 32, nH), dim3(256), 0, s, qkv, out, F, nH);
+    hipLaunchKernelGGL(k_attn_prefill, dim3((F + 31) / 32, nH, nb), dim3(256), 0, s, qkv, out, F, nH);
     Q3T_HIP(hipGetLastError());
     return true;
 }

@@ -73,6 +73,9 @@ _lib.q3t_vocoder_flops.restype = C.c_double
 _lib.q3t_vocoder_flops.argtypes = [_P, C.c_int32]
 _lib.q3t_vocoder_decode.argtypes = [_P, _ip, C.c_int32, _I, _fp, C.POINTER(C.c_int64)]
 _lib.q3t_vocoder_decode_chunked.argtypes = [_P, _ip, C.c_int32, C.c_int32, C.c_int32, _fp, C.POINTER(C.c_int64)]
+_lib.q3t_vocoder_decode_batch.argtypes = [_P, C.c_int32, C.POINTER(C.c_void_p), _ip, _I, C.c_int32,
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
+_lib.q3t_vocoder_set_batch_frames.argtypes = [_P, C.c_int32]
 _lib.q3t_speaker_dim.argtypes = [_P]
 _lib.q3t_ctx_create_speaker.argtypes = [C.c_char_p, _I, C.POINTER(_P)]
 _lib.q3t_speaker_encode.argtypes = [_P, _fp, C.c_int32, _fp]
@@ -93,7 +96,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_generate_queue", "q3t_comm_unique_id", "q3t_ctx_create_shared",
            "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
-           "q3t_vocoder_decode_chunked", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
+           "q3t_vocoder_decode_chunked", "q3t_vocoder_decode_batch", "q3t_vocoder_set_batch_frames", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
            "q3t_tokenizer_decode", "q3t_talker_forward",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
@@ -351,6 +354,22 @@ class Engine:
         ns = C.c_int64(0)
         _check(_lib.q3t_vocoder_decode_chunked(self.h, codes, codes.shape[0], 16, int(chunk_frames), pcm, C.byref(ns)))
         return pcm[:ns.value]
+
+    def vocoder_batch(self, codes_list, mode=VOCODER_FULL, chunk_frames=40):
+        """several utterances through shared launches (q3t_vocoder_decode_batch): returns one PCM array per
+        utterance, each equal to vocoder(codes) (FULL) or vocoder_chunked(codes, chunk_frames) (CHUNK40)"""
+        cs = [np.ascontiguousarray(c, np.int32).reshape(-1, 16) for c in codes_list]
+        n = len(cs)
+        nf = np.array([c.shape[0] for c in cs], np.int32)
+        pcms = [np.zeros(max(self.vocoder_num_samples(int(f), mode), 1), np.float32) for f in nf]
+        cp = (C.c_void_p * max(n, 1))(*[c.ctypes.data for c in cs])
+        pp = (C.c_void_p * max(n, 1))(*[p.ctypes.data for p in pcms])
+        ns = (C.c_int64 * max(n, 1))()
+        _check(_lib.q3t_vocoder_decode_batch(self.h, n, cp, nf, int(mode), int(chunk_frames), pp, ns))
+        return [pcms[i][:ns[i]] for i in range(n)]
+
+    def vocoder_set_batch_frames(self, frames):
+        _check(_lib.q3t_vocoder_set_batch_frames(self.h, int(frames)))
 
     # ---- speaker encoder
     def speaker_dim(self):

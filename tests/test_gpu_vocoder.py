@@ -65,3 +65,40 @@ def test_vocoder_lengths(pair):
         assert eng.vocoder_num_samples(F, 0) == orc.vocoder_len(F, 0)
         assert eng.vocoder_num_samples(F, 1) == F * 1920
     assert eng.vocoder(np.zeros((0, 16), np.int32), 0).shape == (0,)
+
+
+def test_vocoder_batch_matches_single(pair):
+    """q3t_vocoder_decode_batch: utterances of different lengths through shared launches (padded to the batch's
+    longest, causal end to end) equal their single decodes up to the f32 summation order of the row GEMVs (whose
+    K split depends on the row count), and the oracle within PCM_TOL; a batch_frames cap forces several batches"""
+    cfg, eng, orc = pair
+    lens = [33, 7, 40, 1, 64, 12]
+    codes = [_codes(F, 100 + F) for F in lens]
+    for cap in (4096, 80):   # one batch / several batches of <= 80 frames
+        eng.vocoder_set_batch_frames(cap)
+        outs = eng.vocoder_batch(codes, 0)
+        worst = 0.0
+        for c, g in zip(codes, outs):
+            s = eng.vocoder(c, 0)
+            assert g.shape == s.shape
+            worst = max(worst, float(np.abs(g - s).max()))
+        print(f"{cfg} batch(cap {cap}) vs single: max|d|={worst:.3e}")
+        assert worst < 2e-3
+    eng.vocoder_set_batch_frames(4096)
+    for i in (0, 3):
+        o = orc.vocoder(codes[i], 0)
+        assert float(np.abs(outs[i] - o).max()) < PCM_TOL[cfg]
+
+
+def test_vocoder_batch_chunk40(pair):
+    """CHUNK40 through the batch entry: every 40-frame chunk of every utterance is one sequence of the batch"""
+    cfg, eng, orc = pair
+    lens = [47, 40, 5]
+    codes = [_codes(F, 200 + F) for F in lens]
+    outs = eng.vocoder_batch(codes, 1, 40)
+    for c, g in zip(codes, outs):
+        assert g.shape == (c.shape[0] * 1920,)
+        s = eng.vocoder_chunked(c, 40)
+        assert float(np.abs(g - s).max()) < 2e-3
+    o = orc.vocoder(codes[0], 1)
+    assert float(np.abs(outs[0] - o).max()) < PCM_TOL[cfg]
