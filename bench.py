@@ -233,8 +233,10 @@ def main():
         stats["frames_ms"] += fm
         if voc_mode is not None:
             t = time.perf_counter()
-            for c in codes:
-                eng.vocoder(c, voc_mode)
+            if len(codes) == 1:
+                eng.vocoder(codes[0], voc_mode)
+            else:   # utterance batches through shared launches (q3t_vocoder_decode_batch)
+                eng.vocoder_batch(codes, voc_mode)
             stats["vocoder_ms"] += (time.perf_counter() - t) * 1e3
         return codes
 
@@ -259,13 +261,16 @@ def main():
     # ---- vocoder (MFMA-bound): algorithmic FLOPs of the loaded conv / projection shapes over the
     # measured vocoder time of the step; SQ_INSTS_MFMA evidence per kernel in profiles/rNN_pmc_mfma_vocoder.txt
     voc_flops = eng.vocoder_flops(args.frames) if voc_mode == q3t.VOCODER_FULL else None
+    eng_voc_batch = 4096   # q3t_vocoder_set_batch_frames default
 
     def voc_roofline(voc_ms, n_utt, steps):
         if not voc_flops or voc_ms <= 0:
             return None
         tf = voc_flops * n_utt * steps / (voc_ms * 1e-3) / 1e12
-        return {"bound": "mfma", "kernel": "FULL vocoder of one utterance per call (k_conv_mt implicit-GEMM convs on "
-                                           "v_mfma_f32_32x32x16_f16, transposed convs one launch per conv)",
+        return {"bound": "mfma", "kernel": ("FULL vocoder of one utterance per call" if n_utt == 1 else
+                                            f"FULL vocoder, {n_utt} utterances in batches of {eng_voc_batch} frames") +
+                                           " (k_conv_mt implicit-GEMM convs on v_mfma_f32_32x32x16_f16, transposed convs "
+                                           "one launch per conv)",
                 "achieved": round(tf, 1), "peak": MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(tf / MFMA_PEAK_TFLOPS, 4), "flops_per_decode": round(voc_flops),
                 "ms_per_decode": round(voc_ms / (n_utt * steps), 3), "mfma_pmc": pmc_file("vocoder")}
@@ -287,7 +292,7 @@ def main():
         bres = {"config": (f"configs[2]: {batched} concurrent utterances x {args.frames} frames on one GPU"
                            if world == 1 else f"configs[3]: {world} x {batched} utterances x {args.frames} frames, "
                            f"utterance-sharded over {world} GPUs") +
-                          f", vocoder({args.vocoder}) per utterance, temp 0.9 top-k 50",
+                          f", vocoder({args.vocoder}) in utterance batches, temp 0.9 top-k 50",
                 "value": round(world * batched * args.frames / b_el, 1), "unit": "frames/s",
                 "ms_per_step": round(b_el * 1e3, 1), "n_gpus": world, "scaling": "weak",
                 "x_realtime": round(args.frames * FRAME_SEC * batched * world / b_el, 1),

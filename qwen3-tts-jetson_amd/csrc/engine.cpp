@@ -904,7 +904,8 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
                       const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval) {
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
-    auto lk = persist_lock(persist_, device_);
+    // only single-slot runs launch the persistent kernels: batched contexts on one device run concurrently
+    auto lk = persist_lock(persist_ && n_utt == 1, device_);
     StreamState st;
     st.delivered.assign(n_utt, 0);
     st.stop_at.assign(n_utt, -1);
@@ -1312,7 +1313,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
     const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
     if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
     if (gp.max_len > codes_max_len_) { set_error("max_len exceeds the code buffer"); return false; }
-    auto lk = persist_lock(persist_, device_);
+    auto lk = persist_lock(persist_ && S == 1, device_);
     if (!alloc_admission()) return false;
     q_slots_ = S;
     // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
@@ -1459,7 +1460,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
-    auto lk = persist_lock(persist_, device_);
+    auto lk = persist_lock(persist_ && S == 1, device_);
     std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
@@ -1492,7 +1493,7 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
     const int H = c_.hidden;
-    auto lk = persist_lock(persist_, device_);
+    auto lk = persist_lock(persist_ && S == 1, device_);
     for (int attempt = 0; attempt < 2; ++attempt) {
         Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
         Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
@@ -1513,7 +1514,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int H = c_.hidden;
     for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
-    auto lk = persist_lock(persist_, device_);
+    auto lk = persist_lock(persist_ && S == 1, device_);
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;

@@ -163,7 +163,11 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
 // Input: f16 rows (snake already applied).  Epilogue: bias, residual, tanh, f32 and/or f16(snake_next) outputs.
 constexpr int MT_KC = 32, MT_LDK = MT_KC + 8;   // LDS row: 32 f16 + 16 B pad (conflict-free ds_read_b128)
 
-template <int RB, int NT, int MINB = 2>
+// TW: most taps the variant stages per chunk (1, 3 or 7): the chunk's weights go through TW*NT*4/256 registers per
+// thread, loaded one chunk ahead like the input window.  1-tap variants (RB 1) also load their residual rows before
+// the main loop, so the epilogue's f32 reads are in flight while the GEMM runs (these convs are bound by that traffic).
+// ACT: 0 = no activation code in the epilogue (the decoder's convs), -1 = p.act at run time
+template <int RB, int NT, int MINB, int TW, int ACT>
 __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     constexpr int MT = 128 * RB, CB = NT / 32;
     extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
@@ -214,12 +218,37 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
         for (int j = 0; j < CB; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-    // x window staged through registers one chunk ahead (chunk c+1's loads in flight while chunk c multiplies);
-    // the chunk's weights (L2-resident: every workgroup reads the same ones) are loaded all at once and stored
+    // x window and the chunk's weights (L2-resident: every workgroup reads the same ones) staged through registers one
+    // chunk ahead: chunk c+1's loads are in flight while chunk c multiplies
     constexpr int XR = (MT + 64) * (MT_KC / 8) / 256;              // window rows <= MT + 64
-    constexpr int WR = (CONV_MAX_TAPS * NT * (MT_KC / 8) + 255) / 256;
+    constexpr int WR = (TW * NT * (MT_KC / 8) + 255) / 256;
     const int nx = win * (MT_KC / 8), nw = n_taps * NT * (MT_KC / 8);
-    uint4 xr[XR];
+    constexpr int Q = NT / 4;             // channel quads per row (epilogue)
+    constexpr int EK = 32 * Q / 64;       // epilogue iterations per 32-row slice
+    constexpr bool RP = TW == 1 && RB == 1;
+    // weights through registers one chunk ahead, except where that would spill (256-row x 96-channel 7-tap tiles:
+    // 96 accumulator + 44 weight + 20 window registers): there the chunk's weights are loaded and stored at once
+    constexpr bool WPF = !(TW == 7 && RB == 2 && NT == 96);
+    float4 rres[RP ? EK : 1];
+    if constexpr (RP) {
+        if (pres) {
+#pragma unroll
+            for (int k = 0; k < EK; ++k) {
+                const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
+                const int m = min(m0 + wave * 32 + row, M - 1);
+                rres[k] = *reinterpret_cast<const float4 *>(pres + ((size_t)m * so + ob) * ldy + co0 + q4);
+            }
+        }
+    }
+    uint4 xr[XR], wr[WPF ? WR : 1];
+#define Q3T_CONV_WLOAD(C0)                                                                                            \
+    do {                                                                                                              \
+        _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                              \
+            const int e = min(tid + q * 256, nw - 1);                                                                 \
+            const int j = e / (NT * 4), rem = e - j * (NT * 4), co = rem >> 2, c8 = (rem & 3) * 8;                   \
+            wr[q] = ldg16(tapw[j] + (size_t)(co0 + co) * p.C_in + (C0) + c8);                                        \
+        }                                                                                                             \
+    } while (0)
 #define Q3T_CONV_XLOAD(C0)                                                                                            \
     do {                                                                                                              \
         _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                              \
@@ -231,23 +260,36 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
         }                                                                                                             \
     } while (0)
     Q3T_CONV_XLOAD(0);
+    if constexpr (WPF) Q3T_CONV_WLOAD(0);
     for (int c0 = 0; c0 < p.C_in; c0 += MT_KC) {
 #pragma unroll
         for (int q = 0; q < XR; ++q) {
             const int e = tid + q * 256;
             if (e < nx) *reinterpret_cast<uint4 *>(xs + (e >> 2) * MT_LDK + (e & 3) * 8) = xr[q];
         }
-        // (no register array here: the compiler kept one in scratch memory; the loads of the unrolled loop still issue
-        // ahead of their LDS stores)
+        if constexpr (WPF) {
 #pragma unroll
-        for (int q = 0; q < WR; ++q) {
-            const int e = min(tid + q * 256, nw - 1);
-            const int j = e / (NT * 4), rem = e - j * (NT * 4), co = rem >> 2, c8 = (rem & 3) * 8;
-            const uint4 u = ldg16(tapw[j] + (size_t)(co0 + co) * p.C_in + c0 + c8);
-            if (tid + q * 256 < nw) *reinterpret_cast<uint4 *>(ws + (j * NT + co) * MT_LDK + c8) = u;
+            for (int q = 0; q < WR; ++q) {
+                const int e = tid + q * 256;
+                if (e < nw) {
+                    const int j = e / (NT * 4), rem = e - j * (NT * 4), co = rem >> 2, c8 = (rem & 3) * 8;
+                    *reinterpret_cast<uint4 *>(ws + (j * NT + co) * MT_LDK + c8) = wr[q];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < WR; ++q) {
+                const int e = min(tid + q * 256, nw - 1);
+                const int j = e / (NT * 4), rem = e - j * (NT * 4), co = rem >> 2, c8 = (rem & 3) * 8;
+                const uint4 u = ldg16(tapw[j] + (size_t)(co0 + co) * p.C_in + c0 + c8);
+                if (tid + q * 256 < nw) *reinterpret_cast<uint4 *>(ws + (j * NT + co) * MT_LDK + c8) = u;
+            }
         }
         __syncthreads();
-        if (c0 + MT_KC < p.C_in) Q3T_CONV_XLOAD(c0 + MT_KC);
+        if (c0 + MT_KC < p.C_in) {
+            Q3T_CONV_XLOAD(c0 + MT_KC);
+            if constexpr (WPF) Q3T_CONV_WLOAD(c0 + MT_KC);
+        }
         for (int j = 0; j < n_taps; ++j) {
             const uint16_t *ab = xs + (wave * 32 * RB + r + (tapdj[j] - dmin)) * MT_LDK + 8 * h;
             const uint16_t *bb = ws + (j * NT + r) * MT_LDK + 8 * h;
@@ -271,6 +313,18 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     // channels of a row: 16-B residual loads / f32 stores and 8-B f16 stores instead of one instruction per element
     constexpr int ELD = NT + 4;   // f32 row stride of the transposed slice
     float *es = reinterpret_cast<float *>(sm) + wave * 32 * ELD;
+    // the epilogue's per-channel operands of this tile, once in LDS (after the four slices): bias, scale,
+    // exp(alpha) and exp(-beta) of the next SnakeBeta
+    float *prm = reinterpret_cast<float *>(sm) + 4 * 32 * ELD;
+    if (tid < NT) {
+        const int co = co0 + tid;
+        prm[tid] = p.bias ? p.bias[co] : 0.0f;
+        prm[NT + tid] = p.scale ? p.scale[co] : 1.0f;
+        prm[2 * NT + tid] = p.y16_a ? p.y16_a[co] : 0.0f;
+        prm[3 * NT + tid] = p.y16_a ? p.y16_ib[co] : 0.0f;
+    }
+    __syncthreads();
+    constexpr int UF = RP ? EK : 4;
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
 #pragma unroll
@@ -280,9 +334,8 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
                 es[((reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)) * ELD + c * 32 + (lane & 31)] = acc[i][c][reg];
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the slice is in LDS (one wave writes and reads it)
         __builtin_amdgcn_wave_barrier();
-        constexpr int Q = NT / 4;             // channel quads per row
-#pragma unroll 4
-        for (int k = 0; k < 32 * Q / 64; ++k) {
+#pragma unroll UF
+        for (int k = 0; k < EK; ++k) {
             const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
             const int m = m0 + wave * 32 * RB + i * 32 + row;
             if (m >= M) continue;
@@ -291,27 +344,31 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
             const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
             float v[4] = {a.x, a.y, a.z, a.w};
             if (p.bias) {
-                const float4 b = *reinterpret_cast<const float4 *>(p.bias + co0 + q4);
+                const float4 b = *reinterpret_cast<const float4 *>(prm + q4);
                 v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
             }
             if (p.scale) {
-                const float4 g = *reinterpret_cast<const float4 *>(p.scale + co0 + q4);
+                const float4 g = *reinterpret_cast<const float4 *>(prm + NT + q4);
                 v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
             }
             if (pres) {
-                const float4 rr = *reinterpret_cast<const float4 *>(pres + o);
+                float4 rr;
+                if constexpr (RP) rr = rres[k];
+                else rr = *reinterpret_cast<const float4 *>(pres + o);
                 v[0] = rr.x + v[0]; v[1] = rr.y + v[1]; v[2] = rr.z + v[2]; v[3] = rr.w + v[3];
             }
-            if (p.act) {
+            if constexpr (ACT != 0) {
+                if (p.act) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = conv_act(v[q], p.act);
+                    for (int q = 0; q < 4; ++q) v[q] = conv_act(v[q], p.act);
+                }
             }
             if (py) *reinterpret_cast<float4 *>(py + o) = make_float4(v[0], v[1], v[2], v[3]);
             if (py16) {
                 float z[4] = {v[0], v[1], v[2], v[3]};
                 if (p.y16_a) {   // the k_snake_f16 expression, term for term
-                    const float4 sa = *reinterpret_cast<const float4 *>(p.y16_a + co0 + q4);
-                    const float4 sb = *reinterpret_cast<const float4 *>(p.y16_ib + co0 + q4);
+                    const float4 sa = *reinterpret_cast<const float4 *>(prm + 2 * NT + q4);
+                    const float4 sb = *reinterpret_cast<const float4 *>(prm + 3 * NT + q4);
                     const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -329,23 +386,37 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     }
 }
 
-template <int RB, int NT, int MINB = 2>
-static bool launch_mt(const ConvParams &p, hipStream_t s) {
+template <int RB, int NT, int MINB, int TW, int ACT>
+static bool launch_mt2(const ConvParams &p, hipStream_t s) {
     constexpr int MT = 128 * RB;
     // staging area (input window + the chunk's weights of every tap), reused by the epilogue's transposed slices
     // (transposed launches: p.n_taps / dmin / dmax carry the largest tap count and span over the phases)
     const size_t lds = std::max(((size_t)(MT + p.dmax - p.dmin) + (size_t)p.n_taps * NT) * MT_LDK * 2,
-                                (size_t)4 * 32 * (NT + 4) * 4);
+                                (size_t)4 * 32 * (NT + 4) * 4 + (size_t)4 * NT * 4);
     static bool attr = false;
     if (!attr) {
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_mt<RB, NT, MINB>),
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_mt<RB, NT, MINB, TW, ACT>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
         attr = true;
     }
     const dim3 grid((p.M + MT - 1) / MT, p.C_out / NT, (p.ct_st ? p.ct_st : 1) * p.nb);
-    hipLaunchKernelGGL((k_conv_mt<RB, NT, MINB>), grid, dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_conv_mt<RB, NT, MINB, TW, ACT>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
+}
+template <int RB, int NT, int MINB, int TW>
+static bool launch_mt1(const ConvParams &p, hipStream_t s) {
+    return p.act ? launch_mt2<RB, NT, MINB, TW, -1>(p, s) : launch_mt2<RB, NT, MINB, TW, 0>(p, s);
+}
+template <int RB, int NT, int MINB = 2>
+static bool launch_mt(const ConvParams &p, hipStream_t s) {
+    if constexpr (MINB == 3) {   // the 1-tap narrow-channel variant only
+        return launch_mt1<RB, NT, MINB, 1>(p, s);
+    } else {
+        if (p.n_taps <= 1) return launch_mt1<RB, NT, MINB, 1>(p, s);
+        if (p.n_taps <= 3) return launch_mt1<RB, NT, MINB, 3>(p, s);
+        return launch_mt1<RB, NT, MINB, 7>(p, s);
+    }
 }
 
 bool conv(const ConvParams &p, hipStream_t s) {
