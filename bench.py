@@ -184,9 +184,12 @@ def main():
     ap.add_argument("--batched", type=int, default=64,
                     help="secondary measurement: this many concurrent utterances per GPU (BASELINE configs[2] at N=1, "
                          "configs[3] at N>1: weak scaling, value over all ranks); 0 = off")
-    ap.add_argument("--serve", type=int, default=256,
+    ap.add_argument("--serve", type=int, default=512,
                     help="serving measurement (N=1): this many utterances with natural EOS (prompt lengths 10..120 "
-                         "tokens) through `batched` slots, lock-step batches vs continuous batching; 0 = off")
+                         "tokens) through --serve-slots slots, lock-step batches vs continuous batching; 0 = off")
+    ap.add_argument("--serve-slots", type=int, default=256,
+                    help="slots of the serving measurement (one context: the batched path is latency-bound at 64 "
+                         "slots, 288 GB of HBM holds the KV of 256)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -199,7 +202,8 @@ def main():
     voc_mode = {"full": q3t.VOCODER_FULL, "chunk40": q3t.VOCODER_CHUNK40, "none": None}[args.vocoder]
     max_ctx = max(args.frames, args.roofline_pos) + 32
     batched = args.batched
-    slots = max(args.batch, batched)
+    serve_slots = args.serve_slots if args.serve > 0 and world == 1 else 0
+    slots = max(args.batch, batched, serve_slots)
     weights = "local GGUF read"
     if world > 1:
         # rank 0 writes the synthetic GGUFs (node-local), then publishes the RCCL id; the others wait for it
@@ -312,7 +316,7 @@ def main():
     # ---- serving: utterances of different lengths, lock-step batches (every batch runs until its
     # longest utterance ends) vs continuous batching (a finished slot is refilled between frames); codes only
     sres = None
-    if args.serve > 0 and batched > 0 and world == 1:
+    if args.serve > 0 and serve_slots > 0 and world == 1:
         rng = np.random.default_rng(2024)
         sp_prompts = []
         for i in range(args.serve):
@@ -321,22 +325,23 @@ def main():
                                             for j in range(n - 4)])
         sp_spk = [np.zeros(H, np.float32)] * args.serve
         kw = dict(max_len=args.frames, temperature=0.9, top_k=50, repetition_penalty=1.05, seed=4242)
-        eng.generate_queue(sp_prompts[:2 * batched], speakers=sp_spk[:2 * batched], max_active=batched,
+        eng.generate_queue(sp_prompts[:2 * serve_slots], speakers=sp_spk[:2 * serve_slots], max_active=serve_slots,
                            **dict(kw, max_len=2))   # warm-up: every slot's single-slot prefill graph
+        eng.generate(sp_prompts[:serve_slots], speakers=sp_spk[:serve_slots], **dict(kw, max_len=2))
         eng.synchronize()
         t0 = time.perf_counter()
         lock = []
-        for b0 in range(0, args.serve, batched):
-            lock += eng.generate(sp_prompts[b0:b0 + batched], speakers=sp_spk[b0:b0 + batched], **kw)
+        for b0 in range(0, args.serve, serve_slots):
+            lock += eng.generate(sp_prompts[b0:b0 + serve_slots], speakers=sp_spk[b0:b0 + serve_slots], **kw)
         eng.synchronize()
         t_lock = time.perf_counter() - t0
         t0 = time.perf_counter()
-        queue = eng.generate_queue(sp_prompts, speakers=sp_spk, max_active=batched, **kw)
+        queue = eng.generate_queue(sp_prompts, speakers=sp_spk, max_active=serve_slots, **kw)
         eng.synchronize()
         t_queue = time.perf_counter() - t0
         f_lock, f_queue = sum(len(c) for c in lock), sum(len(c) for c in queue)
         sres = {"config": f"{args.serve} utterances (prompts of 10..120 tokens, natural EOS, max {args.frames} frames) "
-                          f"through {batched} slots, codes only (no vocoder), temp 0.9 top-k 50",
+                          f"through {serve_slots} slots of one context, codes only (no vocoder), temp 0.9 top-k 50",
                 "lockstep": {"frames": f_lock, "s": round(t_lock, 3), "value": round(f_lock / t_lock, 1),
                              "unit": "frames/s"},
                 "continuous": {"frames": f_queue, "s": round(t_queue, 3), "value": round(f_queue / t_queue, 1),

@@ -293,10 +293,12 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 // tickets, last-arriver combine) ran at ~2.9 TB/s; here each workgroup walks its context in 64-position chunks with
 // the next chunk's K/V loads in flight (register double buffer), and each wave keeps its own online-softmax state
 // (max, sum, 8-dim accumulator per head) over its 16 positions of every chunk, so no barrier is taken per chunk; the
-// four waves merge once at the end.  Same per-position arithmetic as k_attn (explicit roundings); the rescaling order
-// of the online softmax differs from the split combine (f32).
+// four waves merge once at the end.  The per-position arithmetic differs from k_attn's in summation order (dot2 pairs)
+// and exponential (v_exp_f32), the rescaling order of the online softmax from the split combine (f32): the batched
+// family is checked against the oracle (teacher-forced decisions), not bit for bit against the single-slot kernels.
 //
-// The kernel is issue-bound, not HBM-bound (one wave per SIMD saw every instruction's latency): every chunk but the
+// The kernel is issue-bound, not HBM-bound (one wave per SIMD saw every instruction's latency): scores are
+// v_dot2_f32_f16 on the packed K registers, softmax exponentials v_exp_f32 (__expf), and every chunk but the
 // last is whole (all 64 positions <= pos), so it runs without position masks, without the new-row branch and without
 // the empty-wave test; the new K/V row (pos) is patched into the last chunk's registers once, from LDS (exact: the
 // LDS copy is the f16 value).
@@ -366,11 +368,17 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
         p.vc[head_off + (size_t)pos * D + e] = vh_s[e];
     }
     const float kq_scale = 1.0f / sqrtf((float)D);
-    float q8[R][8];
+    // q is f16-exact (f16r above): the scores are v_dot2_f32_f16 over f16 pairs straight from the K registers (no
+    // per-element conversion; f16 products are exact in f32)
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    h2_t q2[R][4];
 #pragma unroll
     for (int h = 0; h < R; ++h)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) q8[h][e] = q_s[h][li * 8 + e];
+        for (int e = 0; e < 4; ++e) {
+            q2[h][e].x = (_Float16)q_s[h][li * 8 + 2 * e];
+            q2[h][e].y = (_Float16)q_s[h][li * 8 + 2 * e + 1];
+        }
 
     float m[R], l[R], acc[R][8];
 #pragma unroll
@@ -388,13 +396,12 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
             ok[pi] = !LAST || c * 64 + pi * 16 + pg <= pos;
-            float k8[8];
-            unpack8_cvt(kr[pi], k8);
+            const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
 #pragma unroll
             for (int h = 0; h < R; ++h) {
                 float s = 0.0f;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);
+                for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kw[e]), q2[h][e], s, false);
                 s = group_sum<LPP>(s);
                 sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
             }
@@ -407,7 +414,7 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
             mc = rows_max(mc);                      // this wave's 16 positions of the chunk
             const float mn = fmaxf(m[h], mc);
             if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
-            const float alpha = expf(__fsub_rn(m[h], mn));
+            const float alpha = __expf(__fsub_rn(m[h], mn));
             l[h] *= alpha;
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[h][e] *= alpha;
@@ -419,7 +426,7 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
             unpack8_cvt(vr[pi], v8);
 #pragma unroll
             for (int h = 0; h < R; ++h) {
-                const float pr = ok[pi] ? expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
+                const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
                 l[h] += pr;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, acc[h][e]);

@@ -476,9 +476,13 @@ struct StackInput {
 // layer (code-predictor pass 0 has no head).
 static int splitk_for(int N, int S, int K) {
     const int tiles = (N / 32) * ((S + 31) / 32), nch = K / 256;
+    // K chunks per slice must be one of the GEMM kernel's instantiations (gemm_mfma_supported)
+    auto ok = [&](int ks) { const int nk = nch % ks == 0 ? nch / ks : 0; return nk == 1 || nk == 2 || nk == 3 || nk == 4 || nk == 8 || nk == 12; };
     for (int ks : {1, 2, 3, 4})
-        if (nch % ks == 0 && tiles * ks >= 256) return ks;
-    return nch % 4 == 0 ? 4 : nch % 3 == 0 ? 3 : nch % 2 == 0 ? 2 : 1;
+        if (ok(ks) && tiles * ks >= 256) return ks;
+    for (int ks : {4, 3, 2})
+        if (ok(ks)) return ks;
+    return 1;
 }
 static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,

@@ -34,8 +34,10 @@ ref = run(base, N, 1)
 base.synchronize()
 t1 = time.perf_counter() - t
 print(f"1 context x {N} slots: {t1 * 1e3:.1f} ms, {N * F / t1:.0f} frames/s", flush=True)
-for R in (2, 4):
-    n = N // R
+RS = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2, 4]
+PER = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # slots per replica (0: N / R)
+for R in RS:
+    n = PER or N // R
     engs = [base.replica(0, n, F + 32) for _ in range(R)]
     for e in engs:
         run(e, n, 1)
@@ -52,7 +54,7 @@ for R in (2, 4):
     for x in th:
         x.join()
     tr = time.perf_counter() - t
-    print(f"{R} contexts x {n} slots concurrently: {tr * 1e3:.1f} ms, {N * F / tr:.0f} frames/s", flush=True)
+    print(f"{R} contexts x {n} slots concurrently: {tr * 1e3:.1f} ms, {R * n * F / tr:.0f} frames/s", flush=True)
     # serial for comparison
     t = time.perf_counter()
     for i in range(R):
