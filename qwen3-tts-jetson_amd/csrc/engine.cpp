@@ -460,6 +460,7 @@ bool Engine::persist_error() {
 
 struct StackInput {
     int pro = PRO_RMS;
+    bool prenormed = false;              // batched: x / xn already hold layer 0's input (select_embed_norm)
     const float *x = nullptr;
     GatherSum gs;
     SelectSpec sel;                      // PRO_SEL_G1: selection of the gathered token
@@ -496,13 +497,15 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
     const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
     ResidNorm rn;
     rn.S = S; rn.H = H; rn.eps = c.eps; rn.x = x; rn.xn = xn;
-    if (in0 && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
+    if (in0 && in0->prenormed) {
+        // the previous launch (token selection) gathered and normalised layer 0's input
+    } else if (in0 && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
         if (!gather_sum(in0->gs, in0->pro == PRO_RMS_G16 ? 16 : 1, S, H, x, H, s)) return false;
     } else if (in0 && in0->x) {
         rn.xin = in0->x;   // copied into the residual stream by the norm
     }
     rn.nw = layers[0].attn_norm;
-    if (!resid_norm(rn, s)) return false;
+    if (!(in0 && in0->prenormed) && !resid_norm(rn, s)) return false;
     rn.xin = nullptr;
     for (size_t il = 0; il < layers.size(); ++il) {
         const DevLayer &l = layers[il];
@@ -628,7 +631,7 @@ SelectSpec Engine::select_spec(int mode, const GenParams &gp, int frame_offset, 
 // gather_input: the step embedding (tts_transformer.cpp:2529-2553) is assembled by layer 0's QKV prologue from the
 // frame's 16 codes (PRO_RMS_G16) instead of being read from x_
 // select_next: the codec head's last workgroup also selects CB0 of the NEXT frame (frame_ + 1) in the same launch
-bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next) {
+bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
@@ -656,6 +659,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         in0.gs.tok = tokens_; in0.gs.tok_ld = 16; in0.gs.tabs = tabs16_dev_;
         in0.gs.tr = trailing_; in0.gs.tr_len = trailing_len_; in0.gs.frame = frame_;
         in0.gs.tr_ld = max_trailing_ * H; in0.gs.pad = tts_pad_;
+        in0.prenormed = prenormed;
     }
     const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
     if (mm) {
@@ -683,7 +687,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
 // Pass inputs are assembled by layer 0's QKV prologue: pass 0 the talker hidden state, pass 1 codec_embd[code 0],
 // pass p >= 2 code_pred.codec_embd[p-2][code p-1]; the raw row lands in cpx_ (the pass's residual stream).
 // logits_host (tests only, never captured): every head's logits copied out after its GEMV.
-bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
+bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool talker_next) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
     std::vector<float> lg;
@@ -704,8 +708,11 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
     }
     const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
     const bool defer = fsel_all && defer_cp_select_;
+    bool next_prenormed = false;   // batched: this pass's input was prepared by the previous selection launch
     for (int p = 0; p < 16; ++p) {
         StackInput in0;
+        in0.prenormed = next_prenormed;
+        next_prenormed = false;
         if (p == 0) {
             in0.pro = PRO_RMS; in0.x = hidden_;
         } else {
@@ -745,6 +752,24 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
             for (int b = 0; b < S; ++b)
                 std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
         }
+        if (mm && (step < 14 || talker_next)) {
+            // batched: the selecting workgroup of each slot also gathers and normalises the next stage's input (the
+            // next pass's table row, or the talker step embedding after the last pass)
+            EmbedNorm en;
+            en.gs.tok = tokens_; en.gs.tok_ld = 16;
+            if (step < 14) {
+                en.nt = 1; en.gs.tok_col0 = step + 1; en.gs.tab0 = cp_embd_[step];
+                en.x = cpx_; en.nw = CP_[0].attn_norm;
+            } else {
+                en.nt = 16; en.gs.tabs = tabs16_dev_; en.gs.tr = trailing_; en.gs.tr_len = trailing_len_;
+                en.gs.frame = frame_; en.gs.tr_ld = max_trailing_ * H; en.gs.pad = tts_pad_;
+                en.x = x_; en.nw = L_[0].attn_norm;
+            }
+            en.xn = xn_; en.eps = c_.eps; en.H = H;
+            if (!select_embed_norm(select_spec(SEL_CP, gp_, 0, step), cp_logits_, en, S, s)) return false;
+            next_prenormed = true;
+            continue;
+        }
         if (!fsel && !(defer && step < 14) && !select_tokens(select_spec(SEL_CP, gp_, 0, step), cp_logits_, S, s)) return false;
     }
     return true;
@@ -754,8 +779,10 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host) {
 // the CB0 of frame f+1 is chosen inside frame f's talker head launch (frame 0's by generate() after the prefill).
 bool Engine::enqueue_frame(int S, hipStream_t s) {
     if (!fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, s)) return false;
-    if (!enqueue_cp_frame(S, s)) return false;
-    if (!enqueue_talker(S, s, true, fused_select_)) return false;
+    // batched: the last code-predictor selection also assembles and normalises the talker step's input
+    const bool mm = S >= gemm_mfma_min_batch();
+    if (!enqueue_cp_frame(S, s, nullptr, mm)) return false;
+    if (!enqueue_talker(S, s, true, fused_select_, mm)) return false;
     return advance(pos_, frame_, done_, S, s);
 }
 

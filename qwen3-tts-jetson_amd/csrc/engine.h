@@ -149,9 +149,9 @@ private:
                        const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval,
                        StreamState &st, bool *fault);
     bool enqueue_talker_step(int S, hipStream_t s);
-    bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next);
+    bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed = false);
     SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;
-    bool enqueue_cp_frame(int S, hipStream_t s, float *logits_host = nullptr);
+    bool enqueue_cp_frame(int S, hipStream_t s, float *logits_host = nullptr, bool talker_next = false);
     bool enqueue_frame(int S, hipStream_t s);
     bool enqueue_text_projection(int n_rows, hipStream_t s);
     bool graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t));

@@ -174,6 +174,21 @@ struct ResidNorm {
 };
 bool resid_norm(const ResidNorm &r, hipStream_t s);
 
+// batched: the selection launch also prepares the NEXT stage's input (one workgroup per slot): the token selected
+// for slot b, then x[b] = the GatherSum row (nt = 1: the next code-predictor pass; nt = 16: the talker step
+// embedding, the selected token among its 16), then xn[b] = f16(RMSNorm(x[b]) * nw) -- k_gather_sum + k_resid_norm
+// arithmetic, so the fused and the three-launch forms give the same bits
+struct EmbedNorm {
+    GatherSum gs;
+    int nt = 0;
+    float *x = nullptr;
+    uint16_t *xn = nullptr;
+    const float *nw = nullptr;
+    float eps = 1e-6f;
+    int H = 0;
+};
+bool select_embed_norm(const SelectSpec &sp, const float *logits, const EmbedNorm &en, int S, hipStream_t s);
+
 // src/trt_cuda_kernels.cu drop-ins (C ABI wrappers in capi.cpp)
 void launch_f32_to_f16(const float *in, uint16_t *out, int n, hipStream_t s);
 void launch_argmax_f32(const float *in, int32_t *out, int n, hipStream_t s);

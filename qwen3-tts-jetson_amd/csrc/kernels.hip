@@ -218,6 +218,71 @@ __global__ void __launch_bounds__(256) k_resid_norm(const ResidNorm r) {
     h.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
     *reinterpret_cast<uint2 *>(r.xn + o) = h;
 }
+__global__ void __launch_bounds__(256) k_select_embed_norm(const SelectSpec sp, const float *logits, const EmbedNorm en) {
+    __shared__ SelLds S;
+    __shared__ double scr[4];
+    __shared__ int stok;
+    const int b = blockIdx.x, t = threadIdx.x, k = 4 * t;
+    const int tok = select_token<false>(sp, logits + (size_t)b * sp.V, b, S);
+    if (t == 0) {
+        if (tok >= 0) select_commit(sp, b, tok);
+        stok = tok;
+    }
+    __syncthreads();
+    const int sel_col = sp.mode == SEL_CB0 ? 0 : sp.step + 1;   // the column this launch selected
+    const GatherSum &gs = en.gs;
+    auto token = [&](int col) {   // finished slots (no selection) keep the token already in the table
+        return col == sel_col && stok >= 0 ? stok : gs.tok[(size_t)b * gs.tok_ld + col];
+    };
+    const bool ok = k < en.H;
+    const int kk = ok ? k : 0;
+    float a[4];
+    {
+        const uint16_t *r0 = en.nt == 1 ? gs.tab0 + (size_t)token(gs.tok_col0) * en.H : gs.tabs[0] + (size_t)token(0) * en.H;
+        const uint2 u = *reinterpret_cast<const uint2 *>(r0 + kk);
+        a[0] = h2f(u.x & 0xffff); a[1] = h2f(u.x >> 16); a[2] = h2f(u.y & 0xffff); a[3] = h2f(u.y >> 16);
+    }
+    if (en.nt == 16) {
+        for (int j = 1; j < 16; ++j) {
+            const uint2 u = *reinterpret_cast<const uint2 *>(gs.tabs[j] + (size_t)token(j) * en.H + kk);
+            a[0] += h2f(u.x & 0xffff); a[1] += h2f(u.x >> 16); a[2] += h2f(u.y & 0xffff); a[3] += h2f(u.y >> 16);
+        }
+        const int fr = gs.frame[b];
+        const float *extra = fr < gs.tr_len[b] ? gs.tr + (size_t)b * gs.tr_ld + (size_t)fr * en.H : gs.pad + (size_t)b * en.H;
+        const float4 e = *reinterpret_cast<const float4 *>(extra + kk);
+        a[0] += e.x; a[1] += e.y; a[2] += e.z; a[3] += e.w;
+    }
+    float4 x = ok ? make_float4(a[0], a[1], a[2], a[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const size_t o = (size_t)b * en.H + kk;
+    if (ok) *reinterpret_cast<float4 *>(en.x + o) = x;
+    double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);
+    ss = wave_sum_d(ss);
+    if ((t & 63) == 0) scr[t >> 6] = ss;
+    __syncthreads();
+    ss = (scr[0] + scr[1]) + (scr[2] + scr[3]);
+    if (!ok) return;
+    const float scale = 1.0f / sqrtf((float)(ss / en.H) + en.eps);
+    const float4 w = *reinterpret_cast<const float4 *>(en.nw + k);
+    const float y0 = (x.x * scale) * w.x, y1 = (x.y * scale) * w.y, y2 = (x.z * scale) * w.z, y3 = (x.w * scale) * w.w;
+    uint2 h;
+    h.x = (uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16);
+    h.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
+    *reinterpret_cast<uint2 *>(en.xn + o) = h;
+}
+bool select_embed_norm(const SelectSpec &sp, const float *logits, const EmbedNorm &en, int S, hipStream_t s) {
+    if (sp.V > 256 * SEL_VPT_MAX || sp.V <= 0) { set_error("select: vocab must be in (0, 4096]"); return false; }
+    if (en.H > 1024 || en.H % 4 != 0 || !en.x || !en.xn || !en.nw || (en.nt != 1 && en.nt != 16) ||
+        (en.nt == 1 && !en.gs.tab0) || (en.nt == 16 && !(en.gs.tabs && en.gs.frame && en.gs.tr_len && en.gs.pad)) ||
+        !en.gs.tok) {
+        set_error("select_embed_norm: bad parameters");
+        return false;
+    }
+    if (S <= 0) return true;
+    hipLaunchKernelGGL(k_select_embed_norm, dim3(S), dim3(256), 0, s, sp, logits, en);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 bool resid_norm(const ResidNorm &r, hipStream_t s) {
     if (r.S <= 0) return true;
     if (r.H > 1024 || r.H % 4 != 0 || !r.x || !r.nw || !r.xn || (r.parts && (r.ksplit < 1 || r.ksplit > 8))) {
