@@ -4,6 +4,7 @@
 #include "vocoder_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace q3t {
 
@@ -419,6 +420,13 @@ static bool launch_mt(const ConvParams &p, hipStream_t s) {
     }
 }
 
+#ifdef Q3T_DEV
+// development builds: Q3T_CONV_VARIANT picks another tile shape for the multi-tap convs (tools/dev experiments)
+static const int g_conv_variant = [] { const char *e = std::getenv("Q3T_CONV_VARIANT"); return e ? std::atoi(e) : 0; }();
+#else
+static constexpr int g_conv_variant = 0;
+#endif
+
 bool conv(const ConvParams &p, hipStream_t s) {
     if (p.ct_st) {   // one launch over every output phase (multi-tile kernel only)
         const int NT = p.C_out % 96 == 0 ? 96 : p.C_out % 64 == 0 ? 64 : 0;
@@ -452,6 +460,15 @@ bool conv(const ConvParams &p, hipStream_t s) {
         const long tiles256 = (long)((p.M + 255) / 256) * (p.C_out / NT) * p.nb;
         const bool big = tiles256 >= 512;
         if (big && p.n_taps == 1 && p.C_in <= 192) return NT == 96 ? launch_mt<1, 96, 3>(p, s) : launch_mt<1, 64, 3>(p, s);
+        if (g_conv_variant && big && p.n_taps > 1) {
+            switch (g_conv_variant) {
+                case 1: return NT == 96 ? launch_mt1<1, 96, 2, 7>(p, s) : launch_mt1<1, 64, 2, 7>(p, s);
+                case 2: return launch_mt1<2, 32, 3, 7>(p, s);
+                case 3: return launch_mt1<4, 32, 2, 7>(p, s);
+                case 4: return NT == 96 ? launch_mt1<4, 96, 1, 7>(p, s) : launch_mt1<4, 64, 1, 7>(p, s);
+                default: break;
+            }
+        }
         if (NT == 96) return big ? launch_mt<2, 96>(p, s) : launch_mt<1, 96>(p, s);
         return big ? launch_mt<2, 64>(p, s) : launch_mt<1, 64>(p, s);
     }

@@ -12,7 +12,7 @@ fi
 cd /tmp && export TMPDIR=/tmp
 P="$R/gpurun_out/prof_$TAG"
 rm -rf "$P"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$P" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --frames 12 --cpu-baseline off --batched 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof_$TAG.log"; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$P" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --frames 12 --cpu-baseline off --batched 0 --serve 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof_$TAG.log"; exit 1; }
 T=$(find "$P" -name '*kernel_trace.csv' | head -1)
 S=$(find "$P" -name '*kernel_stats.csv' | head -1)
 python3 "$R/tools/dev/prof_stats.py" "$T" > "$R/gpurun_out/prof_${TAG}_summary.txt"

@@ -14,7 +14,7 @@ timeout -k 10 300 python bench.py --vocoder ${VOC:-none} --steps 2 --warmup 1 --
 cat gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
 P="$R/gpurun_out/prof_$TAG"
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- python3 "$R/bench.py" --vocoder none --steps 1 --warmup 0 --frames 12 --cpu-baseline off --batched 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof_$TAG.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- python3 "$R/bench.py" --vocoder none --steps 1 --warmup 0 --frames 12 --cpu-baseline off --batched 0 --serve 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof_$TAG.log"; exit 1; }
 T=$(find "$P" -name '*kernel_trace.csv' | head -1)
 python3 "$R/tools/dev/trace_phases.py" "$T" > "$R/gpurun_out/phases_$TAG.txt"
 cat "$R/gpurun_out/phases_$TAG.txt"
