@@ -13,6 +13,7 @@
 #include "select.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_attn / k_gemv
 
@@ -677,8 +678,13 @@ struct StateLayout {
 
 }  // namespace
 
+#ifdef Q3T_DEV
+static const int g_min_chunk = [] { const char *e = std::getenv("Q3T_PERSIST_CH"); return e ? std::atoi(e) : 64; }();
+#else
+static constexpr int g_min_chunk = 64;
+#endif
 int persist_chunk(int n_ctx) {
-    int ch = 64;
+    int ch = g_min_chunk;
     while (ch * MAXSPLIT < n_ctx) ch += 64;
     return ch;
 }
