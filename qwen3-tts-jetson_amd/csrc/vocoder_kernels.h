@@ -36,6 +36,7 @@ struct ConvParams {
     // inside each utterance (rows outside [0, T_in) of its own segment read as 0)
     int nb = 1;
     int64_t xbs = 0, ybs = 0;
+    int dev_skip = 0;   // development builds only (timing experiments): 1 weight loads, 2 window loads, 4 epilogue
 };
 bool conv(const ConvParams &p, hipStream_t s);
 // out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
