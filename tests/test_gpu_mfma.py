@@ -107,3 +107,25 @@ def test_mfma_generate_batched_matches_oracle(mm, n_utt):
     for i in sorted({1, n_utt - 2}):
         check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf, temperature=0.9, top_k=50,
                         seed=99, utt=i, max_off_frac=MAX_OFF)
+
+
+def test_mfma_generate_over_64_slots_matches_oracle():
+    """contexts above 64 slots (serving: 256): the split-K slice count is chosen among the GEMM's instantiations
+    (160 slots: the down projection splits K three ways), decisions teacher-forced against the oracle"""
+    import q3t
+    tts, tok = synth_dir("full")
+    n_utt, nf = 160, 6
+    eng = q3t.Engine(tts, None, device=0, max_slots=n_utt, max_ctx=96)
+    orc = Oracle(tts, None)
+    try:
+        H = eng.cfg["hidden"]
+        base = prompt("full")
+        prompts = [base[:4] + [(t + 13 * i) % 900 + 20 for t in base[4:]] for i in range(n_utt)]
+        spk = [np.zeros(H, np.float32)] * n_utt
+        outs = eng.generate(prompts, speakers=spk, max_len=nf, temperature=0.0, force_frames=nf)
+        assert all(o.shape == (nf, 16) for o in outs)
+        for i in (0, 97, n_utt - 1):
+            check_decisions(orc, prompts[i], spk[i], outs[i], max_len=nf, force_frames=nf, max_off_frac=MAX_OFF)
+    finally:
+        orc.close()
+        eng.close()
