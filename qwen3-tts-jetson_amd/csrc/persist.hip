@@ -90,7 +90,10 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
                 break;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
+#ifndef Q3T_POLL_SLEEP
+#define Q3T_POLL_SLEEP 1
+#endif
+        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];

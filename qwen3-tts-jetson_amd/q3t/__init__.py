@@ -10,8 +10,10 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# Q3T_DEV_LIB=1 loads the development build (make -C csrc DEV=1: debug hooks for tools/dev), never the default
-LIB_PATH = os.path.join(_HERE, "libq3t_dev.so" if os.environ.get("Q3T_DEV_LIB") == "1" else "libq3t.so")
+# Q3T_DEV_LIB=1 loads the development build (make -C csrc DEV=1: debug hooks for tools/dev), Q3T_DEV_LIB=<name> an
+# experiment build (make -C csrc VARIANT=<name>: libq3t_<name>.so); never the default
+_dev = os.environ.get("Q3T_DEV_LIB", "")
+LIB_PATH = os.path.join(_HERE, "libq3t.so" if not _dev else "libq3t_dev.so" if _dev == "1" else f"libq3t_{_dev}.so")
 
 VOCODER_FULL = 0
 VOCODER_CHUNK40 = 1
