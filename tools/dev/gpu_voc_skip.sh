@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
-for v in 0 1 2 4 7; do
+for v in ${SKIPS:-0 1 2 4 7}; do
   P="$R/gpurun_out/prof_skip$v"; rm -rf "$P"
   Q3T_DEV_LIB=1 Q3T_CONV_SKIP=$v timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$P" -o run -- python3 "$R/tools/dev/voc_only.py" 512 > "$R/gpurun_out/skip$v.log" 2>&1 || exit 1
   T=$(find "$P" -name '*kernel_trace.csv' | head -1)
