@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 
 #include "speaker.h"
 #include "vocoder.h"
@@ -16,17 +17,34 @@ namespace q3t {
 Engine::Engine() = default;
 
 namespace {
-// Persistent grids of two contexts on one device must never run concurrently: two 256-workgroup grids launched on
-// different streams could interleave and leave neither fully resident (every hand-off would then time out).  Every
-// entry point that launches persistent kernels holds its device's lock until its GPU work has drained (they all
-// return synchronised), so contexts driven by different host threads serialise there.  Recursive: a frame callback
-// may call back into the library on the same thread (it must not start generation on another context of the same
-// device; if it does, the overlap ends in a hand-off timeout and the fallback path, not in a hang).
-std::recursive_mutex g_device_mu[64];
-std::unique_lock<std::recursive_mutex> persist_lock(bool on, int device) {
-    if (!on) return std::unique_lock<std::recursive_mutex>();
-    return std::unique_lock<std::recursive_mutex>(g_device_mu[device & 63]);
-}
+// Persistent grids must never share the device with other work: a 256-workgroup grid launched next to another
+// context's kernels could be left partly non-resident (every hand-off would then time out into the fallback path).
+// A reader/writer lock per device: single-slot runs (the only ones that launch persistent kernels) hold it
+// exclusively, batched runs shared, so batched contexts on one device run concurrently with each other but never
+// beside a persistent grid.  Every entry point holds it until its GPU work has drained (they all return
+// synchronised).  Re-entrant per thread (a retry or a frame callback calling back into the library on the same thread
+// keeps the hold it has; a callback must not start generation on another context of the same device).
+std::shared_mutex g_device_rw[64];
+thread_local int t_device_depth[64];
+class DeviceLock {
+public:
+    DeviceLock(bool exclusive, int device) : dev_(device & 63) {
+        if (t_device_depth[dev_]++ > 0) return;
+        mode_ = exclusive ? 2 : 1;
+        if (exclusive) g_device_rw[dev_].lock();
+        else g_device_rw[dev_].lock_shared();
+    }
+    ~DeviceLock() {
+        --t_device_depth[dev_];
+        if (mode_ == 2) g_device_rw[dev_].unlock();
+        else if (mode_ == 1) g_device_rw[dev_].unlock_shared();
+    }
+    DeviceLock(const DeviceLock &) = delete;
+    DeviceLock &operator=(const DeviceLock &) = delete;
+
+private:
+    int dev_, mode_ = 0;
+};
 bool env_flag(const char *name, bool dflt) {
     const char *e = std::getenv(name);
     return e ? std::atoi(e) != 0 : dflt;
@@ -936,7 +954,7 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
     // only single-slot runs launch the persistent kernels: batched contexts on one device run concurrently
-    auto lk = persist_lock(persist_ && n_utt == 1, device_);
+    DeviceLock lk(persist_ && n_utt == 1, device_);
     StreamState st;
     st.delivered.assign(n_utt, 0);
     st.stop_at.assign(n_utt, -1);
@@ -1344,7 +1362,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
     const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
     if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
     if (gp.max_len > codes_max_len_) { set_error("max_len exceeds the code buffer"); return false; }
-    auto lk = persist_lock(persist_ && S == 1, device_);
+    DeviceLock lk(persist_ && S == 1, device_);
     if (!alloc_admission()) return false;
     q_slots_ = S;
     // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
@@ -1491,7 +1509,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
-    auto lk = persist_lock(persist_ && S == 1, device_);
+    DeviceLock lk(persist_ && S == 1, device_);
     std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
@@ -1524,7 +1542,7 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
     const int H = c_.hidden;
-    auto lk = persist_lock(persist_ && S == 1, device_);
+    DeviceLock lk(persist_ && S == 1, device_);
     for (int attempt = 0; attempt < 2; ++attempt) {
         Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
         Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
@@ -1545,7 +1563,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int H = c_.hidden;
     for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
-    auto lk = persist_lock(persist_ && S == 1, device_);
+    DeviceLock lk(persist_ && S == 1, device_);
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;

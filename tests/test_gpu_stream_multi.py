@@ -114,3 +114,44 @@ def test_shared_single_rank_rccl():
         ref.close()
     finally:
         e.close()
+
+
+def test_concurrent_batched_contexts_and_persistent_exclusion():
+    """contexts on one device driven from several host threads: batched runs (shared device lock) overlap and decode
+    exactly as they do alone; a single-slot run (persistent kernels, exclusive lock) in the middle of them is held
+    back until they drain and decodes exactly as alone (no hand-off timeout, no fallback)"""
+    import threading
+    import q3t
+    tts, tok = synth_dir("tiny")
+    a = q3t.Engine(tts, None, device=0, max_slots=8, max_ctx=64)
+    b = a.replica(0, 8, 64)
+    c = a.replica(0, 1, 64)
+    try:
+        H = a.cfg["hidden"]
+        kw = dict(max_len=12, temperature=0.9, top_k=50, seed=5, force_frames=12)
+        pa, pb = _prompts(8), _prompts(8)[::-1]
+        spk8 = [np.zeros(H, np.float32)] * 8
+        ref_a = a.generate(pa, speakers=spk8, **kw)
+        ref_b = b.generate(pb, speakers=spk8, **kw)
+        ref_c = c.generate(pa[:1], speakers=spk8[:1], **kw)
+        out = {}
+
+        def run(name, e, p, n):
+            for _ in range(3):
+                out[name] = e.generate(p, speakers=spk8[:n], **kw)
+        th = [threading.Thread(target=run, args=("a", a, pa, 8)), threading.Thread(target=run, args=("b", b, pb, 8)),
+              threading.Thread(target=run, args=("c", c, pa[:1], 1))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for x, y in zip(out["a"], ref_a):
+            assert np.array_equal(x, y)
+        for x, y in zip(out["b"], ref_b):
+            assert np.array_equal(x, y)
+        assert np.array_equal(out["c"][0], ref_c[0])
+        assert c.persist_status() in (-1, 0)   # never fell back
+    finally:
+        c.close()
+        b.close()
+        a.close()
