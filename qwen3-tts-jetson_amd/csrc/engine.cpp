@@ -29,6 +29,9 @@ thread_local int t_device_depth[64];
 class DeviceLock {
 public:
     DeviceLock(bool exclusive, int device) : dev_(device & 63) {
+#ifdef Q3T_OLD_LOCK
+        exclusive = true;   // experiment builds: every run exclusive (the previous device lock)
+#endif
         if (t_device_depth[dev_]++ > 0) return;
         mode_ = exclusive ? 2 : 1;
         if (exclusive) g_device_rw[dev_].lock();
@@ -507,7 +510,7 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
                              unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
-                             float *final_side, int S_main = 0) {
+                             float *final_side, int S_main = 0, bool cp_attn = false) {
     // S_main: the batch whose kernel choices this stack reproduces (a continuous-batching admission runs ONE slot
     // with the S_main-slot kernels, so its per-token arithmetic is the batch's)
     if (S_main <= 0) S_main = S;
@@ -538,6 +541,11 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         a.n_ctx = n_ctx; a.S = S; a.nH = c.n_heads; a.nKV = c.n_kv; a.D = D;
         a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
         a.seqk = S_main >= 16 && !attn_split;   // enough (slot, kv head) pairs to fill the chip
+        // the code predictor's <= 16 positions: one wave per (slot, kv head) (the 0.6B head layout)
+        a.small = cp_attn && n_ctx <= 16 && D == 128 && c.n_heads == 2 * c.n_kv;
+#ifdef Q3T_NO_SMALL_ATTN
+        a.small = 0;   // experiment builds: the code predictor on k_attn_seq / k_attn as before
+#endif
         a.part = part; a.ticket = ticket; a.out = attn;
         if (!attn_decode(a, s)) return false;
         GemvParams o;
@@ -747,7 +755,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         if (mm) {
             if (!decoder_stack_mm(c_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
-                                  p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_))
+                                  p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_, true))
                 return false;
         } else if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0, cp_fused_attn_)) {
@@ -770,7 +778,11 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
             for (int b = 0; b < S; ++b)
                 std::memcpy(logits_host + ((size_t)b * 15 + step) * c_.cp_vocab, lg.data() + (size_t)b * c_.cp_vocab, c_.cp_vocab * 4);
         }
+#ifdef Q3T_NO_SELFUSE
+        if (false) {
+#else
         if (mm && (step < 14 || talker_next)) {
+#endif
             // batched: the selecting workgroup of each slot also gathers and normalises the next stage's input (the
             // next pass's table row, or the talker step embedding after the last pass)
             EmbedNorm en;
@@ -798,7 +810,11 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
 bool Engine::enqueue_frame(int S, hipStream_t s) {
     if (!fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, s)) return false;
     // batched: the last code-predictor selection also assembles and normalises the talker step's input
+#ifdef Q3T_NO_SELFUSE
+    const bool mm = false;
+#else
     const bool mm = S >= gemm_mfma_min_batch();
+#endif
     if (!enqueue_cp_frame(S, s, nullptr, mm)) return false;
     if (!enqueue_talker(S, s, true, fused_select_, mm)) return false;
     return advance(pos_, frame_, done_, S, s);

@@ -132,6 +132,7 @@ struct AttnParams {
     int n_ctx = 0, S = 0, nH = 0, nKV = 0, D = 0;
     int chunk = 64;               // positions per split workgroup: 64 or 128 (batched decode: fewer, fuller splits)
     int seqk = 0;                 // 1: one workgroup per (slot, kv head) streams the whole context (k_attn_seq; many slots)
+    int small = 0;                // 1: batched code predictor (n_ctx <= 16): one wave per (slot, kv head) (k_attn_small)
     int max_splits = 1;           // grid z = ceil(n_ctx / chunk)
     float *part = nullptr;        // [S][nKV][max_splits][R][D + 2] split partials (m, l, acc)
     unsigned *ticket = nullptr;   // [S][nKV] arrival counters, zero between launches
