@@ -85,7 +85,11 @@ template <class T>
 T *Engine::dalloc(size_t n) {
     void *p = nullptr;
     if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    // zeroed before any kernel can see it: hipMemset runs on the null stream, which the context's non-blocking
+    // streams do not wait for, so without the synchronisation a first launch could read what a previous context
+    // (freed in the same process) left in this memory -- continuous batching read such state (DESIGN §2e')
     hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T));
+    hipDeviceSynchronize();
     allocs_.push_back(p);
     return static_cast<T *>(p);
 }
