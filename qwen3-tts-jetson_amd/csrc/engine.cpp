@@ -405,6 +405,7 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
     }
     Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
+    Q3T_HIP(hipDeviceSynchronize());   // null-stream memset: order it before the non-blocking streams' launches
 #ifdef Q3T_DEV
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
 #endif
@@ -416,6 +417,7 @@ bool Engine::persist_recover() {
     fprintf(stderr, "[q3t] persistent kernel flagged an in-launch hand-off fault on device %d: "
                     "falling back to the launch-per-op graphs for this context\n", device_);
     Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
+    Q3T_HIP(hipDeviceSynchronize());   // null-stream memset: order it before the non-blocking streams' launches
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
@@ -1233,6 +1235,7 @@ bool Engine::alloc_admission() {
         return false;
     }
     Q3T_HIP(hipMemset(aticket_, 0, (size_t)S * c_.n_kv * 4));
+    Q3T_HIP(hipDeviceSynchronize());
     Q3T_HIP(hipStreamCreateWithFlags(&astream_, hipStreamNonBlocking));
     return true;
 }
