@@ -108,3 +108,30 @@ def test_queue_admitted_utterances_match_oracle(full):
             print(f"utterance {u}: {len(outs[u])} frames, {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
     finally:
         eng.close()
+
+
+def test_queue_after_other_contexts_in_the_process(full):
+    """regression: a context's buffers are zeroed before its non-blocking streams can read them.  Before, a context
+    freed earlier in the process (here: one that ran a text projection and a talker step) left state that a later
+    context's continuous batching read through the unsynchronised null-stream memset, and the codes changed"""
+    import q3t
+    tts, tok, orc = full
+    prev = q3t.Engine(tts, None, device=0, max_slots=64, max_ctx=96)
+    Hd = prev.cfg["hidden"]
+    prev.project_text(prompt("full"))
+    rng = np.random.default_rng(9)
+    prev.talker_forward((rng.standard_normal((1, Hd)) * 0.5).astype(np.float32), [0])
+    prev.close()
+    slots, n_utt, nf = 12, 20, 40
+    eng = q3t.Engine(tts, None, device=0, max_slots=slots, max_ctx=nf + 40)
+    try:
+        prompts = _prompts(n_utt, slots)
+        kw = dict(speakers=[np.zeros(Hd, np.float32)] * n_utt, max_len=nf, temperature=0.9, top_k=50, seed=77)
+        a = eng.generate_queue(prompts, max_active=slots, **kw)
+        b = eng.generate_queue(prompts, max_active=3, **kw)
+        for u in range(n_utt):
+            assert np.array_equal(a[u], b[u]), u
+        check_decisions(orc, prompts[0], kw["speakers"][0], a[0], max_len=nf, temperature=0.9, top_k=50, seed=77,
+                        utt=0, max_off_frac=MM_MAX_OFF)
+    finally:
+        eng.close()
