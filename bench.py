@@ -38,12 +38,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n):
+def _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n, cfg0_frames):
+    """one thread count: (a) prefill + n frames + the vocoder of those n frames, extrapolated to `frames`;
+    (b) BASELINE configs[0] measured directly: one cfg0_frames-frame utterance end to end (prefill, frames, vocoder)"""
     import numpy as np
     from oracle_py import Oracle
     o = Oracle(tts, tok, threads=threads)
     spk = np.zeros(o.cfg["hidden"], np.float32)
     kw = dict(spk=spk, temperature=0.9, top_k=50, seed=1, rep=1.05)
+    o.generate(prompt, max_len=1, force_frames=1, **kw)   # page the weights in (mmap) before anything is timed
     t0 = time.perf_counter()
     o.generate(prompt, max_len=1, force_frames=1, **kw)
     t1 = time.perf_counter()
@@ -53,30 +56,52 @@ def _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n):
     t_prefill = max(0.0, (t1 - t0) - t_frame)
     t_voc = 0.0
     if vocoder_mode is not None:
+        o.vocoder(codes[:8], vocoder_mode)   # vocoder weights paged in
         t3 = time.perf_counter()
         o.vocoder(codes, vocoder_mode)
         t_voc = (time.perf_counter() - t3) / len(codes)
+    t4 = time.perf_counter()
+    c0 = o.generate(prompt, max_len=cfg0_frames, force_frames=cfg0_frames, **kw)
+    if vocoder_mode is not None:
+        o.vocoder(c0, vocoder_mode)
+    t_cfg0 = time.perf_counter() - t4
     o.close()
     total = t_prefill + frames * (t_frame + t_voc)
-    return total, t_prefill, t_frame, t_voc, len(codes), time.perf_counter() - t0
+    return dict(total=total, t_prefill=t_prefill, t_frame=t_frame, t_voc=t_voc, n=len(codes), t_cfg0=t_cfg0,
+                wall=time.perf_counter() - t0)
 
 
-def cpu_baseline(tts, tok, prompt, frames, vocoder_mode):
+def cpu_baseline(tts, tok, prompt, frames, vocoder_mode, gpu):
     """The oracle (C restatement of the reference GGML-CPU path) timed on a bounded sample and extrapolated to the
-    workload: t = t_prefill + frames * (t_frame + t_vocoder_per_frame).  Main number at 4 threads: the reference
-    never plumbs n_threads (src/qwen3_tts.h:32), so the ggml CPU backend runs its default GGML_DEFAULT_N_THREADS = 4
-    [ggml-upstream]; the all-cores figure (OMP_NUM_THREADS) is reported beside it."""
+    workload: t = t_prefill + frames * (t_frame + t_vocoder_per_frame), plus BASELINE configs[0] (one 32-frame utterance)
+    measured end to end without extrapolation.  The vocoder convs run as ggml runs them (im2col rows of the f16-rounded
+    input times the f16 kernel, f32 accumulation) on a register-blocked AVX2/F16C GEMM.  Main number at 4 threads: the
+    reference never plumbs n_threads (src/qwen3_tts.h:32), so the ggml CPU backend runs its default
+    GGML_DEFAULT_N_THREADS = 4 [ggml-upstream]; the all-cores figure (OMP_NUM_THREADS) is reported beside it.
+    gpu: the GPU's own per-frame decode / vocoder times and configs[0] RTF, for the per-stage ratios."""
     res = {}
     allc = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    # samples sized to ~10-30 s of CPU work in total (4 threads: ~110 ms/frame; all cores: ~35 ms/frame)
-    for threads, n in ((4, 96), (allc, 128)):
-        total, tp, tf, tv, nf, wall = _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n)
-        res[threads] = dict(value=round(frames / total, 3), rtf=round(total / (frames * FRAME_SEC), 4),
-                            sample=f"prefill + {nf} frames + vocoder of {nf} frames ({wall:.1f} s of CPU work): "
-                                   f"t_prefill {tp:.2f}s, {tf * 1e3:.1f} ms/frame, vocoder {tv * 1e3:.1f} ms/frame, "
-                                   f"extrapolated to {frames} frames")
+    cfg0 = 32
+    # samples sized to ~10-30 s of CPU work in total
+    for threads, n in ((4, 64), (allc, 96)):
+        r = _time_oracle(tts, tok, prompt, frames, vocoder_mode, threads, n, cfg0)
+        rtf0 = r["t_cfg0"] / (cfg0 * FRAME_SEC)
+        res[threads] = dict(
+            value=round(frames / r["total"], 3), rtf=round(r["total"] / (frames * FRAME_SEC), 4),
+            decode_only={"cpu_ms_per_frame": round(r["t_frame"] * 1e3, 2),
+                         "gpu_ms_per_frame": round(gpu["decode_ms_per_frame"], 3),
+                         "ratio": round(r["t_frame"] * 1e3 / gpu["decode_ms_per_frame"], 1)},
+            vocoder_only=None if vocoder_mode is None else {
+                "cpu_ms_per_frame": round(r["t_voc"] * 1e3, 2), "gpu_ms_per_frame": round(gpu["vocoder_ms_per_frame"], 4),
+                "ratio": round(r["t_voc"] * 1e3 / gpu["vocoder_ms_per_frame"], 1)},
+            configs0={"frames": cfg0, "cpu_s": round(r["t_cfg0"], 3), "cpu_rtf": round(rtf0, 4),
+                      "gpu_rtf": round(gpu["cfg0_rtf"], 5), "rtf_ratio": round(rtf0 / gpu["cfg0_rtf"], 1)},
+            sample=f"prefill + {r['n']} frames + vocoder of {r['n']} frames, then one {cfg0}-frame utterance end to "
+                   f"end ({r['wall']:.1f} s of CPU work): t_prefill {r['t_prefill']:.2f}s, {r['t_frame'] * 1e3:.1f} "
+                   f"ms/frame, vocoder {r['t_voc'] * 1e3:.1f} ms/frame, extrapolated to {frames} frames")
     r4 = res[4]
     return {"value": r4["value"], "unit": "frames/s", "cores": 4, "kind": "port", "rtf": r4["rtf"],
+            "decode_only": r4["decode_only"], "vocoder_only": r4["vocoder_only"], "configs0": r4["configs0"],
             "sample": "oracle/q3t_oracle.c (GGML-CPU restatement, f16 weights, f16-rounded matmul inputs) on the full "
                       "0.6B synthetic model at the reference's ggml default of 4 threads: " + r4["sample"],
             "all_cores": {"cores": allc, **res[allc]}}
@@ -254,6 +279,23 @@ def main():
     total_frames = world * B * args.frames * args.steps
     value = total_frames / elapsed
 
+    # ---- per-stage GPU times for the CPU-baseline ratios: decode loop and vocoder per frame of the timed steps, and
+    # BASELINE configs[0] (one 32-frame utterance, prefill + frames + vocoder) end to end, median of 5 wall-clock runs
+    gpu_stage = {"decode_ms_per_frame": main_stats["frames_ms"] / (args.steps * args.frames),
+                 "vocoder_ms_per_frame": main_stats["vocoder_ms"] / (args.steps * args.frames * B)}
+    if rank == 0 and args.cpu_baseline == "on" and world == 1:
+        t_c0 = []
+        for k in range(6):
+            eng.synchronize()
+            t = time.perf_counter()
+            c0 = eng.generate([prompt], speakers=[spks[0]], max_len=32, temperature=0.9, top_k=50,
+                              repetition_penalty=1.05, seed=77, force_frames=32)
+            if voc_mode is not None:
+                eng.vocoder(c0[0], voc_mode)
+            eng.synchronize()
+            t_c0.append(time.perf_counter() - t)
+        gpu_stage["cfg0_rtf"] = sorted(t_c0[1:])[2] / (32 * FRAME_SEC)
+
     # ---- roofline of the talker decode step (SURVEY §8(d) definition) at the mid-utterance position
     p_mid = args.roofline_pos
     t_talker = eng.time_stage(0, B, p_mid, args.stage_iters)
@@ -383,7 +425,7 @@ def main():
         if args.cpu_baseline == "on" and world == 1:
             try:
                 res["cpu_baseline"] = cpu_baseline(tts, tok if voc_mode is not None else None, prompt, args.frames,
-                                                   voc_mode)
+                                                   voc_mode, gpu_stage)
             except Exception as e:  # the GPU number stands on its own
                 res["cpu_baseline"] = {"value": None, "error": str(e)}
         else:

@@ -812,13 +812,29 @@ static void mul_mat_vec(const q3o_model *m, const mat16 *W, const float *x, floa
     for (int r = 0; r < W->rows; ++r) y[r] = dot_f16_f32(W->w + (size_t)r * W->cols, xr, W->cols);
     free(xr);
 }
-/* Y[t][rows] = W · round(X[t])  for T columns (row-major X [T][cols]) */
+static inline float dot_f32(const float *a, const float *b, int n);
+/* Y[t][rows] = W · round(X[t])  for T columns (row-major X [T][cols]).  Several columns: each weight row is widened
+ * to f32 once (exact) and dotted with every column by dot_f32, which sums in dot_f16_f32's order (bit-identical) */
 static void mul_mat_rows(const q3o_model *m, const mat16 *W, const float *X, int T, float *Y) {
     float *xr = malloc(sizeof(float) * (size_t)W->cols * (size_t)T);
     round_in(m, X, xr, W->cols * T);
+    if (T < 4) {
 #pragma omp parallel for schedule(static)
-    for (int r = 0; r < W->rows; ++r)
-        for (int t = 0; t < T; ++t) Y[(size_t)t * W->rows + r] = dot_f16_f32(W->w + (size_t)r * W->cols, xr + (size_t)t * W->cols, W->cols);
+        for (int r = 0; r < W->rows; ++r)
+            for (int t = 0; t < T; ++t) Y[(size_t)t * W->rows + r] = dot_f16_f32(W->w + (size_t)r * W->cols, xr + (size_t)t * W->cols, W->cols);
+    } else {
+#pragma omp parallel
+        {
+            float *wr = malloc(sizeof(float) * (size_t)W->cols);
+#pragma omp for schedule(static)
+            for (int r = 0; r < W->rows; ++r) {
+                const uint16_t *w = W->w + (size_t)r * W->cols;
+                for (int c = 0; c < W->cols; ++c) wr[c] = q3o_f16_to_f32(w[c]);
+                for (int t = 0; t < T; ++t) Y[(size_t)t * W->rows + r] = dot_f32(wr, xr + (size_t)t * W->cols, W->cols);
+            }
+            free(wr);
+        }
+    }
     free(xr);
 }
 
@@ -1372,14 +1388,94 @@ static void snake_apply(const snake_t *s, const float *x, float *y, int T) {   /
         }
     }
 }
+#define CG_T 16
+#ifdef Q3O_SIMD
+/* The conv as ggml computes it (im2col to F16, then mul_mat of the F16 kernel [OC][IC*K] with the im2col rows,
+ * f32 accumulation: ggml_conv_1d / ggml_conv_transpose_1d, src/audio_tokenizer_decoder.cpp:551-620, 705-790) as a
+ * register-blocked GEMM on AVX2/F16C.  The im2col matrix is never materialised: its row j = (ci, tap) is the
+ * f16-rounded input row ci shifted by off[tap].  Micro-tile: 6 output channels x 16 time steps (12 ymm accumulators,
+ * 2 loads + 6 broadcasts per 12 FMAs), accumulated over (ci, tap) in the order of the scalar loop below, so the
+ * result is the scalar restatement's bit for bit.
+ *   Y[co][t] (stored at y[co * ldy + t * sy]) = bias[co] + sum_ci sum_tap W(co, ci, tap) * X[ci][t + off[tap]]
+ * wt: [ceil(OC/6)][IC][NT][6] f32 weights (rows past OC zero); x already offset to output t = 0. */
+#define CG_CO 6
+static void conv_gemm(const float *wt, int OC, int IC, int NT, const int *off, const float *x, size_t ldx, int n,
+                      const float *bias, float *y, size_t ldy, int sy) {
+    const int nct = (OC + CG_CO - 1) / CG_CO, TB = 256, ntb = (n + TB - 1) / TB;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int tb = 0; tb < ntb; ++tb)
+        for (int ct = 0; ct < nct; ++ct) {
+            const float *wc = wt + (size_t)ct * IC * NT * CG_CO;
+            const int t1 = (tb + 1) * TB < n ? (tb + 1) * TB : n;
+            for (int t = tb * TB; t < t1; t += CG_T) {
+                const int tn = t1 - t < CG_T ? t1 - t : CG_T;
+                float out[CG_CO][CG_T];
+                if (tn == CG_T) {
+                    __m256 a[CG_CO][2];
+                    for (int c = 0; c < CG_CO; ++c) a[c][0] = a[c][1] = _mm256_setzero_ps();
+                    for (int ci = 0; ci < IC; ++ci) {
+                        const float *xr = x + (size_t)ci * ldx + t;
+                        const float *wp = wc + (size_t)ci * NT * CG_CO;
+                        for (int k = 0; k < NT; ++k, wp += CG_CO) {
+                            const __m256 b0 = _mm256_loadu_ps(xr + off[k]), b1 = _mm256_loadu_ps(xr + off[k] + 8);
+                            for (int c = 0; c < CG_CO; ++c) {
+                                const __m256 w = _mm256_broadcast_ss(wp + c);
+                                a[c][0] = _mm256_fmadd_ps(w, b0, a[c][0]);
+                                a[c][1] = _mm256_fmadd_ps(w, b1, a[c][1]);
+                            }
+                        }
+                    }
+                    for (int c = 0; c < CG_CO; ++c) { _mm256_storeu_ps(out[c], a[c][0]); _mm256_storeu_ps(out[c] + 8, a[c][1]); }
+                } else {   /* tail: the same order, scalar */
+                    for (int c = 0; c < CG_CO; ++c)
+                        for (int j = 0; j < tn; ++j) out[c][j] = 0.f;
+                    for (int ci = 0; ci < IC; ++ci) {
+                        const float *xr = x + (size_t)ci * ldx + t;
+                        const float *wp = wc + (size_t)ci * NT * CG_CO;
+                        for (int k = 0; k < NT; ++k, wp += CG_CO)
+                            for (int c = 0; c < CG_CO; ++c)
+                                for (int j = 0; j < tn; ++j) out[c][j] = fmaf(wp[c], xr[off[k] + j], out[c][j]);
+                    }
+                }
+                for (int c = 0; c < CG_CO; ++c) {
+                    const int co = ct * CG_CO + c;
+                    if (co >= OC) break;
+                    const float b = bias ? bias[co] : 0.f;
+                    for (int j = 0; j < tn; ++j) y[(size_t)co * ldy + (size_t)(t + j) * sy] = out[c][j] + b;
+                }
+            }
+        }
+}
+#endif
+
 /* causal conv1d: left pad `pad`, kernel k, dilation d, stride 1 (ggml_pad_ext + ggml_conv_1d/_dw: im2col F16) */
 static float *conv1d(const q3o_model *m, const conv_t *cv, const float *x, int T, int pad, int dil, int depthwise, int *Tout) {
     const int Tp = T + pad, To = Tp - dil * (cv->k - 1);
     const int C_in = depthwise ? cv->oc : cv->ic;
-    float *xr = calloc((size_t)C_in * Tp, sizeof(float));
+    float *xr = calloc((size_t)C_in * Tp + CG_T, sizeof(float));
     for (int ci = 0; ci < C_in; ++ci)
         for (int t = 0; t < T; ++t) { float v = x[(size_t)ci * T + t]; xr[(size_t)ci * Tp + pad + t] = m->round ? f16r(v) : v; }
     float *y = malloc(sizeof(float) * (size_t)cv->oc * To);
+#ifdef Q3O_SIMD
+    if (!depthwise) {
+        const int OC = cv->oc, IC = cv->ic, K = cv->k, nct = (OC + CG_CO - 1) / CG_CO;
+        float *wt = calloc((size_t)nct * IC * K * CG_CO, sizeof(float));
+        for (int co = 0; co < OC; ++co)
+            for (int ci = 0; ci < IC; ++ci)
+                for (int k = 0; k < K; ++k)
+                    wt[(((size_t)(co / CG_CO) * IC + ci) * K + k) * CG_CO + co % CG_CO] = q3o_f16_to_f32(cv->w[((size_t)co * IC + ci) * K + k]);
+        int off[64];
+        for (int k = 0; k < K && k < 64; ++k) off[k] = k * dil;
+        if (K <= 64) {
+            conv_gemm(wt, OC, IC, K, off, xr, (size_t)Tp, To, cv->b, y, (size_t)To, 1);
+            free(wt);
+            free(xr);
+            *Tout = To;
+            return y;
+        }
+        free(wt);
+    }
+#endif
     const int TB = 512;
 #pragma omp parallel for schedule(dynamic)
     for (int co = 0; co < cv->oc; ++co) {
@@ -1410,6 +1506,43 @@ static float *convT1d(const q3o_model *m, const convT_t *cv, const float *x, int
     float *xr = malloc(sizeof(float) * (size_t)cv->ic * T);
     for (size_t i = 0; i < (size_t)cv->ic * T; ++i) xr[i] = m->round ? f16r(x[i]) : x[i];
     float *y = malloc(sizeof(float) * (size_t)cv->oc * To);
+#ifdef Q3O_SIMD
+    /* polyphase: output o' = q*s + r (o' = o + trim into the untrimmed result) takes taps k = r + m*s at input q - m,
+     * added in (ic, k) order like the scatter loop below; each phase is a conv_gemm over q with offsets mmax - m
+     * into the zero-padded rows */
+    if (cv->k <= 64 * s) {
+        const int IC = cv->ic, OC = cv->oc, K = cv->k, mmax = (K + s - 1) / s, nct = (OC + CG_CO - 1) / CG_CO;
+        const size_t ld = (size_t)T + 2 * mmax + CG_T;
+        float *xp = calloc((size_t)IC * ld, sizeof(float));
+        for (int ic = 0; ic < IC; ++ic) memcpy(xp + (size_t)ic * ld + mmax, xr + (size_t)ic * T, sizeof(float) * (size_t)T);
+        float *wt = malloc(sizeof(float) * (size_t)nct * IC * mmax * CG_CO);
+        for (int r = 0; r < s; ++r) {
+            const int nt = (K - r + s - 1) / s;   /* taps of this phase */
+            if (nt <= 0) continue;
+            /* outputs of this phase: o = q*s + r - trim in [0, To) */
+            int q0 = (trim - r + s - 1) / s;
+            if (q0 < 0) q0 = 0;
+            const int o0 = q0 * s + r - trim;
+            if (o0 >= To) continue;
+            const int n = (To - o0 + s - 1) / s;
+            memset(wt, 0, sizeof(float) * (size_t)nct * IC * nt * CG_CO);
+            for (int oc = 0; oc < OC; ++oc)
+                for (int ic = 0; ic < IC; ++ic)
+                    for (int mm = 0; mm < nt; ++mm)
+                        wt[(((size_t)(oc / CG_CO) * IC + ic) * nt + mm) * CG_CO + oc % CG_CO] =
+                            q3o_f16_to_f32(cv->w[((size_t)ic * OC + oc) * K + r + mm * s]);
+            int off[64];
+            for (int mm = 0; mm < nt; ++mm) off[mm] = mmax - mm;
+            /* input index q - m = (q0 + j) - m -> xp column mmax + q0 + j - m */
+            conv_gemm(wt, OC, IC, nt, off, xp + q0, ld, n, cv->b, y + o0, (size_t)To, s);
+        }
+        free(wt);
+        free(xp);
+        free(xr);
+        *Tout = To;
+        return y;
+    }
+#endif
 #pragma omp parallel for schedule(dynamic)
     for (int oc = 0; oc < cv->oc; ++oc) {
         float *full = calloc((size_t)Tfull, sizeof(float));

@@ -5,6 +5,7 @@
 #include <exception>
 
 #include "comm.h"
+#include "devlock.h"
 #include "engine.h"
 #include "speaker.h"
 #include "tokenizer.h"
@@ -253,6 +254,7 @@ int q3t_vocoder_decode(q3t_ctx *ctx, const int32_t *codes, int32_t n_frames, int
     if (!v || !v->loaded()) { q3t::set_error("vocoder not loaded (no tokenizer GGUF given)"); return Q3T_ERR; }
     if (mode != Q3T_VOCODER_FULL && mode != Q3T_VOCODER_CHUNK40) { q3t::set_error("bad vocoder mode"); return Q3T_ERR; }
     if (n_frames > 0 && (!codes || !pcm)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    q3t::DeviceLock lk(false, ctx->engine.device());   // never beside a persistent grid (devlock.h)
     return v->decode(codes, n_frames, mode, pcm, n_samples) ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
@@ -266,6 +268,7 @@ int q3t_vocoder_decode_chunked(q3t_ctx *ctx, const int32_t *codes, int32_t n_fra
     if (n_codebooks != 16) { q3t::set_error("n_codebooks must be 16"); return Q3T_ERR; }
     if (chunk_frames <= 0) { q3t::set_error("chunk_frames must be > 0"); return Q3T_ERR; }
     if (n_frames > 0 && (!codes || !pcm)) { q3t::set_error("null argument"); return Q3T_ERR; }
+    q3t::DeviceLock lk(false, ctx->engine.device());   // never beside a persistent grid (devlock.h)
     return v->decode(codes, n_frames, Q3T_VOCODER_CHUNK40, pcm, n_samples, chunk_frames) ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
@@ -282,6 +285,7 @@ int q3t_vocoder_decode_batch(q3t_ctx *ctx, int32_t n_utt, const int32_t *const *
         if (n_frames[u] > 0 && (!codes[u] || !pcm[u])) { q3t::set_error("null argument"); return Q3T_ERR; }
     if (mode == Q3T_VOCODER_CHUNK40 && chunk_frames <= 0) { q3t::set_error("chunk_frames must be > 0"); return Q3T_ERR; }
     std::vector<int> nf(n_frames, n_frames + n_utt);
+    q3t::DeviceLock lk(false, ctx->engine.device());   // never beside a persistent grid (devlock.h)
     return v->decode_batch(n_utt, codes, nf.data(), mode, pcm, n_samples, chunk_frames) ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
@@ -322,6 +326,7 @@ int q3t_speaker_encode(q3t_ctx *ctx, const float *samples, int32_t n_samples, fl
     q3t::SpeakerEncoder *s = ctx->engine.speaker();
     if (!s || !s->loaded()) { q3t::set_error("Model not loaded (no speaker encoder tensors in the TTS GGUF)"); return Q3T_ERR; }
     if (!samples || !embedding || n_samples <= 0) { q3t::set_error("null argument"); return Q3T_ERR; }
+    q3t::DeviceLock lk(false, ctx->engine.device());   // never beside a persistent grid (devlock.h)
     return s->encode(samples, n_samples, embedding) ? Q3T_OK : Q3T_ERR;
     GUARD_END
 }
@@ -335,6 +340,7 @@ int q3t_speaker_mel(q3t_ctx *ctx, const float *samples, int32_t n_samples, float
     if (!samples || !n_frames || n_samples <= 0) { q3t::set_error("null argument"); return Q3T_ERR; }
     std::vector<float> m;
     int F = 0;
+    q3t::DeviceLock lk(false, ctx->engine.device());
     if (!s->mel(samples, n_samples, m, &F)) return Q3T_ERR;
     *n_frames = F;
     if (mel) {

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <shared_mutex>
 
+#include "devlock.h"
 #include "speaker.h"
 #include "vocoder.h"
 
@@ -17,37 +18,24 @@ namespace q3t {
 Engine::Engine() = default;
 
 namespace {
-// Persistent grids must never share the device with other work: a 256-workgroup grid launched next to another
-// context's kernels could be left partly non-resident (every hand-off would then time out into the fallback path).
-// A reader/writer lock per device: single-slot runs (the only ones that launch persistent kernels) hold it
-// exclusively, batched runs shared, so batched contexts on one device run concurrently with each other but never
-// beside a persistent grid.  Every entry point holds it until its GPU work has drained (they all return
-// synchronised).  Re-entrant per thread (a retry or a frame callback calling back into the library on the same thread
-// keeps the hold it has; a callback must not start generation on another context of the same device).
 std::shared_mutex g_device_rw[64];
 thread_local int t_device_depth[64];
-class DeviceLock {
-public:
-    DeviceLock(bool exclusive, int device) : dev_(device & 63) {
-#ifdef Q3T_OLD_LOCK
-        exclusive = true;   // experiment builds: every run exclusive (the previous device lock)
-#endif
-        if (t_device_depth[dev_]++ > 0) return;
-        mode_ = exclusive ? 2 : 1;
-        if (exclusive) g_device_rw[dev_].lock();
-        else g_device_rw[dev_].lock_shared();
-    }
-    ~DeviceLock() {
-        --t_device_depth[dev_];
-        if (mode_ == 2) g_device_rw[dev_].unlock();
-        else if (mode_ == 1) g_device_rw[dev_].unlock_shared();
-    }
-    DeviceLock(const DeviceLock &) = delete;
-    DeviceLock &operator=(const DeviceLock &) = delete;
+}  // namespace
 
-private:
-    int dev_, mode_ = 0;
-};
+// devlock.h: exclusive for single-slot (persistent-kernel) runs, shared for everything else
+DeviceLock::DeviceLock(bool exclusive, int device) : dev_(device & 63) {
+    if (t_device_depth[dev_]++ > 0) return;
+    mode_ = exclusive ? 2 : 1;
+    if (exclusive) g_device_rw[dev_].lock();
+    else g_device_rw[dev_].lock_shared();
+}
+DeviceLock::~DeviceLock() {
+    --t_device_depth[dev_];
+    if (mode_ == 2) g_device_rw[dev_].unlock();
+    else if (mode_ == 1) g_device_rw[dev_].unlock_shared();
+}
+
+namespace {
 bool env_flag(const char *name, bool dflt) {
     const char *e = std::getenv(name);
     return e ? std::atoi(e) != 0 : dflt;
@@ -77,6 +65,9 @@ Engine::~Engine() {
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     voc_.reset();
     for (void *p : allocs_) hipFree(p);
+    if (qout_) hipFree(qout_);
+    if (pin_) hipHostFree(pin_);
+    for (PinnedChunk &c : chunk_pool_) { hipHostFree(c.codes); hipEventDestroy(c.ev); }
     if (stream_) hipStreamDestroy(stream_);
     if (astream_) hipStreamDestroy(astream_);
 }
@@ -85,13 +76,38 @@ template <class T>
 T *Engine::dalloc(size_t n) {
     void *p = nullptr;
     if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
-    // zeroed before any kernel can see it: hipMemset runs on the null stream, which the context's non-blocking
-    // streams do not wait for, so without the synchronisation a first launch could read what a previous context
-    // (freed in the same process) left in this memory -- continuous batching read such state (DESIGN §2e')
-    hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T));
-    hipDeviceSynchronize();
     allocs_.push_back(p);
+    // zeroed on the context's own stream, and drained before any other stream (the admission stream, or a
+    // synchronous null-stream copy into the buffer right after this call) can touch it: without the ordering a first
+    // launch could read what a previous context freed in the same process left in this memory (DESIGN §2e').  Only
+    // this context's stream is waited for, never the device.
+    if (hipMemsetAsync(p, 0, std::max<size_t>(n, 1) * sizeof(T), stream_) != hipSuccess ||
+        hipStreamSynchronize(stream_) != hipSuccess) {
+        set_error("dalloc: zeroing failed");
+        return nullptr;
+    }
     return static_cast<T *>(p);
+}
+
+// the pinned / device scratch of generate() and generate_queue(), kept across calls: a per-call hipFree or
+// hipHostFree would synchronise the whole device (every other context on it included)
+bool Engine::ensure_pinned(size_t bytes) {
+    if (bytes <= pin_cap_) return true;
+    if (pin_) hipHostFree(pin_);
+    pin_ = nullptr;
+    pin_cap_ = 0;
+    if (hipHostMalloc(&pin_, bytes, hipHostMallocDefault) != hipSuccess) { pin_ = nullptr; set_error("hipHostMalloc failed"); return false; }
+    pin_cap_ = bytes;
+    return true;
+}
+bool Engine::ensure_qout(size_t bytes) {
+    if (bytes <= qout_cap_) return true;
+    if (qout_) hipFree(qout_);
+    qout_ = nullptr;
+    qout_cap_ = 0;
+    if (hipMalloc(&qout_, bytes) != hipSuccess) { qout_ = nullptr; set_error("device allocation failed"); return false; }
+    qout_cap_ = bytes;
+    return true;
 }
 
 namespace {
@@ -108,6 +124,7 @@ bool check_shape(const GgufTensor *t, const char *name, int64_t cols, int64_t ro
 
 bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
                   bool recv_weights) {
+    DeviceLock lk(false, device);   // allocation zeroing / weight upload run kernels and copies on this device
     device_ = device;
     tts_path_ = tts_gguf;
     tok_path_ = tok_gguf;
@@ -185,6 +202,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
 }
 
 bool Engine::load_speaker_only(const std::string &tts_gguf, int device) {
+    DeviceLock lk(false, device);
     device_ = device;
     tts_path_ = tts_gguf;
     talker_ = false;
@@ -404,8 +422,7 @@ bool Engine::setup_persist() {
         std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
     }
-    Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
-    Q3T_HIP(hipDeviceSynchronize());   // null-stream memset: order it before the non-blocking streams' launches
+    // (pstate_ was zeroed on the context stream by dalloc)
 #ifdef Q3T_DEV
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
 #endif
@@ -416,8 +433,8 @@ bool Engine::persist_recover() {
     Q3T_HIP(hipStreamSynchronize(stream_));
     fprintf(stderr, "[q3t] persistent kernel flagged an in-launch hand-off fault on device %d: "
                     "falling back to the launch-per-op graphs for this context\n", device_);
-    Q3T_HIP(hipMemset(pstate_, 0, persist_state_bytes()));
-    Q3T_HIP(hipDeviceSynchronize());   // null-stream memset: order it before the non-blocking streams' launches
+    Q3T_HIP(hipMemsetAsync(pstate_, 0, persist_state_bytes(), stream_));   // ordered before the re-run on stream_
+    Q3T_HIP(hipStreamSynchronize(stream_));
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
@@ -874,6 +891,7 @@ bool Engine::enqueue_text_projection(int n_rows, hipStream_t s, const int *idx, 
 bool Engine::project_text(int n, const int32_t *toks, float *out) {
     if (n <= 0) return true;
     if (n > proj_cap_) { set_error("too many text rows"); return false; }
+    DeviceLock lk(false, device_);
     for (int i = 0; i < n; ++i)
         if (toks[i] < 0 || toks[i] >= c_.text_vocab) { set_error("text token out of range"); return false; }
     Q3T_HIP(hipMemcpyAsync(proj_idx_, toks, n * 4, hipMemcpyHostToDevice, stream_));
@@ -912,6 +930,7 @@ static bool plan_rows(const Config &c, int n_utt, const int32_t *const *tokens, 
 bool Engine::prefill_embd(const int32_t *toks, int n, const float *spk, int language_id, float *prefill, int *prefill_len,
                           float *trailing, int *trailing_len, float *tts_pad) {
     // host entry for the parity tests: run the same device assembly as generate() on slot 0
+    DeviceLock lk(false, device_);
     const int32_t *tk[1] = {toks};
     std::vector<int> idx;
     std::vector<SlotPlan> plan;
@@ -961,6 +980,7 @@ bool Engine::prefill_embd(const int32_t *toks, int n, const float *spk, int lang
 
 // ------------------------------------------------------------------------------------------ hot path
 bool Engine::copy_weights_from(Engine &src) {
+    DeviceLock lk(false, device_);
     std::vector<WeightArena *> a = weight_arenas(), b = src.weight_arenas();
     if (a.size() != b.size()) { set_error("copy_weights_from: contexts differ in vocoder presence"); return false; }
     for (size_t i = 0; i < a.size(); ++i) {
@@ -1077,23 +1097,38 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     Q3T_HIP(hipEventRecord(e1, stream_));
     // ---- frame loop: one graph per frame; done flags polled every 16 frames
     if (!graph_for(g_frame_, S, &Engine::enqueue_frame)) return false;
-    int *done_h = nullptr;
-    Q3T_HIP(hipHostMalloc(&done_h, S * 4, hipHostMallocDefault));
+    if (!ensure_pinned((size_t)S * 4)) return false;
+    int *done_h = static_cast<int *>(pin_);
     // streaming (frame callback): chunk [start, start+interval) of every slot copied to pinned memory behind the
-    // frame that completes it; delivered one chunk late so the GPU keeps running the queued frames meanwhile
+    // frame that completes it; delivered one chunk late so the GPU keeps running the queued frames meanwhile.  The
+    // pinned chunks are the context's (chunk_pool_), reused across calls.
     const bool stream_cb = on_frames && interval > 0;
     struct Chunk { int start; int32_t *codes; int *done; hipEvent_t ev; };
+    const size_t chunk_bytes = ((size_t)S * std::max(interval, 1) * NCB + S) * 4;
+    size_t next_chunk = 0;   // chunk_pool_[0, next_chunk) are in use by this call
     std::vector<Chunk> pend;
     std::vector<Chunk> pool;
+    auto take_chunk = [&](Chunk &c) -> bool {
+        if (next_chunk == chunk_pool_.size()) chunk_pool_.push_back(PinnedChunk{});
+        PinnedChunk &pc = chunk_pool_[next_chunk++];
+        if (pc.cap < chunk_bytes) {
+            if (pc.codes) hipHostFree(pc.codes);
+            pc.codes = nullptr;
+            pc.cap = 0;
+            Q3T_HIP(hipHostMalloc(&pc.codes, chunk_bytes, hipHostMallocDefault));
+            pc.cap = chunk_bytes;
+        }
+        if (!pc.ev) Q3T_HIP(hipEventCreateWithFlags(&pc.ev, hipEventDisableTiming));
+        c.codes = pc.codes;
+        c.done = pc.codes + (size_t)S * interval * NCB;
+        c.ev = pc.ev;
+        return true;
+    };
     std::vector<int> &delivered = st.delivered, &stop_at = st.stop_at;
     int n_live = S;   // a fallback re-run regenerates utterances stopped earlier too (their frames are returned)
     auto release = [&]() {
-        for (Chunk &c : pend) pool.push_back(c);
         pend.clear();
-        for (Chunk &c : pool) { hipHostFree(c.codes); hipHostFree(c.done); hipEventDestroy(c.ev); }
         pool.clear();
-        if (done_h) hipHostFree(done_h);
-        done_h = nullptr;
         hipEventDestroy(e0); hipEventDestroy(e1); hipEventDestroy(e2);
     };
     // a chunk is handed to the caller only once the persistent kernels behind it are known to be fault-free
@@ -1124,11 +1159,7 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
         if (stream_cb && (f + 1) % interval == 0) {
             Chunk c;
             if (!pool.empty()) { c = pool.back(); pool.pop_back(); }
-            else {
-                Q3T_HIP(hipHostMalloc(&c.codes, (size_t)S * interval * NCB * 4, hipHostMallocDefault));
-                Q3T_HIP(hipHostMalloc(&c.done, S * 4, hipHostMallocDefault));
-                Q3T_HIP(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
-            }
+            else if (!take_chunk(c)) { release(); return false; }
             c.start = f + 1 - interval;
             for (int s = 0; s < S; ++s)
                 Q3T_HIP(hipMemcpyAsync(c.codes + (size_t)s * interval * NCB, codes_ + ((size_t)s * codes_max_len_ + c.start) * NCB,
@@ -1234,8 +1265,7 @@ bool Engine::alloc_admission() {
         set_error("device allocation failed");
         return false;
     }
-    Q3T_HIP(hipMemset(aticket_, 0, (size_t)S * c_.n_kv * 4));
-    Q3T_HIP(hipDeviceSynchronize());
+    // every buffer was zeroed on stream_ and drained by dalloc before the admission stream exists
     Q3T_HIP(hipStreamCreateWithFlags(&astream_, hipStreamNonBlocking));
     return true;
 }
@@ -1365,8 +1395,9 @@ bool Engine::activate_slot(int k, uint64_t utt, int trailing_len, int n_tok, con
     return select_tokens(sp, alogits_ + (size_t)k * c_.codec_vocab, 1, stream_);
 }
 
-bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
-                            const GenParams &gp, int32_t *codes, int *n_frames, int max_active) {
+bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                                 const GenParams &gp, int32_t *codes, int *n_frames, int max_active, bool *faulted) {
+    *faulted = false;
     if (n_utt <= 0) return true;
     const int S = std::min(max_slots_, n_utt), NCB = 16;
     if (max_active <= 0 || max_active > S) max_active = S;
@@ -1385,7 +1416,6 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
     const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
     if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
     if (gp.max_len > codes_max_len_) { set_error("max_len exceeds the code buffer"); return false; }
-    DeviceLock lk(persist_ && S == 1, device_);
     if (!alloc_admission()) return false;
     q_slots_ = S;
     // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
@@ -1395,14 +1425,12 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
         g_frame_.clear();
     }
     gp_ = gp;
-    int32_t *out_dev = nullptr;   // the finished utterances' codes, copied to the caller once at the end
-    Q3T_HIP(hipMalloc(&out_dev, (size_t)n_utt * gp.max_len * NCB * 4));
-    int *pin = nullptr;   // [S][8] activation staging, [S] done flags, [S] admission targets, one constant 0 (parking)
-    if (hipHostMalloc(&pin, ((size_t)S * 10 + 1) * 4, hipHostMallocDefault) != hipSuccess) {
-        hipFree(out_dev);
-        set_error("hipHostMalloc failed");
-        return false;
-    }
+    // the finished utterances' codes, copied to the caller once at the end (device scratch kept by the context)
+    if (!ensure_qout((size_t)n_utt * gp.max_len * NCB * 4)) return false;
+    int32_t *out_dev = static_cast<int32_t *>(qout_);
+    // [S][8] activation staging, [S] done flags, [S] admission targets, one constant 0 (parking): pinned, kept
+    if (!ensure_pinned(((size_t)S * 10 + 1) * 4)) return false;
+    int *pin = static_cast<int *>(pin_);
     int *done_h = pin + (size_t)S * 8, *tgt_h = pin + (size_t)S * 9, *park = pin + (size_t)S * 10;
     *park = 0;
     hipEvent_t aev = nullptr, pev = nullptr;
@@ -1411,12 +1439,11 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
         hipStreamSynchronize(stream_);
         if (aev) hipEventDestroy(aev);
         if (pev) hipEventDestroy(pev);
-        hipFree(out_dev);
-        hipHostFree(pin);
         policy_slots_ = 0;
         std::vector<uint64_t> ident(max_slots_);   // generate() keys sampling by slot index again
         for (int k = 0; k < max_slots_; ++k) ident[k] = (uint64_t)k;
-        hipMemcpy(utt_, ident.data(), max_slots_ * 8, hipMemcpyHostToDevice);
+        hipMemcpyAsync(utt_, ident.data(), max_slots_ * 8, hipMemcpyHostToDevice, stream_);
+        hipStreamSynchronize(stream_);
     };
     Q3T_HIP(hipEventCreateWithFlags(&aev, hipEventDisableTiming));
     Q3T_HIP(hipEventCreateWithFlags(&pev, hipEventDisableTiming));
@@ -1491,6 +1518,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
         }
         hipGraphExec_t fg = nullptr;
         if (!frame_graph(&fg)) { cleanup(); return false; }
+        if (!persist_fault_hook(S, persist_cp_ ? 2 : 1)) { cleanup(); return false; }
         Q3T_HIP(hipGraphLaunch(fg, stream_));
         ++f;
         if (polled) {
@@ -1526,8 +1554,21 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
     Q3T_HIP(hipStreamSynchronize(stream_));
     const bool fault = persist_error();
     cleanup();
-    if (fault) { set_error("persistent kernel: an in-launch hand-off timed out"); return false; }
+    if (fault) { set_error("persistent kernel: an in-launch hand-off timed out"); *faulted = true; return false; }
     return true;
+}
+
+bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                            const GenParams &gp, int32_t *codes, int *n_frames, int max_active) {
+    const int S = std::min(max_slots_, std::max(n_utt, 1));
+    DeviceLock lk(persist_ && S == 1, device_);
+    bool fault = false;
+    if (generate_queue_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, max_active, &fault)) return true;
+    if (!fault) return false;
+    // a single-slot persistent launch gave up on a hand-off: continue on the launch-per-op graphs, which are
+    // bit-identical, and re-run the queue (sampling is keyed by utterance, so the re-run gives the same codes)
+    if (!persist_recover()) return false;
+    return generate_queue_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, max_active, &fault);
 }
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
@@ -1618,6 +1659,7 @@ bool Engine::cb0_select_host(int S, const float *logits, const uint8_t *seen, co
                              const GenParams &gp, int *tok) {
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int V = c_.codec_vocab;
+    DeviceLock lk(false, device_);
     Q3T_HIP(hipMemcpyAsync(logits_, logits, (size_t)S * V * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(seen_, seen, (size_t)S * V, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, frame, S * 4, hipMemcpyHostToDevice, stream_));

@@ -148,6 +148,15 @@ private:
     bool generate_once(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
                        const GenParams &gp, int32_t *codes, int *n_frames, FrameCb on_frames, void *user, int interval,
                        StreamState &st, bool *fault);
+    bool generate_queue_once(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
+                             const GenParams &gp, int32_t *codes, int *n_frames, int max_active, bool *faulted);
+    // host scratch kept across calls (a per-call hipFree / hipHostFree synchronises the whole device)
+    struct PinnedChunk { size_t cap = 0; int32_t *codes = nullptr; hipEvent_t ev = nullptr; };
+    std::vector<PinnedChunk> chunk_pool_;   // streaming chunks of generate()
+    void *pin_ = nullptr, *qout_ = nullptr;
+    size_t pin_cap_ = 0, qout_cap_ = 0;
+    bool ensure_pinned(size_t bytes);
+    bool ensure_qout(size_t bytes);
     bool enqueue_talker_step(int S, hipStream_t s);
     bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed = false);
     SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;

@@ -27,8 +27,8 @@ constexpr int MAXSPLIT = G / NKV;
 constexpr int R = NH / NKV;     // q heads per kv head
 constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
-constexpr int PSLOT = 264;
-constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgroup only at 32 splits)      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
+constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
+constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgroup only at 32 splits)
 
 template <class V>
 __device__ __forceinline__ V ldgv(const void *p) {
@@ -122,8 +122,9 @@ struct Lds {
     SelLds sel;
     float pl[MAXSPLIT * 264];    // split-0 combiner: every split's partial, split order
     PLayerW layers[MAXL];
-    const uint16_t *heads[16];   // code-predictor lm_heads (MODE 1)        // the layer pointer table, copied once: a pointer fetched from global memory inside
-                                 // the chain would make the next wait cover every weight stream in flight (vmcnt order)
+    const uint16_t *heads[16];   // code-predictor lm_heads (MODE 1)
+    // (layers / heads: the pointer tables, copied once: a pointer fetched from global memory inside the chain would
+    // make the next wait cover every weight stream in flight, vmcnt order)
 };
 
 __device__ __forceinline__ double block_sum_d(double v, double *scr) {

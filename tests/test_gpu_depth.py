@@ -1,0 +1,161 @@
+"""GPU parity at the bench's exact depths (VERDICT r02 "pin parity at the bench's exact depths").
+
+Every headline number of bench.py runs on a configuration checked here, teacher-forced against the CPU oracle
+(q3t_testutil.check_decisions, partial replay with from_frame so the oracle's time stays bounded):
+
+  B=1, 512 frames, max_ctx 544      bench.py's main workload (configs[1]): k_persist<0,64> with up to 9 attention splits
+                                    per kv group at the last frames (KV positions up to 522).  First and last 64 frames
+                                    checked, greedy and T=0.9 (the bench's sampling parameters).
+  64 slots, 512 frames, max_ctx 544 bench.py's `batched` section (configs[2]): the matrix-core path with k_attn_seq over
+                                    up to nch = 9 64-position chunks.  Slots 0, 31 and 63: the last 64 frames (and the
+                                    first 64 of slot 0), T=0.9.
+  continuous batching, 64 slots,    bench.py's `serving` section in miniature: q3t_generate_queue with 160 utterances of
+  160 utterances                    10..40 text tokens (natural EOS), all 64 slots vs 16 in flight bit-identical, three
+                                    admitted utterances (first refill, middle, last) teacher-forced against the oracle.
+
+Source semantics: src/tts_transformer.cpp:2416-2560 (frame loop), :1376-1512 (talker step).  Tolerances: the sampled
+decisions of test_gpu_long.py (5 % off-interval at most, each within 5e-2 of the mass) and the matrix-core near-tie
+fraction of test_gpu_mfma.py (6 %).
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from q3t_testutil import REPO, check_decisions, prompt, synth_dir
+
+sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
+pytestmark = pytest.mark.gpu
+
+NF = 512            # bench.py --frames default
+MAX_CTX = 544       # bench.py: max(frames, roofline_pos) + 32
+TAIL = 64           # frames checked at the end of each run
+MM_MAX_OFF = 0.06
+
+
+@pytest.fixture(scope="module")
+def full():
+    tts, tok = synth_dir("full")
+    orc = Oracle(tts, tok)
+    yield tts, tok, orc
+    orc.close()
+
+
+def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max_off=None):
+    nf = out.shape[0]
+    kw = dict(force_frames=nf, temperature=temperature, top_k=50, seed=seed, utt=utt)
+    if max_off is None:
+        max_off = 0.03 if temperature <= 0 else 0.05
+    res = []
+    if head:   # frames [0, TAIL): the oracle replays the prefix only (max_len = TAIL: no early-stop semantics)
+        res.append(check_decisions(orc, toks, spk, out[:TAIL], max_len=TAIL, max_off_frac=max_off, **kw))
+    # frames [nf - TAIL, nf): the earlier frames advance the oracle's talker with the GPU's codes
+    res.append(check_decisions(orc, toks, spk, out, max_len=nf, from_frame=nf - TAIL, max_off_frac=max_off, **kw))
+    return res
+
+
+@pytest.mark.parametrize("temperature", [0.0, 0.9])
+def test_b1_512_frames_at_bench_context(full, temperature):
+    """k_persist<0,64> at n_ctx 544: 9 splits of 64 positions per kv group by the last frame (position 522)"""
+    import q3t
+    tts, tok, orc = full
+    eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=MAX_CTX)
+    try:
+        assert eng.persist_status() == 0
+        toks = prompt("full")
+        spk = np.zeros(eng.cfg["hidden"], np.float32)
+        out = eng.generate([toks], speakers=[spk], max_len=NF, temperature=temperature, top_k=50, seed=1000,
+                           force_frames=NF)[0]
+        assert out.shape == (NF, 16)
+        assert eng.persist_status() == 0
+        t0 = time.time()
+        for n_off, n_dec, worst in _check_head_tail(orc, toks, spk, out, temperature, 1000, 0):
+            print(f"B=1 512 frames T={temperature}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
+        print(f"  oracle {time.time() - t0:.1f} s")
+    finally:
+        eng.close()
+
+
+@pytest.fixture(scope="module")
+def batched64(full):
+    """64 concurrent utterances x 512 frames at T=0.9 (bench.py `batched`), generated once for the slot checks"""
+    import q3t
+    tts, tok, orc = full
+    n = 64
+    eng = q3t.Engine(tts, None, device=0, max_slots=n, max_ctx=MAX_CTX)
+    try:
+        base = prompt("full")
+        prompts = [base[:4] + [(t + 31 * i) % 900 + 20 for t in base[4:]] for i in range(n)]
+        spk = [np.zeros(eng.cfg["hidden"], np.float32)] * n
+        outs = eng.generate(prompts, speakers=spk, max_len=NF, temperature=0.9, top_k=50, seed=4321,
+                            force_frames=NF)
+    finally:
+        eng.close()
+    assert all(o.shape == (NF, 16) for o in outs)
+    return prompts, spk, outs
+
+
+@pytest.mark.parametrize("slot", [0, 31, 63])
+def test_64_slots_512_frames(full, batched64, slot):
+    """the matrix-core step with k_attn_seq over up to 9 chunks (positions up to 522); generate() keys sampling by
+    slot index"""
+    tts, tok, orc = full
+    prompts, spk, outs = batched64
+    t0 = time.time()
+    for n_off, n_dec, worst in _check_head_tail(orc, prompts[slot], spk[slot], outs[slot], 0.9, 4321, slot,
+                                                head=slot == 0, max_off=MM_MAX_OFF):
+        print(f"64 slots, slot {slot}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
+    print(f"  oracle {time.time() - t0:.1f} s")
+
+
+def _serving_prompts(n, seed):
+    base = prompt("full")
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(10, 41))
+        out.append(base[:4] + [(base[4 + j % (len(base) - 4)] + 13 * i + 7 * j) % 900 + 20 for j in range(k - 4)])
+    return out
+
+
+@pytest.fixture(scope="module")
+def queue64(full):
+    import q3t
+    tts, tok, orc = full
+    slots, n_utt, nf = 64, 160, 128
+    eng = q3t.Engine(tts, None, device=0, max_slots=slots, max_ctx=nf + 40)
+    try:
+        H = eng.cfg["hidden"]
+        prompts = _serving_prompts(n_utt, 2025)
+        spk = [np.zeros(H, np.float32)] * n_utt
+        kw = dict(speakers=spk, max_len=nf, temperature=0.9, top_k=50, seed=99)
+        t0 = time.time()
+        full_q = eng.generate_queue(prompts, max_active=slots, **kw)
+        t1 = time.time()
+        narrow = eng.generate_queue(prompts, max_active=16, **kw)
+        print(f"queue: 64 in flight {t1 - t0:.2f} s, 16 in flight {time.time() - t1:.2f} s")
+    finally:
+        eng.close()
+    return prompts, spk, nf, full_q, narrow
+
+
+def test_queue_64_slots_invariant(queue64):
+    prompts, spk, nf, a, b = queue64
+    lens = [len(c) for c in a]
+    assert 0 < min(lens) and max(lens) <= nf
+    assert sum(n < nf for n in lens) >= 20, "too few EOS stops: the refill path after EOS was not exercised"
+    for u in range(len(prompts)):
+        assert np.array_equal(a[u], b[u]), (u, len(a[u]), len(b[u]))
+
+
+@pytest.mark.parametrize("u", [64, 100, 159])
+def test_queue_64_slots_admitted_match_oracle(full, queue64, u):
+    """utterances admitted into refilled slots (64 = the first refill) teacher-forced with their own utterance id"""
+    tts, tok, orc = full
+    prompts, spk, nf, a, b = queue64
+    n_off, n_dec, worst = check_decisions(orc, prompts[u], spk[u], a[u], max_len=nf, temperature=0.9, top_k=50,
+                                          seed=99, utt=u, max_off_frac=MM_MAX_OFF)
+    print(f"utterance {u}: {len(a[u])} frames, {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
