@@ -175,7 +175,7 @@ def release_uid():
 
 def pmc_traffic(slots):
     """HBM bytes per talker-step replay from the newest committed rocprofv3 FETCH_SIZE pass
-    (profiles/rNN_pmc_fetch_talker_step[_b64].txt, tools/dev/gpu_bench.sh; x2 gfx950 correction applied there)."""
+    (profiles/rNN_pmc_fetch_talker_step[_b64].txt, tools/dev/gpu.sh fetch; x2 gfx950 correction applied there)."""
     import glob
     import re
     suffix = "" if slots == 1 else f"_b{slots}"
@@ -187,7 +187,7 @@ def pmc_traffic(slots):
 
 
 def pmc_file(tag):
-    """newest committed MFMA-utilisation table (tools/dev/gpu_mfma.sh: kernel trace + SQ_INSTS_MFMA / FETCH / WRITE)"""
+    """newest committed MFMA-utilisation table (tools/dev/gpu.sh mfma: kernel trace + SQ_INSTS_MFMA / FETCH / WRITE)"""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_mfma_{tag}.txt")))
     return os.path.relpath(files[-1], REPO) if files else None
