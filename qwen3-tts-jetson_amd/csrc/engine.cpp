@@ -696,9 +696,6 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         p.rope = rope_; p.pos = pos_; p.kc = kc_; p.vc = vc_; p.kv_layer = kv_layer; p.n_ctx = max_ctx_;
         p.head = codec_head_; p.out_norm = out_norm_; p.hidden = hidden_; p.logits = logits_;
         if (select_next) p.sel = select_spec(SEL_CB0, gp_, 1, 0);
-#ifdef Q3T_DEV
-        if (std::getenv("Q3T_PERSIST_DBG")) { p.dbg_qkv = qkv_; p.dbg_attn = attn_; }   // layer-0 intermediates
-#endif
         p.prof = pprof_;
         return persist_talker_step(p, s);
     }

@@ -48,8 +48,6 @@ struct PersistParams {
     uint64_t *gtok = nullptr;      // [16] code-predictor tokens of the launch (granules)
     uint64_t *glog = nullptr;      // [3072] head logits (granules): the selecting workgroup gathers them
     const uint16_t *const *heads = nullptr;   // code-predictor frame: device array of the 15 lm_heads
-    float *dbg_qkv = nullptr;      // development: layer 0's QKV rows / attention output copied out (null = off)
-    uint16_t *dbg_attn = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
 };

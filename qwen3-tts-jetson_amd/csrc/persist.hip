@@ -305,10 +305,6 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 issue_rows_k1024(Lw.gu, gu_row + 16, wu);
                 S.raw[2 * t] = __uint_as_float(u[0]);
                 S.raw[2 * t + 1] = __uint_as_float(u[1]);
-                if (p.dbg_qkv && l == 0 && as == 0) {
-                    p.dbg_qkv[gi] = __uint_as_float(u[0]);
-                    p.dbg_qkv[gi + 1] = __uint_as_float(u[1]);
-                }
             }
             __syncthreads();
             {   // wave v: q head 0 / q head 1 / k (head norm + RoPE) / v (f16 rounding)
@@ -434,18 +430,6 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                     const float a0 = (S.ared[0][h][d] + S.ared[1][h][d]) + (S.ared[2][h][d] + S.ared[3][h][d]);
                     const float a1 = (S.ared[0][h][d + 1] + S.ared[1][h][d + 1]) + (S.ared[2][h][d + 1] + S.ared[3][h][d + 1]);
                     g_put(gout + t, (uint32_t)f2h(a0 / Lsum[h]) | ((uint32_t)f2h(a1 / Lsum[h]) << 16), TAG(ph0 + 5 * l + 1));
-                    if (p.dbg_attn && l == 0) {
-                        p.dbg_attn[(ag * R + h) * D + d] = f2h(a0 / Lsum[h]);
-                        p.dbg_attn[(ag * R + h) * D + d + 1] = f2h(a1 / Lsum[h]);
-                        if (ag == 5) {   // dev dump into the (unused at one split) partial buffer
-                            float *dd = p.part + 16384;
-                            dd[516 + h * D + d] = a0 / Lsum[h];
-                            dd[516 + h * D + d + 1] = a1 / Lsum[h];
-                            dd[t] = S.q_s[0][t]; dd[128 + t] = S.q_s[1][t];
-                            dd[256 + t] = S.kn_s[t]; dd[384 + t] = S.vn_s[t];
-                            if (t == 0) { dd[512] = M[0]; dd[513] = M[1]; dd[514] = Lsum[0]; dd[515] = Lsum[1]; }
-                        }
-                    }
                 }
             } else {
                 // splits >= 1 publish their partial (acc [2][128], m [2], l [2]) as granules; split 0 polls them and

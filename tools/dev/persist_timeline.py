@@ -18,7 +18,7 @@ tts, _ = synth_dir("full")
 eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=pos + 64)
 assert eng.persist_status() == 0
 ms = eng.time_stage(0, 1, pos, 20)
-PH = 160
+PH = 448   # persist.h PROF_PH
 T = eng.debug_read(5, 256 * PH * 4 * 8).view(np.uint64).reshape(256, PH, 4).astype(np.int64)
 t0 = T[:, 0, 3].min()
 T = np.where(T > 0, T - t0, -1) * 10e-3   # -> microseconds
