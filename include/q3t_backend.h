@@ -19,6 +19,7 @@
  *   q3t_ctx_create_shared on one Jetson): RCCL broadcast of rank 0's packed weight blobs over xGMI
  *   q3t_ctx_create_replica, q3t_comm_allreduce_max
  *   q3t_talker_forward    TTSTransformer::forward_step (src/tts_transformer.h:189-192, .cpp:1952-2028)
+ *   q3t_talker_prefill    TTSTransformer::forward_prefill (src/tts_transformer.h:196-198, .cpp:1233-1374, 1829-1920)
  *   q3t_codepred_frame    TTSTransformer::predict_codes_autoregressive (src/tts_transformer.h:203-207) /
  *                         TRTCodePredictor::run_greedy_loop / run_sampling_loop (src/trt_code_predictor.h:68-79)
  *   q3t_cb0_select        CB0 logit processing inside generate (src/tts_transformer.cpp:2417-2499)
@@ -179,6 +180,12 @@ int q3t_tokenizer_decode(const q3t_tokenizer *tok, const int32_t *tokens, int32_
 /* ---- stage entry points (used by the parity tests; each syncs the context stream) */
 int q3t_talker_forward(q3t_ctx *ctx, int n_slots, const float *embd /* [n][H] */, const int32_t *pos /* [n] */,
                        float *hidden /* [n][H] or NULL */, float *logits /* [n][codec_vocab] or NULL */);
+/* causal prefill from position 0 (the pass q3t_generate runs): the n_rows <= 10 rows of each of n_utt utterances in one
+ * pass, K/V into slots 0..n_utt-1; hidden = the final-norm hidden state of every row, logits = the codec logits of each
+ * utterance's last row.  family_slots (0: n_utt) picks the kernels of a family_slots-slot decode step: every row then
+ * equals q3t_talker_forward with that many slots replayed at its position, bit for bit. */
+int q3t_talker_prefill(q3t_ctx *ctx, int n_utt, int n_rows, const float *embd /* [n_utt][n_rows][H] */, int family_slots,
+                       float *hidden /* [n_utt][n_rows][H] or NULL */, float *logits /* [n_utt][codec_vocab] or NULL */);
 int q3t_codepred_frame(q3t_ctx *ctx, int n_slots, const float *hidden /* [n][H] */, const int32_t *cb0 /* [n] */,
                        float temperature, int32_t top_k, uint64_t seed, int32_t frame,
                        int32_t *codes15 /* [n][15] */, float *logits /* [n][15][cp_vocab] or NULL */);

@@ -151,7 +151,15 @@ bool TTSTransformer::forward_prefill(const float *prefill_embd, int32_t n_tokens
     const int32_t H = config_.hidden_size;
     output.resize((size_t)n_tokens * H);
     if (logits_out) logits_out->resize(config_.codec_vocab_size);
-    // causal: row i attends to positions <= n_past + i, exactly the decode step replayed row by row
+    if (n_past == 0 && n_tokens <= 10) {
+        // the causal prefill pass (every row equals the single-slot decode step replayed at its position)
+        std::vector<float> lg(config_.codec_vocab_size);
+        if (q3t_talker_prefill(ctx_, 1, n_tokens, prefill_embd, 1, output.data(), lg.data()) != Q3T_OK) return fail();
+        if (logits_out) *logits_out = lg;
+        last_hidden_.assign(output.end() - H, output.end());
+        return true;
+    }
+    // longer or continued prompts: row i attends to positions <= n_past + i, the decode step replayed row by row
     for (int32_t i = 0; i < n_tokens; ++i) {
         const int32_t pos = n_past + i;
         float *lg = (logits_out && i == n_tokens - 1) ? logits_out->data() : nullptr;

@@ -590,6 +590,136 @@ __global__ void __launch_bounds__(64) k_attn_small(const AttnParams p) {
     *reinterpret_cast<uint2 *>(p.out + (size_t)slot * p.nH * D + (size_t)(g * R + vh) * D + vd) = o;
 }
 
+// ------------------------------------------------------------------ causal prefill attention
+// build_prefill_forward_graph (src/tts_transformer.cpp:1233-1374): every prompt row of an utterance in one pass --
+// q / k head RMSNorm + NEOX RoPE at the row's position, the F16 K/V rows appended to the cache, explicit KQ, scale,
+// diag_mask_inf, soft_max and KQV per row.  One workgroup per (utterance, kv head) holds the utterance's <= 16 rows of
+// that head group in LDS; the head-norm / RoPE prologue is k_attn's (one wave per vector, the same roundings).
+__device__ __forceinline__ float tree16(const float (&v)[16]) {
+    float a[8], b[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = v[2 * k] + v[2 * k + 1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) b[k] = a[2 * k] + a[2 * k + 1];
+    return (b[0] + b[1]) + (b[2] + b[3]);
+}
+template <int D, int R>
+__global__ void __launch_bounds__(256) k_prefill_attn(const PrefillAttnParams p) {
+    constexpr int PMAX = PREFILL_MAX_ROWS, E = D / 64, LPP = D / 8, GROUPS = 256 / LPP;
+    static_assert(PMAX == 16, "tree16: the decode kernel's first 16 positions");
+    __shared__ float q_s[PMAX][R][D];
+    __shared__ float k_s[PMAX][D], v_s[PMAX][D];
+    const int u = blockIdx.x, g = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int plen = p.plen, QKV = (p.nH + 2 * p.nKV) * D;
+    const size_t head_off = ((size_t)p.slot[u] * p.nKV + g) * p.n_ctx * D;
+    // ---- prologue: vectors (row i, v) with v < R the q heads, v == R the k row, v == R + 1 the v row
+    for (int task = wave; task < plen * (R + 2); task += 4) {
+        const int i = task / (R + 2), v = task % (R + 2);
+        const float *qkv = p.qkv + (size_t)(u * plen + i) * QKV;
+        if (v == R + 1) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float y = f16r(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
+                v_s[i][lane + 64 * e] = y;
+                p.vc[head_off + (size_t)i * D + lane + 64 * e] = f2h(y);
+            }
+            continue;
+        }
+        const bool isk = v == R;
+        const float *src = isk ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
+        const float *w = isk ? p.kn : p.qn;
+        const float *rope = p.rope + (size_t)i * D;
+        float x[E];
+        double ss = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { x[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(x[e], x[e]); }
+        ss = wave_sum_d(ss);
+        const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+        float y[E];
+        if constexpr (D == 128) {
+            const float c = rope[2 * lane], sn = rope[2 * lane + 1];
+            y[0] = opaque(opaque(x[0] * c) - opaque(x[1] * sn));
+            y[1] = opaque(opaque(x[0] * sn) + opaque(x[1] * c));
+        } else {
+            const int ii = lane & 31;
+            const float c = rope[2 * ii], sn = rope[2 * ii + 1];
+            const float other = __shfl_xor(x[0], 32, 64);
+            y[0] = lane < 32 ? x[0] * c - other * sn : other * sn + x[0] * c;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const float r = f16r(y[e]);
+            if (isk) {
+                k_s[i][lane + 64 * e] = r;
+                p.kc[head_off + (size_t)i * D + lane + 64 * e] = f2h(r);
+            } else {
+                q_s[i][v][lane + 64 * e] = r;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- attention: one LPP-lane group per (row i, head h); lane li holds dims li*8 .. li*8+7.  Row i < 16 lies in
+    // the first 64-position chunk of the decode kernel, and the sums below are k_attn's reduction tree over that
+    // chunk's 16 leading positions (pairs of neighbours, then pairs of pairs ...; masked positions add +0), so every
+    // prefill row equals the decode step replayed at its position bit for bit.
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    const int grp = t / LPP, li = t % LPP;
+    for (int task = grp; task < plen * R; task += GROUPS) {
+        const int i = task / R, h = task % R;
+        float q8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q8[e] = q_s[i][h][li * 8 + e];
+        float sc[PMAX];
+        float m = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {   // rows j >= plen hold stale LDS: computed, then masked
+            float d = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d = __fmaf_rn(k_s[j][li * 8 + e], q8[e], d);
+            d = group_sum<LPP>(d);
+            sc[j] = j <= i ? __fmul_rn(d, kq_scale) : -INFINITY;
+            m = fmaxf(m, sc[j]);
+        }
+        float pj[PMAX];
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) pj[j] = j <= i ? expf(__fsub_rn(sc[j], m)) : 0.0f;
+        const float l = tree16(pj);
+        uint16_t *o = p.out + (size_t)(u * plen + i) * p.nH * D + (size_t)(g * R + h) * D + li * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float pv[PMAX];
+#pragma unroll
+            for (int j = 0; j < PMAX; ++j)   // k_attn's fma onto 0, then + 0 from its masked passes (-0 -> +0)
+                pv[j] = j <= i ? __fadd_rn(__fmaf_rn(pj[j], v_s[j][li * 8 + e], 0.0f), 0.0f) : 0.0f;
+            o[e] = f2h(tree16(pv) / l);
+        }
+    }
+}
+
+bool prefill_attn(const PrefillAttnParams &p, hipStream_t s) {
+    if (p.n_utt <= 0) return true;
+    if (p.plen < 1 || p.plen > PREFILL_MAX_ROWS || p.nKV <= 0 || p.nH % p.nKV != 0 || !p.qkv || !p.slot || !p.kc || !p.vc ||
+        !p.out || !p.rope) {
+        set_error("prefill_attn: bad parameters");
+        return false;
+    }
+    const dim3 grid(p.n_utt, p.nKV);
+    const int R = p.nH / p.nKV;
+#define Q3T_PF_LAUNCH(DD, RR) hipLaunchKernelGGL((k_prefill_attn<DD, RR>), grid, dim3(256), 0, s, p)
+    if (p.D == 128 && R == 2) Q3T_PF_LAUNCH(128, 2);
+    else if (p.D == 128 && R == 1) Q3T_PF_LAUNCH(128, 1);
+    else if (p.D == 128 && R == 4) Q3T_PF_LAUNCH(128, 4);
+    else if (p.D == 64 && R == 2) Q3T_PF_LAUNCH(64, 2);
+    else if (p.D == 64 && R == 1) Q3T_PF_LAUNCH(64, 1);
+    else if (p.D == 64 && R == 4) Q3T_PF_LAUNCH(64, 4);
+    else { set_error("prefill_attn: unsupported head layout"); return false; }
+#undef Q3T_PF_LAUNCH
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 bool attn_decode(const AttnParams &p, hipStream_t s) {
     if (p.small) {
         if (p.n_ctx > 16 || p.D != 128 || p.nH != 2 * p.nKV) { set_error("attn_decode: small-context attention needs n_ctx <= 16, D 128, 2 q heads per kv head"); return false; }

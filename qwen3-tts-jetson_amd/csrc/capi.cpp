@@ -411,6 +411,16 @@ int q3t_talker_forward(q3t_ctx *ctx, int n, const float *embd, const int32_t *po
     GUARD_END
 }
 
+int q3t_talker_prefill(q3t_ctx *ctx, int n_utt, int n_rows, const float *embd, int family_slots, float *hidden,
+                       float *logits) {
+    GUARD_BEGIN
+    CHECK_CTX(ctx);
+    CHECK_TALKER(ctx);
+    if (!embd) { q3t::set_error("null argument"); return Q3T_ERR; }
+    return ctx->engine.talker_prefill(n_utt, n_rows, embd, family_slots, hidden, logits) ? Q3T_OK : Q3T_ERR;
+    GUARD_END
+}
+
 int q3t_codepred_frame(q3t_ctx *ctx, int n, const float *hidden, const int32_t *cb0, float temperature, int32_t top_k,
                        uint64_t seed, int32_t frame, int32_t *codes15, float *logits) {
     GUARD_BEGIN

@@ -61,7 +61,7 @@ Engine::~Engine() {
     if (device_ >= 0) hipSetDevice(device_);
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
-    for (auto &kv : g_stage_) hipGraphExecDestroy(kv.second);
+    for (auto &kv : g_prefill_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     voc_.reset();
     for (void *p : allocs_) hipFree(p);
@@ -370,6 +370,8 @@ bool Engine::alloc_state() {
     cp_pos_ = dalloc<int>((size_t)16 * S);
     seen_ = dalloc<uint8_t>((size_t)S * c_.codec_vocab);
     utt_ = dalloc<uint64_t>(S);
+    seed_dev_ = dalloc<uint64_t>(1);
+    slot_iota_ = dalloc<int>(S);
     trailing_ = dalloc<float>((size_t)S * max_trailing_ * H);
     tts_pad_ = dalloc<float>((size_t)S * H);
     prefill_ = dalloc<float>((size_t)S * 10 * H);
@@ -388,6 +390,9 @@ bool Engine::alloc_state() {
     std::vector<uint64_t> utt(S);
     for (int s = 0; s < S; ++s) utt[s] = (uint64_t)s;
     Q3T_HIP(hipMemcpy(utt_, utt.data(), S * 8, hipMemcpyHostToDevice));
+    std::vector<int> iota(S);
+    for (int s = 0; s < S; ++s) iota[s] = s;
+    Q3T_HIP(hipMemcpy(slot_iota_, iota.data(), S * 4, hipMemcpyHostToDevice));
     return true;
 }
 
@@ -438,8 +443,7 @@ bool Engine::persist_recover() {
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
-    for (auto &kv : g_stage_) hipGraphExecDestroy(kv.second);
-    g_talker_.clear(); g_frame_.clear(); g_cp_.clear(); g_stage_.clear();
+    g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
     persist_ = persist_cp_ = false;
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
     // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
@@ -529,11 +533,20 @@ static int splitk_for(int N, int S, int K) {
         if (ok(ks)) return ks;
     return 1;
 }
+// the causal prefill's attention in place of the decode launch: layer `il`'s cache and the stack's activations
+static bool prefill_layer_attn(const PrefillAttnParams &pf, const Config &c, const DevLayer &l, const float *qkv,
+                               const float *rope, uint16_t *kc, uint16_t *vc, int n_ctx, uint16_t *attn, hipStream_t s) {
+    PrefillAttnParams q = pf;
+    q.qkv = qkv; q.qn = l.qn; q.kn = l.kn; q.eps = c.eps; q.rope = rope; q.kc = kc; q.vc = vc;
+    q.n_ctx = n_ctx; q.nH = c.n_heads; q.nKV = c.n_kv; q.D = c.head_dim; q.out = attn;
+    return prefill_attn(q, s);
+}
+
 static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
                              unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
-                             float *final_side, int S_main = 0, bool cp_attn = false) {
+                             float *final_side, int S_main = 0, bool cp_attn = false, const PrefillAttnParams *pf = nullptr) {
     // S_main: the batch whose kernel choices this stack reproduces (a continuous-batching admission runs ONE slot
     // with the S_main-slot kernels, so its per-token arithmetic is the batch's)
     if (S_main <= 0) S_main = S;
@@ -570,7 +583,7 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         a.small = 0;   // experiment builds: the code predictor on k_attn_seq / k_attn as before
 #endif
         a.part = part; a.ticket = ticket; a.out = attn;
-        if (!attn_decode(a, s)) return false;
+        if (pf ? !prefill_layer_attn(*pf, c, l, qkv, rope, a.kc, a.vc, n_ctx, attn, s) : !attn_decode(a, s)) return false;
         GemvParams o;
         o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
         o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
@@ -607,10 +620,12 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
 static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, int S, float *x, float *qkv,
                           uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc, size_t kv_layer, int n_ctx,
                           int max_splits, const int *pos, const float *rope, float *part, unsigned *ticket,
-                          hipStream_t s, const StackInput *in0 = nullptr, bool fused_cp_attn = false) {
+                          hipStream_t s, const StackInput *in0 = nullptr, bool fused_cp_attn = false,
+                          const PrefillAttnParams *pf = nullptr, int family_b = 0) {
+    // pf: the causal prefill (S = its rows, run with the vector kernels of a family_b-slot step)
     const int H = c.hidden, D = c.head_dim, QKV = (c.n_heads + 2 * c.n_kv) * D;
     // batched (matrix-core) path: gathers become their own launch and the code predictor's attention runs unfused
-    const bool mm = S >= gemm_mfma_min_batch();
+    const bool mm = (family_b > 0 ? family_b : S) >= gemm_mfma_min_batch();
     if (mm) fused_cp_attn = false;
     for (size_t il = 0; il < layers.size(); ++il) {
         const DevLayer &l = layers[il];
@@ -625,11 +640,14 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
                 g.sel = in0->sel; g.sel_logits = in0->sel_logits;
             }
         }
-        g.out_f32 = qkv; g.ldo = QKV;
+        g.out_f32 = qkv; g.ldo = QKV; g.family_b = family_b;
         if (!gemv(g, s)) return false;
         GemvParams o;
-        o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
-        if (fused_cp_attn) {
+        o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S; o.family_b = family_b;
+        if (pf) {
+            if (!prefill_layer_attn(*pf, c, l, qkv, rope, kc + il * kv_layer, vc + il * kv_layer, n_ctx, attn, s)) return false;
+            o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
+        } else if (fused_cp_attn) {
             // code predictor: attention recomputed inside the O-projection prologue (<= 16 positions)
             o.pro = PRO_CPATT;
             o.att.qkv = qkv; o.att.ld = QKV; o.att.qn = l.qn; o.att.kn = l.kn; o.att.eps = c.eps;
@@ -651,10 +669,10 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
         GemvParams gu;
         gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
         gu.pro = PRO_RMS; gu.x = x; gu.ldx = H; gu.nw = l.ffn_norm; gu.eps = c.eps;
-        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter;
+        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter; gu.family_b = family_b;
         if (!gemv(gu, s)) return false;
         GemvParams dn;
-        dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;
+        dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S; dn.family_b = family_b;
         dn.pro = PRO_F16; dn.x = hmlp; dn.ldx = c.inter;
         dn.resid = x; dn.ldr = H; dn.out_f32 = x; dn.ldo = H;
         if (!gemv(dn, s)) return false;
@@ -671,7 +689,7 @@ SelectSpec Engine::select_spec(int mode, const GenParams &gp, int frame_offset, 
     sp.ticket = sel_ticket_;
     sp.tokens = tokens_; sp.codes = codes_; sp.max_len = codes_max_len_; sp.ncb = 16;
     sp.frame = frame_; sp.frame_offset = frame_offset; sp.done = done_;
-    sp.temperature = gp.temperature; sp.top_k = gp.top_k; sp.seed = gp.seed; sp.utt = utt_;
+    sp.temperature = gp.temperature; sp.top_k = gp.top_k; sp.seed = gp.seed; sp.seed_dev = seed_dev_; sp.utt = utt_;
     sp.step = step;
     sp.seen = seen_; sp.n_tokens = n_tokens_; sp.force_frames = force_; sp.eos = c_.codec_eos; sp.rep = gp.rep_penalty;
     return sp;
@@ -866,6 +884,87 @@ bool Engine::set_slot_state(int S, const std::vector<int> &pos, const std::vecto
     return true;
 }
 
+// ------------------------------------------------------------------------------------------ causal prefill
+// build_prefill_forward_graph (src/tts_transformer.cpp:1233-1374): the plen prompt rows of n_utt utterances in ONE
+// pass of the talker stack -- every projection over all n_utt * plen rows (one weight stream for the whole prompt
+// instead of plen), causal attention per utterance (prefill_attn) writing the K/V rows [0, plen) of slot pf_slot_[u]
+// directly.  The projections run the kernels of an S_main-slot decode step with its K split (family_b / S_main),
+// and the attention reproduces the decode kernel's reduction tree over its first positions, so every row equals the
+// S_main-slot step replayed at its position bit for bit (tests/cpp/test_host_api.cpp, tests/test_gpu_prefill.py).
+// Outputs: pf_hid_ / pf_logits_ rows u * plen + plen - 1 (final-norm hidden state and codec logits of the last row).
+bool Engine::ensure_prefill() {
+    if (pf_x_) return true;
+    const size_t R = (size_t)max_slots_ * 10, H = c_.hidden, D = c_.head_dim;
+    const size_t QKV = (size_t)(c_.n_heads + 2 * c_.n_kv) * D;
+    pf_x_ = dalloc<float>(R * H);
+    pf_xn_ = dalloc<uint16_t>(R * H);
+    pf_parts_ = dalloc<float>(4 * R * H);
+    pf_qkv_ = dalloc<float>(R * QKV);
+    pf_attn_ = dalloc<uint16_t>(R * c_.n_heads * D);
+    pf_hmlp_ = dalloc<uint16_t>(R * c_.inter);
+    pf_hid_ = dalloc<float>(R * H);
+    pf_logits_ = dalloc<float>(R * c_.codec_vocab);
+    pf_slot_ = dalloc<int>(max_slots_);
+    if (!pf_x_ || !pf_xn_ || !pf_parts_ || !pf_qkv_ || !pf_attn_ || !pf_hmlp_ || !pf_hid_ || !pf_logits_ || !pf_slot_) {
+        set_error("device allocation failed");
+        return false;
+    }
+    return true;
+}
+
+// the captured body: key = (S_main * 1024 + n_utt) * 16 + plen
+bool Engine::enqueue_prefill_rows(int key, hipStream_t s) {
+    const int plen = key % 16, n_utt = key / 16 % 1024, S_main = key / (16 * 1024);
+    const int rows = n_utt * plen, H = c_.hidden, V = c_.codec_vocab;
+    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
+    const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
+    PrefillAttnParams pf;
+    pf.slot = pf_slot_; pf.n_utt = n_utt; pf.plen = plen;
+    GemvParams h;   // final RMSNorm (hidden side output) + codec head over every row, as the S_main-slot step
+    h.W = codec_head_; h.N = V; h.K = H; h.B = rows; h.out_f32 = pf_logits_; h.ldo = V;
+    if (S_main >= gemm_mfma_min_batch()) {
+        if (!decoder_stack_mm(c_, opt_.attn_split, L_, rows, pf_x_, pf_xn_, pf_parts_, pf_qkv_, pf_attn_, pf_hmlp_, kc_, vc_,
+                              kv_layer, max_ctx_, max_splits, pos_, rope_, part_, ticket_, s, nullptr, out_norm_, pf_hid_,
+                              S_main, false, &pf))
+            return false;
+        h.pro = PRO_F16; h.x = pf_xn_; h.ldx = H; h.force_mm = true;
+        return gemv(h, s);
+    }
+    if (!decoder_stack(c_, L_, rows, pf_x_, pf_qkv_, pf_attn_, pf_hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_,
+                       part_, ticket_, s, nullptr, false, &pf, S_main))
+        return false;
+    h.pro = PRO_RMS; h.x = pf_x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = pf_hid_; h.family_b = S_main;
+    return gemv(h, s);
+}
+
+// src: [n_utt][10][H] prompt rows (rows [0, plen) of each used); pf_slot_[0, n_utt) must hold the target slots
+bool Engine::prefill(int n_utt, int plen, const float *src, int S_main, hipStream_t s) {
+    const int H = c_.hidden;
+    if (n_utt <= 0 || n_utt > max_slots_ || plen < 1 || plen > 10 || S_main < 1 || S_main > 4096) {
+        set_error("prefill: bad shape");
+        return false;
+    }
+    if (!ensure_prefill()) return false;
+    Q3T_HIP(hipMemcpy2DAsync(pf_x_, (size_t)plen * H * 4, src, (size_t)10 * H * 4, (size_t)plen * H * 4, n_utt,
+                             hipMemcpyDeviceToDevice, s));
+    const int key = (S_main * 1024 + n_utt) * 16 + plen;
+    if (!g_prefill_.count(key)) {
+        hipGraph_t graph = nullptr;
+        Q3T_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        const bool ok = enqueue_prefill_rows(key, s);
+        hipError_t e = hipStreamEndCapture(s, &graph);
+        if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
+        if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
+        hipGraphExec_t exec = nullptr;
+        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
+        g_prefill_[key] = exec;
+    }
+    Q3T_HIP(hipGraphLaunch(g_prefill_[key], s));
+    return true;
+}
+
 // ------------------------------------------------------------------------------------------ prefill pieces
 bool Engine::enqueue_text_projection(int n_rows, hipStream_t s) {
     return enqueue_text_projection(n_rows, s, proj_idx_, proj_h_, proj_out_);
@@ -976,6 +1075,12 @@ bool Engine::prefill_embd(const int32_t *toks, int n, const float *spk, int lang
 }
 
 // ------------------------------------------------------------------------------------------ hot path
+bool Engine::set_seed(uint64_t seed, hipStream_t s) {
+    seed_host_ = seed;   // a member: the (pageable) source outlives the copy
+    Q3T_HIP(hipMemcpyAsync(seed_dev_, &seed_host_, 8, hipMemcpyHostToDevice, s));
+    return true;
+}
+
 bool Engine::copy_weights_from(Engine &src) {
     DeviceLock lk(false, device_);
     std::vector<WeightArena *> a = weight_arenas(), b = src.weight_arenas();
@@ -1024,11 +1129,13 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     const int n_pre = gp.language_id < 0 ? 3 : 4;
     const int plen = 3 + (n_pre + (has_spk ? 1 : 0) + 2 - 1) + 1;
     if (plen + gp.max_len + 8 > max_ctx_) { set_error("max_len exceeds the context reserved at ctx creation"); return false; }
-    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty && gp.seed == gp_.seed)) {
+    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty)) {
         for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
         g_frame_.clear();
     }
     gp_ = gp;
+    if (!set_seed(gp.seed, stream_)) return false;
+    if (!ensure_prefill()) return false;
     hipEvent_t e0, e1, e2;
     hipEventCreate(&e0); hipEventCreate(&e1); hipEventCreate(&e2);
     Q3T_HIP(hipEventRecord(e0, stream_));
@@ -1073,15 +1180,14 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     Q3T_HIP(hipMemcpyAsync(done_, done0.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemsetAsync(seen_, 0, (size_t)S * c_.codec_vocab, stream_));
     Q3T_HIP(hipMemsetAsync(codes_, 0, (size_t)S * codes_max_len_ * NCB * 4, stream_));
-    // ---- prefill: plen talker steps (token-by-token; the step graph is replayed)
-    if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false;
+    // ---- prefill: one causal pass over the plen rows of every slot; the last row's hidden state / logits per slot
+    Q3T_HIP(hipMemcpyAsync(pf_slot_, slot_iota_, S * 4, hipMemcpyDeviceToDevice, stream_));
+    if (!prefill(S, plen, prefill_, policy_slots_ > 0 ? policy_slots_ : S, stream_)) return false;
+    Q3T_HIP(hipMemcpy2DAsync(hidden_, H * 4, pf_hid_ + (size_t)(plen - 1) * H, (size_t)plen * H * 4, H * 4, S,
+                             hipMemcpyDeviceToDevice, stream_));
+    Q3T_HIP(hipMemcpy2DAsync(logits_, (size_t)c_.codec_vocab * 4, pf_logits_ + (size_t)(plen - 1) * c_.codec_vocab,
+                             (size_t)plen * c_.codec_vocab * 4, (size_t)c_.codec_vocab * 4, S, hipMemcpyDeviceToDevice, stream_));
     std::vector<int> posv(S);
-    for (int t = 0; t < plen; ++t) {
-        Q3T_HIP(hipMemcpy2DAsync(x_, H * 4, prefill_ + (size_t)t * H, (size_t)10 * H * 4, H * 4, S, hipMemcpyDeviceToDevice, stream_));
-        Q3T_HIP(hipMemcpyAsync(pos_, cp_pos_ + (size_t)t * max_slots_, S * 4, hipMemcpyDeviceToDevice, stream_));
-        if (!persist_fault_hook(S, 1)) return false;
-        Q3T_HIP(hipGraphLaunch(g_talker_[S], stream_));
-    }
     for (int s = 0; s < S; ++s) posv[s] = plen;
     if (!set_slot_state(S, posv, frame0)) return false;
     if (fused_select_ && !select_tokens(select_spec(SEL_CB0, gp_, 0, 0), logits_, S, stream_)) return false;
@@ -1223,42 +1329,26 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
 // ------------------------------------------------------------------------------------------ continuous batching
 // Admissions run on their own stream with private scratch, overlapping the frame loop of the other slots (at many
 // slots the decode step leaves most of the chip idle).  The slots freed since the last admission are admitted
-// together: their prompts are projected in one pass and prefilled as a batch of STAGING slots (private x / hidden /
-// logits rows and a 16-position staging KV cache), then k_kv_stage_copy moves the prefill's K/V rows [0, plen) into
-// the target slots.  A target slot is parked in the frame loop meanwhile (done >= 0: no selection, no advance, its
-// position >= plen): the frame graph still runs it, but writes only its own x / hidden / logits rows and the KV row
-// at its parked position, none of which the admission writes.  The slot joins the frame loop (activate_slot, main
-// stream, between two frames) once its admission batch has finished.  On the matrix-core path the staging batch runs
-// the running batch's kernels (S_main), whose per-token arithmetic does not depend on the other tokens: a slot's
-// prefill is what generate()'s batched prefill computes for it, whichever slots were admitted alongside.
+// together: their prompts are projected in one pass and run through ONE causal prefill (Engine::prefill), which
+// writes the K/V rows [0, plen) of the target slots directly.  A target slot is parked in the frame loop meanwhile
+// (done >= 0: no selection, no advance, its position >= plen): the frame graph still runs it, but writes only its own
+// x / hidden / logits rows and the KV row at its parked position, none of which the admission writes.  The slot joins
+// the frame loop (activate_slot, main stream, between two frames) once its admission batch has finished.  The prefill
+// runs the running batch's kernels (S_main = q_slots_), whose per-row arithmetic does not depend on the other rows: a
+// slot's prefill is what generate()'s prefill computes for it, whichever slots were admitted alongside.
 bool Engine::alloc_admission() {
-    if (ax_) return true;
-    const int S = max_slots_, H = c_.hidden, D = c_.head_dim;
-    const int QKV = (c_.n_heads + 2 * c_.n_kv) * D;
-    ax_ = dalloc<float>((size_t)S * H);
-    axn_ = dalloc<uint16_t>((size_t)S * H);
-    aparts_ = dalloc<float>((size_t)4 * S * H);
-    aqkv_ = dalloc<float>((size_t)S * QKV);
-    aattn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
-    ahmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
-    apart_ = dalloc<float>((size_t)S * c_.n_heads * (D + 2));
-    aticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
-    const size_t skv = (size_t)S * c_.n_kv * 16 * D;
-    akc_ = dalloc<uint16_t>(skv * c_.n_layers);
-    avc_ = dalloc<uint16_t>(skv * c_.n_layers);
+    if (astream_) return true;
+    const int S = max_slots_, H = c_.hidden;
+    if (!ensure_prefill()) return false;
     aprefill_ = dalloc<float>((size_t)S * 10 * H);
-    ashid_ = dalloc<float>((size_t)S * H);
-    aslog_ = dalloc<float>((size_t)S * c_.codec_vocab);
     ahidden_ = dalloc<float>((size_t)S * H);
     alogits_ = dalloc<float>((size_t)S * c_.codec_vocab);
-    astage_pos_ = dalloc<int>(S);
-    atarget_ = dalloc<int>(S);
     aproj_cap_ = S * (max_trailing_ + 16);
     aproj_idx_ = dalloc<int>(aproj_cap_);
     aproj_h_ = dalloc<uint16_t>((size_t)aproj_cap_ * c_.text_dim);
     aproj_out_ = dalloc<float>((size_t)aproj_cap_ * H);
     arecipe_ = dalloc<RowRecipe>(aproj_cap_);
-    if (!ax_ || !akc_ || !avc_ || !aticket_ || !alogits_ || !arecipe_ || !aproj_out_) {
+    if (!aprefill_ || !ahidden_ || !alogits_ || !aproj_idx_ || !aproj_h_ || !aproj_out_ || !arecipe_) {
         set_error("device allocation failed");
         return false;
     }
@@ -1267,29 +1357,8 @@ bool Engine::alloc_admission() {
     return true;
 }
 
-// the talker step of staging slots 0..a-1 at position astage_pos_[j] (the prefill of an admission batch), with the
-// kernels of the running q_slots_-slot batch
-bool Engine::enqueue_stage_step(int a, hipStream_t s) {
-    const int H = c_.hidden;
-    const size_t kvl = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
-    GemvParams h;   // final RMSNorm (hidden side output) + codec head, as enqueue_talker
-    h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = a;
-    h.out_f32 = aslog_; h.ldo = c_.codec_vocab;
-    if (q_slots_ >= gemm_mfma_min_batch()) {
-        if (!decoder_stack_mm(c_, opt_.attn_split, L_, a, ax_, axn_, aparts_, aqkv_, aattn_, ahmlp_, akc_, avc_, kvl, 16, 1,
-                              astage_pos_, rope_, apart_, aticket_, s, nullptr, out_norm_, ashid_, q_slots_))
-            return false;
-        h.pro = PRO_F16; h.x = axn_; h.ldx = H; h.force_mm = true;
-        return gemv(h, s);
-    }
-    if (!decoder_stack(c_, L_, a, ax_, aqkv_, aattn_, ahmlp_, akc_, avc_, kvl, 16, 1, astage_pos_, rope_, apart_, aticket_, s))
-        return false;
-    h.pro = PRO_RMS; h.x = ax_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = ashid_;
-    return gemv(h, s);
-}
-
 // admission batch on stream `as`: utterances utt[j] into slots tgt[j] (text projection, prefill / trailing / pad
-// rows, plen staging steps, K/V rows into the target slots, hidden / logits rows per target slot).  tgt_h: pinned
+// rows, the causal prefill into the target slots, hidden / logits rows per target slot).  tgt_h: pinned
 // copy of tgt (alive until the batch has run); trailing_len[j]: the slot's trailing-text length
 bool Engine::admit_batch(const std::vector<int> &tgt, const std::vector<int> &utt, const int32_t *const *tokens,
                          const int *n_tokens, const float *const *speaker, const GenParams &gp, int plen, hipStream_t as,
@@ -1335,34 +1404,16 @@ bool Engine::admit_batch(const std::vector<int> &tgt, const std::vector<int> &ut
     if ((int)rec.size() > aproj_cap_) { set_error("recipe overflow"); return false; }
     Q3T_HIP(hipMemcpyAsync(arecipe_, rec.data(), rec.size() * sizeof(RowRecipe), hipMemcpyHostToDevice, as));
     if (!rows_recipe(arecipe_, (int)rec.size(), H, as)) return false;
-    const int gkey = q_slots_ * 4096 + a;
-    if (!g_stage_.count(gkey)) {   // the staging step for (batch size, admission size), captured once
-        hipGraph_t graph = nullptr;
-        Q3T_HIP(hipStreamBeginCapture(as, hipStreamCaptureModeThreadLocal));
-        const bool ok = enqueue_stage_step(a, as);
-        hipError_t e = hipStreamEndCapture(as, &graph);
-        if (!ok) { if (graph) hipGraphDestroy(graph); return false; }
-        if (e != hipSuccess) { set_error(std::string("graph capture: ") + hipGetErrorString(e)); return false; }
-        hipGraphExec_t exec = nullptr;
-        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (e != hipSuccess) { set_error(std::string("graph instantiate: ") + hipGetErrorString(e)); return false; }
-        g_stage_[gkey] = exec;
-    }
-    for (int t = 0; t < plen; ++t) {
-        Q3T_HIP(hipMemcpy2DAsync(ax_, H * 4, aprefill_ + (size_t)t * H, (size_t)10 * H * 4, H * 4, a, hipMemcpyDeviceToDevice, as));
-        Q3T_HIP(hipMemcpyAsync(astage_pos_, cp_pos_ + (size_t)t * max_slots_, a * 4, hipMemcpyDeviceToDevice, as));
-        Q3T_HIP(hipGraphLaunch(g_stage_[gkey], as));
-    }
+    // the causal prefill of the batch with the running batch's kernels (S_main = q_slots_), K/V straight into the
+    // target slots' rows [0, plen)
     for (int j = 0; j < a; ++j) tgt_h[j] = tgt[j];
-    Q3T_HIP(hipMemcpyAsync(atarget_, tgt_h, a * 4, hipMemcpyHostToDevice, as));
-    const size_t skvl = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim, kvl = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
-    if (!kv_stage_copy(akc_, avc_, kc_, vc_, atarget_, a, c_.n_layers, c_.n_kv, plen, c_.head_dim, skvl, kvl, 16, max_ctx_, as))
-        return false;
+    Q3T_HIP(hipMemcpyAsync(pf_slot_, tgt_h, a * 4, hipMemcpyHostToDevice, as));
+    if (!prefill(a, plen, aprefill_, q_slots_, as)) return false;
+    const int V = c_.codec_vocab;
     for (int j = 0; j < a; ++j) {
-        Q3T_HIP(hipMemcpyAsync(ahidden_ + (size_t)tgt[j] * H, ashid_ + (size_t)j * H, H * 4, hipMemcpyDeviceToDevice, as));
-        Q3T_HIP(hipMemcpyAsync(alogits_ + (size_t)tgt[j] * c_.codec_vocab, aslog_ + (size_t)j * c_.codec_vocab,
-                               (size_t)c_.codec_vocab * 4, hipMemcpyDeviceToDevice, as));
+        const size_t r = (size_t)j * plen + plen - 1;
+        Q3T_HIP(hipMemcpyAsync(ahidden_ + (size_t)tgt[j] * H, pf_hid_ + r * H, H * 4, hipMemcpyDeviceToDevice, as));
+        Q3T_HIP(hipMemcpyAsync(alogits_ + (size_t)tgt[j] * V, pf_logits_ + r * V, (size_t)V * 4, hipMemcpyDeviceToDevice, as));
     }
     return true;
 }
@@ -1417,11 +1468,12 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
     q_slots_ = S;
     // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
     hipStream_t as = (S == 1 && persist_) ? stream_ : astream_;
-    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty && gp.seed == gp_.seed)) {
+    if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty)) {
         for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
         g_frame_.clear();
     }
     gp_ = gp;
+    if (!set_seed(gp.seed, stream_)) return false;
     // the finished utterances' codes, copied to the caller once at the end (device scratch kept by the context)
     if (!ensure_qout((size_t)n_utt * gp.max_len * NCB * 4)) return false;
     int32_t *out_dev = static_cast<int32_t *>(qout_);
@@ -1599,6 +1651,25 @@ bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
 }
 
 // ------------------------------------------------------------------------------------------ test entry points
+bool Engine::talker_prefill(int n_utt, int n_rows, const float *embd, int family_slots, float *hidden, float *logits) {
+    if (n_utt <= 0 || n_utt > max_slots_) { set_error("bad utterance count"); return false; }
+    if (n_rows <= 0 || n_rows > 10 || n_rows > max_ctx_) { set_error("prefill rows must be in [1, 10]"); return false; }
+    if (family_slots < 0 || family_slots > 4096) { set_error("bad family slot count"); return false; }
+    const int H = c_.hidden, V = c_.codec_vocab;
+    DeviceLock lk(false, device_);
+    if (!ensure_prefill()) return false;
+    Q3T_HIP(hipMemcpy2DAsync(prefill_, (size_t)10 * H * 4, embd, (size_t)n_rows * H * 4, (size_t)n_rows * H * 4, n_utt,
+                             hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipMemcpyAsync(pf_slot_, slot_iota_, n_utt * 4, hipMemcpyDeviceToDevice, stream_));
+    if (!prefill(n_utt, n_rows, prefill_, family_slots > 0 ? family_slots : n_utt, stream_)) return false;
+    if (hidden) Q3T_HIP(hipMemcpyAsync(hidden, pf_hid_, (size_t)n_utt * n_rows * H * 4, hipMemcpyDeviceToHost, stream_));
+    if (logits)
+        Q3T_HIP(hipMemcpy2DAsync(logits, (size_t)V * 4, pf_logits_ + (size_t)(n_rows - 1) * V, (size_t)n_rows * V * 4,
+                                 (size_t)V * 4, n_utt, hipMemcpyDeviceToHost, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
 bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hidden, float *logits) {
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
@@ -1628,6 +1699,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;
+    if (!set_seed(seed, stream_)) return false;
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     g_frame_.clear();
     Q3T_HIP(hipMemcpyAsync(hidden_, hidden, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
@@ -1664,7 +1736,9 @@ bool Engine::cb0_select_host(int S, const float *logits, const uint8_t *seen, co
     std::vector<int> force(S, gp.force_frames), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(force_, force.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(done_, dn.data(), S * 4, hipMemcpyHostToDevice, stream_));
-    if (!select_tokens(select_spec(SEL_CB0, gp, 0, 0), logits_, S, stream_)) return false;
+    SelectSpec sp = select_spec(SEL_CB0, gp, 0, 0);
+    sp.seed_dev = nullptr;
+    if (!select_tokens(sp, logits_, S, stream_)) return false;
     std::vector<int> tk((size_t)S * 16);
     Q3T_HIP(hipMemcpyAsync(tk.data(), tokens_, tk.size() * 4, hipMemcpyDeviceToHost, stream_));
     Q3T_HIP(hipStreamSynchronize(stream_));

@@ -108,6 +108,7 @@ public:
     bool copy_weights_from(Engine &src);
 
     // ---- stage entry points (host buffers) used by the parity tests
+    bool talker_prefill(int n_utt, int n_rows, const float *embd, int family_slots, float *hidden, float *logits);
     bool talker_forward(int S, const float *embd, const int *pos, float *hidden, float *logits);
     bool codepred_frame(int S, const float *hidden, const int *cb0, float temperature, int top_k, uint64_t seed,
                         int frame, int32_t *codes15, float *logits_all);
@@ -167,22 +168,26 @@ private:
     bool graph_for_key(std::map<int, hipGraphExec_t> &cache, int key, int S, bool (Engine::*fn)(int, hipStream_t));
     int policy_slots_ = 0;         // > 0: the batched stacks choose kernels as for this many slots (queue graphs)
     bool set_slot_state(int S, const std::vector<int> &pos, const std::vector<int> &frame);
-    // continuous batching: admission batches on their own stream and scratch (staging slots + staging KV), then
+    // causal prefill (one pass over the prompt rows of n_utt utterances, K/V written into slots pf_slot_[u])
+    bool ensure_prefill();
+    bool enqueue_prefill_rows(int key, hipStream_t s);
+    bool prefill(int n_utt, int plen, const float *src, int S_main, hipStream_t s);
+    std::map<int, hipGraphExec_t> g_prefill_;
+    float *pf_x_ = nullptr, *pf_qkv_ = nullptr, *pf_parts_ = nullptr, *pf_hid_ = nullptr, *pf_logits_ = nullptr;
+    uint16_t *pf_xn_ = nullptr, *pf_attn_ = nullptr, *pf_hmlp_ = nullptr;
+    int *pf_slot_ = nullptr, *slot_iota_ = nullptr;
+    // continuous batching: admission batches on their own stream (their prefill on the prefill scratch), then
     // activation of each slot on the main stream between two frames
     bool alloc_admission();
-    bool enqueue_stage_step(int a, hipStream_t s);
     bool admit_batch(const std::vector<int> &tgt, const std::vector<int> &utt, const int32_t *const *tokens,
                      const int *n_tokens, const float *const *speaker, const GenParams &gp, int plen, hipStream_t as,
                      int *tgt_h, std::vector<int> &trailing_len);
     bool activate_slot(int slot, uint64_t utt, int trailing_len, int n_tok, const GenParams &gp, int plen, int *state_h);
     bool enqueue_text_projection(int n_rows, hipStream_t s, const int *idx, uint16_t *hbuf, float *out);
-    std::map<int, hipGraphExec_t> g_stage_;
     hipStream_t astream_ = nullptr;
-    float *ax_ = nullptr, *aqkv_ = nullptr, *aparts_ = nullptr, *apart_ = nullptr, *aprefill_ = nullptr;
-    float *ashid_ = nullptr, *aslog_ = nullptr, *ahidden_ = nullptr, *alogits_ = nullptr, *aproj_out_ = nullptr;
-    uint16_t *axn_ = nullptr, *aattn_ = nullptr, *ahmlp_ = nullptr, *aproj_h_ = nullptr, *akc_ = nullptr, *avc_ = nullptr;
-    unsigned *aticket_ = nullptr;
-    int *astage_pos_ = nullptr, *atarget_ = nullptr, *aproj_idx_ = nullptr;
+    float *aprefill_ = nullptr, *ahidden_ = nullptr, *alogits_ = nullptr, *aproj_out_ = nullptr;
+    uint16_t *aproj_h_ = nullptr;
+    int *aproj_idx_ = nullptr;
     RowRecipe *arecipe_ = nullptr;
     int aproj_cap_ = 0;
     int q_slots_ = 0;              // slot count of the running queue (the batch the admissions reproduce)
@@ -218,6 +223,9 @@ private:
     int *n_tokens_ = nullptr, *force_ = nullptr, *trailing_len_ = nullptr, *cp_pos_ = nullptr;
     uint8_t *seen_ = nullptr;
     uint64_t *utt_ = nullptr;
+    uint64_t *seed_dev_ = nullptr;   // the sampling seed read by the captured selections (SelectSpec::seed_dev)
+    uint64_t seed_host_ = 0;
+    bool set_seed(uint64_t seed, hipStream_t s);
     float *trailing_ = nullptr, *tts_pad_ = nullptr, *prefill_ = nullptr;
     int32_t *codes_ = nullptr;
     int codes_max_len_ = 0;

@@ -46,7 +46,7 @@ __device__ __forceinline__ float4 gldf4(const void *p) {
 __device__ __forceinline__ half8_t as_h8(const uint4 &u) { return __builtin_bit_cast(half8_t, u); }
 }  // namespace
 
-constexpr int MM_ROWS = 32, MM_TOK = 64;   // weight rows / tokens per workgroup
+constexpr int MM_ROWS = 32;   // weight rows per workgroup (tokens: TT x 32)
 
 // epilogue shared by the kernels: acc register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r;
 // sumf(tt, i) returns the K-summed value of register i of token tile tt for this lane
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr bool kLds = PRO != PRO_F16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-    const int K = NCH * 256, N = p.N;
+    const int K = NCH * 256;
     const int row0 = blockIdx.x * MM_ROWS;
     const int t0 = blockIdx.y * (TT * 32);
     const int nt = min(TT * 32, p.B - t0);
@@ -558,7 +558,7 @@ static int nch_of(int K) {
 }
 
 bool gemm_mfma_supported(const GemvParams &p) {
-    if ((p.B < gemm_mfma_min_batch() && !p.force_mm) || p.sel.mode != SEL_NONE || p.N % MM_ROWS != 0) return false;
+    if (((p.family_b > 0 ? p.family_b : p.B) < gemm_mfma_min_batch() && !p.force_mm) || p.sel.mode != SEL_NONE || p.N % MM_ROWS != 0) return false;
     const int nch = nch_of(p.K);
     if (!nch) return false;
     const bool swiglu = p.act == ACT_SWIGLU;

@@ -763,7 +763,12 @@ bool gemv(const GemvParams &p, hipStream_t s) {
     const int gy = (p.B + bt - 1) / bt;
     const int rpg = swiglu ? 2 : 1;
     const int units = swiglu ? p.N / 2 : p.N;   // output rows (SwiGLU: gate/up pairs)
-    auto blocks_for = [&](int ks) { return (long)((units + (16 / ks) - 1) / (16 / ks)) * gy; };
+    // the K split (the only launch choice that changes a row's summation order) from the family batch's grid
+    const int fb = p.family_b > 0 ? p.family_b : p.B;
+    int fbt = fb == 1 ? 1 : fb == 2 ? 2 : fb <= 4 ? 4 : 8;
+    while (fbt > 1 && (size_t)Kp * 2 * fbt > 48 * 1024) fbt /= 2;
+    const int fgy = (fb + fbt - 1) / fbt;
+    auto blocks_for = [&](int ks) { return (long)((units + (16 / ks) - 1) / (16 / ks)) * fgy; };
     int ks = 4;
     for (int c : {1, 2, 4})
         if (blocks_for(c) >= gemv_min_blocks()) { ks = c; break; }

@@ -32,6 +32,8 @@ struct SelectSpec {
     float temperature = 0.f;
     int top_k = 50;
     uint64_t seed = 0;
+    const uint64_t *seed_dev = nullptr;   // if set, the seed is read here (one device word: a captured graph serves
+                                          // every seed; the host writes it before the frame loop)
     const uint64_t *utt = nullptr;  // [S]
     int step = 0;                   // SEL_CP: 0..14
     // SEL_CB0
@@ -109,6 +111,8 @@ struct GemvParams {
     int ksplit = 1;
     bool force_mm = false;   // matrix-core path even below gemm_mfma_min_batch() (a single slot reproducing the
                              // per-token arithmetic of a batch that runs there)
+    int family_b = 0;        // > 0: kernel family (vector / matrix core) and K split chosen as for a batch of
+                             // family_b rows -- the per-row arithmetic of that batch, for any B (the causal prefill)
 };
 bool gemv(const GemvParams &p, hipStream_t s);   // routes wide batches to gemm_mfma (gemm_mfma.hip)
 // matrix-core path for B >= gemm_mfma_min_batch() tokens (Q3T_MFMA_MIN_B, default 4; 0 = off): F16 / F32 / RMS / LN
@@ -141,6 +145,23 @@ struct AttnParams {
 };
 bool attn_decode(const AttnParams &p, hipStream_t s);
 constexpr int ATTN_CHUNK = 64;
+
+// Causal attention over the prompt rows of n_utt utterances in one launch (the real prefill,
+// src/tts_transformer.cpp:1233-1374): row i of utterance u is token u*plen + i at position i of slot slot[u]; q / k
+// head RMSNorm + NEOX RoPE at i, F16 K/V rows written to the slot's cache rows [0, plen), softmax(QK^T / sqrt(D)) V over
+// positions 0..i.  One workgroup per (utterance, kv head).
+constexpr int PREFILL_MAX_ROWS = 16;
+struct PrefillAttnParams {
+    const float *qkv = nullptr;   // [n_utt * plen][(nH + 2 nKV) * D] f32 raw QKV rows
+    const float *qn = nullptr, *kn = nullptr;
+    float eps = 1e-6f;
+    const float *rope = nullptr;  // [pos][D] (cos, sin) pairs
+    uint16_t *kc = nullptr, *vc = nullptr;   // this layer's cache base [slot][nKV][n_ctx][D] f16
+    const int *slot = nullptr;    // [n_utt] cache slot of each utterance
+    int n_ctx = 0, n_utt = 0, plen = 0, nH = 0, nKV = 0, D = 0;
+    uint16_t *out = nullptr;      // [n_utt * plen][nH * D] f16 (the O-projection input)
+};
+bool prefill_attn(const PrefillAttnParams &p, hipStream_t s);
 constexpr int ATTN_MAX_SPLITS = 160;   // n_ctx <= 10240
 
 
@@ -152,12 +173,6 @@ bool advance(int *pos, int *frame, const int *done, int S, hipStream_t s);   // 
 struct RowTerm { const void *ptr; int is_f16; };
 struct RowRecipe { float *out; RowTerm t[3]; };
 bool rows_recipe(const RowRecipe *recipe_dev, int n_rows, int H, hipStream_t s);
-// K/V rows [0, rows) of staging slots 0..n-1 (cache [layer][slot][kv][src_ctx][D]) -> slots dst_slot[0..n) of a
-// [layer][slot][kv][dst_ctx][D] cache (continuous-batching admissions)
-bool kv_stage_copy(const uint16_t *sk, const uint16_t *sv, uint16_t *dk, uint16_t *dv, const int *dst_slot, int n,
-                   int n_layers, int nkv, int rows, int D, size_t src_layer, size_t dst_layer, int src_ctx, int dst_ctx,
-                   hipStream_t s);
-
 // batched residual + RMSNorm between the matrix-core projections (one workgroup per token, H <= 1024):
 //   x[b] = xin[b] + parts[0][b] + ... + parts[ksplit-1][b]   (written to x when parts or xin != x)
 //   xn[b] = f16((x[b] * rsqrt(mean(x[b]^2) + eps)) * nw)       (double sums, as the GEMV prologues)

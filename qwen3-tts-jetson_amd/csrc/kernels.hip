@@ -93,28 +93,6 @@ __global__ void k_rows_recipe(const RowRecipe *rec, int H) {
         R.out[h] = v;
     }
 }
-// continuous batching: K/V rows [0, rows) of staging slot j -> slot dst_slot[j] of the context's cache, every layer
-// and kv head (blockIdx: x = j, y = kv head, z = layer * 2 + K/V); rows * D halves per block, 16-byte moves
-__global__ void k_kv_stage_copy(const uint16_t *sk, const uint16_t *sv, uint16_t *dk, uint16_t *dv, const int *dst_slot,
-                                int nkv, int rows, int D, size_t src_layer, size_t dst_layer, int src_ctx, int dst_ctx) {
-    const int j = blockIdx.x, g = blockIdx.y, l = blockIdx.z >> 1, v = blockIdx.z & 1;
-    const uint16_t *src = (v ? sv : sk) + l * src_layer + ((size_t)j * nkv + g) * src_ctx * D;
-    uint16_t *dst = (v ? dv : dk) + l * dst_layer + ((size_t)dst_slot[j] * nkv + g) * dst_ctx * D;
-    const int n16 = rows * D / 8;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x)
-        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-}
-bool kv_stage_copy(const uint16_t *sk, const uint16_t *sv, uint16_t *dk, uint16_t *dv, const int *dst_slot, int n,
-                   int n_layers, int nkv, int rows, int D, size_t src_layer, size_t dst_layer, int src_ctx, int dst_ctx,
-                   hipStream_t s) {
-    if (n <= 0) return true;
-    if ((rows * D) % 8 != 0) { set_error("kv_stage_copy: rows * D must be a multiple of 8"); return false; }
-    hipLaunchKernelGGL(k_kv_stage_copy, dim3(n, nkv, n_layers * 2), dim3(256), 0, s, sk, sv, dk, dv, dst_slot, nkv, rows, D,
-                       src_layer, dst_layer, src_ctx, dst_ctx);
-    Q3T_HIP(hipGetLastError());
-    return true;
-}
-
 bool rows_recipe(const RowRecipe *recipe_dev, int n_rows, int H, hipStream_t s) {
     if (n_rows <= 0) return true;
     hipLaunchKernelGGL(k_rows_recipe, dim3(n_rows), dim3(256), 0, s, recipe_dev, H);

@@ -393,6 +393,7 @@ __device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v
     if (sp.done[s] >= 0) return -1;   // uniform over the workgroup
     const int t = threadIdx.x, V = sp.V, vpt = (V + 255) / 256;
     const int frame = sp.frame[s] + sp.frame_offset;
+    const uint64_t seed = sp.seed_dev ? *sp.seed_dev : sp.seed;
     int keep = -1;
     float u;
     if constexpr (MODE == SEL_CB0) {
@@ -422,9 +423,9 @@ __device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v
             if (masked) v[e] = -INFINITY;
         }
         keep = masked ? -1 : EOS;
-        u = uniform24(sp.seed, sp.utt[s], (uint64_t)frame, 0);
+        u = uniform24(seed, sp.utt[s], (uint64_t)frame, 0);
     } else {
-        u = uniform24(sp.seed, sp.utt[s], (uint64_t)frame, (uint64_t)sp.step + 1);
+        u = uniform24(seed, sp.utt[s], (uint64_t)frame, (uint64_t)sp.step + 1);
     }
     return sp.temperature <= 0.0f ? sel_argmax(v, V, vpt, S) : sel_sample(v, V, vpt, sp.temperature, sp.top_k, u, keep, S);
 }

@@ -88,6 +88,7 @@ _lib.q3t_tokenizer_info.argtypes = [_P] + [C.POINTER(C.c_int32)] * 4
 _lib.q3t_tokenizer_encode.argtypes = [_P, C.c_char_p, C.c_int64, _I, _P, C.c_int32, C.POINTER(C.c_int32)]
 _lib.q3t_tokenizer_decode.argtypes = [_P, _P, C.c_int32, _P, C.c_int64, C.POINTER(C.c_int64)]
 _lib.q3t_talker_forward.argtypes = [_P, _I, _fp, _ip, _P, _P]
+_lib.q3t_talker_prefill.argtypes = [_P, _I, _I, _fp, _I, _P, _P]
 _lib.q3t_codepred_frame.argtypes = [_P, _I, _fp, _ip, _F, C.c_int32, C.c_uint64, C.c_int32, _ip, _P]
 _lib.q3t_cb0_select.argtypes = [_P, _I, _fp, np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS"), _ip, _ip,
                                 C.POINTER(GenParams), _ip]
@@ -100,7 +101,7 @@ EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_de
            "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_vocoder_decode_batch", "q3t_vocoder_set_batch_frames", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
-           "q3t_tokenizer_decode", "q3t_talker_forward",
+           "q3t_tokenizer_decode", "q3t_talker_forward", "q3t_talker_prefill",
            "q3t_codepred_frame", "q3t_cb0_select", "q3t_project_text", "q3t_prefill_embd", "gpu_fp32_to_fp16",
            "gpu_argmax_f32", "gpu_embedding_lookup_by_gpu_id", "gpu_sample_topk_f32"]
 
@@ -403,6 +404,19 @@ class Engine:
         hid = np.zeros((n, self.cfg["hidden"]), np.float32)
         lg = np.zeros((n, self.cfg["codec_vocab"]), np.float32)
         _check(_lib.q3t_talker_forward(self.h, n, embd, pos, _addr(hid), _addr(lg)))
+        return hid, lg
+
+    def talker_prefill(self, embd, family_slots=0):
+        """causal prefill from position 0: embd [n_utt][n_rows][H] -> (hidden [n_utt][n_rows][H], last-row logits
+        [n_utt][V]); K/V rows [0, n_rows) of slots 0..n_utt-1 (TTSTransformer::forward_prefill)"""
+        H = self.cfg["hidden"]
+        embd = np.ascontiguousarray(embd, np.float32)
+        if embd.ndim == 2:
+            embd = embd[None]
+        n_utt, n_rows = embd.shape[0], embd.shape[1]
+        hid = np.zeros((n_utt, n_rows, H), np.float32)
+        lg = np.zeros((n_utt, self.cfg["codec_vocab"]), np.float32)
+        _check(_lib.q3t_talker_prefill(self.h, n_utt, n_rows, embd.reshape(-1), int(family_slots), _addr(hid), _addr(lg)))
         return hid, lg
 
     def codepred_frame(self, hidden, cb0, temperature=0.0, top_k=50, seed=0, frame=0, want_logits=False):
