@@ -47,6 +47,7 @@ Options Options::from_env() {
     o.persist = env_flag("Q3T_PERSIST", true);
     o.persist_cp = env_flag("Q3T_PERSIST_CP", true);
     o.cp_fused_attn = env_flag("Q3T_CP_FUSED_ATTN", true);
+    o.cp_qkv_table = env_flag("Q3T_CP_QKV_TABLE", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
     o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
@@ -426,11 +427,44 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
         std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
+        if (opt_.cp_qkv_table && !build_cp_qkv_table()) return false;
     }
     // (pstate_ was zeroed on the context stream by dalloc)
 #ifdef Q3T_DEV
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
 #endif
+    return true;
+}
+
+// Layer 0 of code-predictor passes 1..15 starts from a table row (codec_embd / code_pred.codec_embd[p-2]), so its
+// raw QKV row is a function of the token alone: computed here once for every token of the 15 tables with the per-op
+// pass-input GEMV (PRO_RMS_G1, the K split of a 1-slot step: family_b = 1), whose arithmetic the persistent frame's
+// phase A reproduces bit for bit.  The persistent frame then reads the row instead of running layer 0's norm + QKV
+// phase and its all-to-all edge (persist.hip).  520 MB of f32.
+bool Engine::build_cp_qkv_table() {
+    const int H = c_.hidden, QKV = (c_.n_heads + 2 * c_.n_kv) * c_.head_dim;
+    if (c_.codec_vocab != 3072 || c_.cp_vocab != 2048 || (int)cp_embd_.size() < 14) return true;   // shapes persist.hip supports
+    const size_t rows = persist_qkv_table_rows();
+    cp_qkvtab_ = dalloc<float>(rows * QKV);
+    int *iota = dalloc<int>(c_.codec_vocab);
+    if (!cp_qkvtab_ || !iota) { set_error("device allocation failed (code-predictor QKV table)"); return false; }
+    std::vector<int> ih(c_.codec_vocab);
+    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
+    Q3T_HIP(hipMemcpyAsync(iota, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+    size_t row0 = 0;
+    for (int t = 0; t < 15; ++t) {
+        const int V = t == 0 ? c_.codec_vocab : c_.cp_vocab;
+        GemvParams g;
+        g.W = CP_[0].qkv; g.N = QKV; g.K = H; g.B = V;
+        g.pro = PRO_RMS_G1; g.nw = CP_[0].attn_norm; g.eps = c_.eps;
+        g.gs.tok = iota; g.gs.tok_ld = 1; g.gs.tok_col0 = 0;
+        g.gs.tab0 = t == 0 ? codec_embd_ : cp_embd_[t - 1];
+        g.out_f32 = cp_qkvtab_ + row0 * QKV; g.ldo = QKV;
+        g.family_b = 1;
+        if (!gemv(g, stream_)) return false;
+        row0 += V;
+    }
+    Q3T_HIP(hipStreamSynchronize(stream_));
     return true;
 }
 
@@ -766,6 +800,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         p.gs.tok = tokens_; p.gs.tok_ld = 16; p.gs.tabs = tabs16_dev_;
         p.rope = rope_; p.kc = cpkc_; p.vc = cpvc_; p.kv_layer = kv_layer; p.n_ctx = 16;
         p.heads = heads_dev_; p.out_norm = cp_out_norm_; p.logits = cp_logits_;
+        p.qkvtab = cp_qkvtab_;
         p.sel = select_spec(SEL_CP, gp_, 0, 0);
         p.prof = pprof_;
         return persist_cp_frame(p, s);

@@ -56,6 +56,7 @@ struct PLayerW;
 // Development-only knobs (Q3T_TALKER_LAYERS, Q3T_PERSIST_PROF, ...) exist only in a -DQ3T_DEV build.
 struct Options {
     bool persist = true, persist_cp = true, cp_fused_attn = true, fused_select = true, defer_cp_select = true;
+    bool cp_qkv_table = true;   // Q3T_CP_QKV_TABLE: the persistent code-predictor frame reads layer 0's QKV rows from a table
     bool attn_split = false;
     unsigned persist_fault_at = 0;
     int poll_every = 16;   // frames between done-flag polls
@@ -246,6 +247,8 @@ private:
     bool persist_fallback_ = false;   // persistent kernels disabled after a flagged fault
     PLayerW *pl_dev_ = nullptr, *pl_cp_dev_ = nullptr;
     const uint16_t **heads_dev_ = nullptr;
+    float *cp_qkvtab_ = nullptr;         // persistent code-predictor frame: layer 0's QKV row per table token
+    bool build_cp_qkv_table();
     bool persist_cp_ = false;
     uint8_t *pstate_ = nullptr;
     uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline

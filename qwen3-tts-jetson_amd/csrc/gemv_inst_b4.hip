@@ -1,0 +1,11 @@
+// gemv_inst_b4.hip — explicit instantiations of the GEMV launch templates (gemv_kernel.h)
+#include "gemv_kernel.h"
+
+namespace q3t {
+template void launch_pro<1, 4, 1>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+template void launch_pro<1, 4, 2>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+template void launch_pro<1, 4, 4>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+template void launch_pro<2, 4, 1>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+template void launch_pro<2, 4, 2>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+template void launch_pro<2, 4, 4>(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s);
+}  // namespace q3t

@@ -48,6 +48,10 @@ struct PersistParams {
     uint64_t *gtok = nullptr;      // [16] code-predictor tokens of the launch (granules)
     uint64_t *glog = nullptr;      // [3072] head logits (granules): the selecting workgroup gathers them
     const uint16_t *const *heads = nullptr;   // code-predictor frame: device array of the 15 lm_heads
+    // code-predictor frame (optional): layer 0's raw QKV row of every table token, f32 [3072 + 14 * 2048][4096] (pass 1:
+    // codec_embd rows, pass p >= 2: code_pred.codec_embd[p-2] rows), computed with the per-op QKV GEMV's arithmetic
+    // (persist_qkv_table_rows): passes 1..15 then skip layer 0's norm + QKV phase and its edge
+    const float *qkvtab = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
 };
@@ -68,5 +72,6 @@ bool persist_talker_step(const PersistParams &p, hipStream_t s);
 // sel = SEL_CP (step set per pass)
 bool persist_cp_frame(const PersistParams &p, hipStream_t s);
 int persist_chunk(int n_ctx);                    // positions per attention split workgroup
+size_t persist_qkv_table_rows();                 // rows of PersistParams::qkvtab (3072 + 14 * 2048)
 
 }  // namespace q3t

@@ -29,6 +29,12 @@ constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait give
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
 constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
 constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgroup only at 32 splits)
+#ifndef Q3T_SEL_HOIST0
+#define Q3T_SEL_HOIST0 1        // talker step: SELW loads the selection's per-slot inputs at launch start
+#endif
+#ifndef Q3T_SEL_HOIST1
+#define Q3T_SEL_HOIST1 1        // code-predictor frame: the selectors load them at launch start
+#endif
 
 template <class V>
 __device__ __forceinline__ V ldgv(const void *p) {
@@ -189,6 +195,13 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     const int ag = w & (NKV - 1), as = w >> 3;   // attention role: kv group, split
     const bool att = as < nsplit;
     const bool has_pos = as == nsplit - 1;
+    // code-predictor frame with the layer-0 QKV table: the 8 attention workgroups select each pass's token themselves
+    // (no hand-off before the next pass's attention), workgroup 0 records it and hands it to the others (they need it
+    // only for layer 0's residual row, off the chain); otherwise SELW selects and hands the token to everyone
+    const bool tab = MODE == 1 && p.qkvtab != nullptr;
+    const bool selector = tab ? att : w == SELW;
+    const bool committer = tab ? w == 0 : w == SELW;
+    int cur_tok = MODE == 1 ? p.gs.tok[0] : 0;   // tab: this attention workgroup's token of the previous pass
     const int pg = t >> 4, li = t & 15;          // attention: position group, 8-dim chunk
 
     // development timeline (p.prof): wall clock at wait start / input arrived / output published, per phase
@@ -219,6 +232,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     };
     if (t < p.n_layers) S.layers[t] = p.L[t];
     if (MODE == 1 && t < 15) S.heads[t] = p.heads[t];
+    // the selection's per-slot inputs (done, frame, seed, utterance, CB0 seen bytes) loaded before any wait, so that
+    // none of these dependent loads sits between the last logits and the token
+    SelPre spre;
+    constexpr int SELM = MODE == 0 ? SEL_CB0 : SEL_CP;
+    constexpr bool HOIST = MODE == 1 ? Q3T_SEL_HOIST1 : Q3T_SEL_HOIST0;
+    if (HOIST && p.sel.mode != SEL_NONE && selector) sel_prefetch<SELM>(p.sel, 0, spre);
     issue_rows_k1024(p.L[0].qkv, w * 16 + grp, wq);
     if (att) issue_kv(0, pos);
     float4 nwA = ldf4(p.L[0].attn_norm + 4 * t), nwD;   // attn_norm(l) / ffn_norm(l) for this thread's 4 elements
@@ -231,9 +250,25 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     for (int l = 0; l < nl; ++l) {
         const PLayerW Lw = S.layers[l];
         const size_t kvo = (size_t)l * p.kv_layer + (size_t)ag * p.n_ctx * D;
+        const bool from_tab = tab && l == 0 && pass >= 1;   // layer 0's QKV rows come from the table
+        uint2 traw = make_uint2(0, 0);                      // from_tab: this thread's two raw QKV values
         // ================= A: x -> RMSNorm -> QKV rows
         float4 x;
-        if (l == 0) {
+        if (from_tab) {
+            int tok = cur_tok;
+            if (!att && pass >= 2) {
+                uint32_t u1[1];
+                g_wait<1>(p.gtok + pass - 1, TAG(ph0 - 1), u1, c);
+                tok = min((int)u1[0], p.sel.V - 1);   // an aborted wait returns a stale payload: keep it in the table
+            }
+            if (att) {   // the attention operands straight from the table row (gi: B's layout of the raw row)
+                const int gi = t < 128 ? ag * 256 + 2 * t : t < 192 ? NH * D + ag * D + 2 * (t - 128) : (NH + NKV) * D + ag * D + 2 * (t - 192);
+                const size_t row = (size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok;
+                traw = ld8(p.qkvtab + row * QKVN + gi);
+            }
+            const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);   // the residual row
+            x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
+        } else if (l == 0) {
             if (MODE == 0 && p.gather) {
                 const GatherSum &gs = p.gs;
                 const int *tk = gs.tok;
@@ -277,6 +312,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
         __syncthreads();
         *reinterpret_cast<float4 *>(S.xr + 4 * t) = x;
+        if (!from_tab) {
         rms_to_lds(x, nwA, p.eps, S, nullptr);
         __syncthreads();
         if (l > 0) PROF(ph0 + 5 * l + 0, 3);
@@ -288,6 +324,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             if (l16 == 0) g_put(p.gqkv + w * 16 + grp, __float_as_uint(acc), TAG(ph0 + 5 * l + 0));
             PROF(ph0 + 5 * l + 0, 2);
         }
+        }
         // ================= B: attention (kv group ag, split as)
         if (!att) {
             nwD = ldf4(Lw.ffn_norm + 4 * t);
@@ -298,7 +335,8 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 uint32_t u[2];
                 const int gi = t < 128 ? ag * 256 + 2 * t : t < 192 ? NH * D + ag * D + 2 * (t - 128) : (NH + NKV) * D + ag * D + 2 * (t - 192);
                 PROF(ph0 + 5 * l + 1, 0);
-                g_wait<2>(p.gqkv + gi, TAG(ph0 + 5 * l + 0), u, c);
+                if (from_tab) { u[0] = traw.x; u[1] = traw.y; }
+                else g_wait<2>(p.gqkv + gi, TAG(ph0 + 5 * l + 0), u, c);
                 PROF(ph0 + 5 * l + 1, 1);
                 nwD = ldf4(Lw.ffn_norm + 4 * t);
                 issue_rows_k1024(Lw.gu, gu_row, wg);
@@ -527,7 +565,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             } else if (head_here) {
                 nwA = ldf4(p.out_norm + 4 * t);
                 issue_rows_k1024(MODE == 0 ? p.head : S.heads[pass - 1], w * RPW + min(grp, RPW - 1), wq);
-            } else {   // code-predictor pass 0 (no head): the next pass's layer 0
+            } else if (!tab) {   // code-predictor pass 0 (no head): the next pass's layer 0
                 nwA = ldf4(S.layers[0].attn_norm + 4 * t);
                 issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
             }
@@ -601,8 +639,10 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 #pragma unroll
         for (int tt = 0; tt < 8; ++tt) wh[tt] = wq[tt];
         if (MODE == 1 && pass + 1 < npass) {
-            nwA = ldf4(S.layers[0].attn_norm + 4 * t);
-            issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
+            if (!tab) {
+                nwA = ldf4(S.layers[0].attn_norm + 4 * t);
+                issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
+            }
             if (att) issue_kv(0, pos + 1);
         }
         float a0 = 0.0f, a1 = 0.0f;
@@ -620,11 +660,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         PROF(hph, 2);
         // one fixed workgroup gathers the logits granules and selects: no arrival ticket, no store drain and no
         // reload of the logits row on the chain (the last 256 -> 1 fan-in of the step)
-        if (w == SELW) {
+        if (selector) {
             int tok = -1;
             SelectSpec sp = p.sel;
             if (MODE == 1) sp.step = pass - 1;
-            if (p.prof && t == 0) p.prof[((size_t)w * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection start
+            const bool rec = p.prof && t == 0 && w == (tab ? 1 : SELW);   // one selector records its timeline
+            if (rec) p.prof[((size_t)w * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection start
             if (sp.mode != SEL_NONE) {
                 constexpr int VPT = MODE == 0 ? VOC / G : 2048 / G;
                 uint32_t u[VPT];
@@ -632,14 +673,16 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 float v[SEL_VPT_MAX];
 #pragma unroll
                 for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = e < VPT ? __uint_as_float(u[e]) : -INFINITY;
-                tok = select_token_regs<MODE == 0 ? SEL_CB0 : SEL_CP>(sp, v, 0, S.sel);
+                if (!HOIST) sel_prefetch<SELM>(sp, 0, spre);
+                tok = select_token_pre<SELM>(sp, spre, v, S.sel);
             }
-            if (p.prof && t == 0) p.prof[((size_t)0 * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection end (row 0)
-            if (t == 0) {
+            if (rec) p.prof[((size_t)0 * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection end (row 0)
+            if (committer && t == 0) {
+                if (MODE == 1 && pass + 1 < npass) g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
                 if (tok >= 0) select_commit(sp, 0, tok);
                 if (pass + 1 == npass) __hip_atomic_store(p.seq, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (MODE == 1 && pass + 1 < npass) g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
             }
+            if (MODE == 1) cur_tok = max(tok, 0);
         }
     }
     }   // passes
@@ -671,6 +714,8 @@ static const int g_min_chunk = [] { const char *e = std::getenv("Q3T_PERSIST_CH"
 #else
 static constexpr int g_min_chunk = 64;
 #endif
+size_t persist_qkv_table_rows() { return (size_t)VOC + 14 * 2048; }
+
 int persist_chunk(int n_ctx) {
     int ch = g_min_chunk;
     while (ch * MAXSPLIT < n_ctx) ch += 64;

@@ -381,24 +381,57 @@ __device__ __forceinline__ void sel_load_exact(const float *row, float (&v)[SEL_
     for (int e = VPT; e < SEL_VPT_MAX; ++e) v[e] = -INFINITY;
 }
 
-// the token of slot s (uniform over the workgroup), or -1 if the slot is done; no side effects
-// select_token on a row already loaded into the owner registers (sel_load): lets a kernel issue the logits loads
-// ahead of its weight stream
-// MODE: SEL_CB0 / SEL_CP at compile time (the code-predictor path carries none of the CB0 rules), or SEL_NONE to
-// dispatch on sp.mode
-template <int MODE = SEL_NONE>
-__device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v)[SEL_VPT_MAX], int s, SelLds &S) {
-    if constexpr (MODE == SEL_NONE)
-        return sp.mode == SEL_CB0 ? select_token_regs<SEL_CB0>(sp, v, s, S) : select_token_regs<SEL_CP>(sp, v, s, S);
-    if (sp.done[s] >= 0) return -1;   // uniform over the workgroup
+// Per-slot selection inputs that do not depend on the logits (done flag, frame, seed, utterance id, CB0 prompt
+// length / EOS mask / seen bytes of this thread's indices).  A kernel that knows its slot early loads them before
+// it waits for the logits, so none of these dependent global loads sits on the chain after the logits arrive.
+struct SelPre {
+    int done, frame, n_tokens, force;
+    uint64_t seed, utt;
+    uint32_t seen[SEL_VPT_MAX / 4];   // CB0 seen flags of this thread's indices, byte e of the thread in byte e % 4 of word e / 4
+};
+template <int MODE>
+__device__ __forceinline__ void sel_prefetch(const SelectSpec &sp, int s, SelPre &q) {
     const int t = threadIdx.x, V = sp.V, vpt = (V + 255) / 256;
-    const int frame = sp.frame[s] + sp.frame_offset;
-    const uint64_t seed = sp.seed_dev ? *sp.seed_dev : sp.seed;
+    q.done = sp.done[s];
+    q.frame = sp.frame[s] + sp.frame_offset;
+    q.seed = sp.seed_dev ? *sp.seed_dev : sp.seed;
+    q.utt = sp.utt[s];
+    q.n_tokens = 0;
+    q.force = 0;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX / 4; ++e) q.seen[e] = 0;
+    if constexpr (MODE == SEL_CB0) {
+        q.n_tokens = sp.n_tokens[s];
+        q.force = sp.force_frames[s];
+        if (sp.rep != 1.0f) {
+            const uint8_t *seen = sp.seen + (size_t)s * V;
+            if (V % 1024 == 0) {   // vpt % 4 == 0 and every index in range: whole words (the row is 4-byte aligned)
+                const uint32_t *sw = reinterpret_cast<const uint32_t *>(seen + (size_t)t * vpt);
+#pragma unroll
+                for (int e = 0; e < SEL_VPT_MAX / 4; ++e)
+                    if (4 * e < vpt) q.seen[e] = sw[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < SEL_VPT_MAX; ++e) {
+                    const int i = t * vpt + e;
+                    if (e < vpt && i < V) q.seen[e >> 2] |= (uint32_t)seen[i] << (8 * (e & 3));
+                }
+            }
+        }
+    }
+}
+
+// the token of a slot from its prefetched inputs (uniform over the workgroup), or -1 if the slot is done; no side
+// effects.  MODE: SEL_CB0 / SEL_CP at compile time (the code-predictor path carries none of the CB0 rules)
+template <int MODE>
+__device__ __forceinline__ int select_token_pre(const SelectSpec &sp, const SelPre &q, float (&v)[SEL_VPT_MAX], SelLds &S) {
+    if (q.done >= 0) return -1;   // uniform over the workgroup
+    const int t = threadIdx.x, V = sp.V, vpt = (V + 255) / 256;
+    const int frame = q.frame;
     int keep = -1;
     float u;
     if constexpr (MODE == SEL_CB0) {
         const int EOS = sp.eos;
-        const uint8_t *seen = sp.seen + (size_t)s * V;
         float m = -INFINITY;
 #pragma unroll
         for (int e = 0; e < SEL_VPT_MAX; ++e) {
@@ -406,13 +439,13 @@ __device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v
             if (e >= vpt || i >= V) continue;
             float x = v[e];
             if (i >= V - 1024 && i != EOS) x = -INFINITY;                          // :2418-2422
-            if (sp.rep != 1.0f && seen[i]) x = x > 0.0f ? x / sp.rep : x * sp.rep;  // :2425-2435
+            if (sp.rep != 1.0f && ((q.seen[e >> 2] >> (8 * (e & 3))) & 0xffu)) x = x > 0.0f ? x / sp.rep : x * sp.rep;  // :2425-2435
             v[e] = x;
             m = fmaxf(m, x);
         }
         m = sel_block_max(m, S);
-        const int expected = max(20, sp.n_tokens[s] * 4);                          // :2439-2445
-        const bool masked = frame < sp.force_frames[s];
+        const int expected = max(20, q.n_tokens * 4);                              // :2439-2445
+        const bool masked = frame < q.force;
 #pragma unroll
         for (int e = 0; e < SEL_VPT_MAX; ++e) {
             if (t * vpt + e != EOS || e >= vpt) continue;
@@ -423,11 +456,26 @@ __device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v
             if (masked) v[e] = -INFINITY;
         }
         keep = masked ? -1 : EOS;
-        u = uniform24(seed, sp.utt[s], (uint64_t)frame, 0);
+        u = uniform24(q.seed, q.utt, (uint64_t)frame, 0);
     } else {
-        u = uniform24(seed, sp.utt[s], (uint64_t)frame, (uint64_t)sp.step + 1);
+        u = uniform24(q.seed, q.utt, (uint64_t)frame, (uint64_t)sp.step + 1);
     }
     return sp.temperature <= 0.0f ? sel_argmax(v, V, vpt, S) : sel_sample(v, V, vpt, sp.temperature, sp.top_k, u, keep, S);
+}
+
+// the token of slot s (uniform over the workgroup), or -1 if the slot is done; no side effects
+// select_token on a row already loaded into the owner registers (sel_load): lets a kernel issue the logits loads
+// ahead of its weight stream
+// MODE: SEL_CB0 / SEL_CP at compile time, or SEL_NONE to dispatch on sp.mode
+template <int MODE = SEL_NONE>
+__device__ __forceinline__ int select_token_regs(const SelectSpec &sp, float (&v)[SEL_VPT_MAX], int s, SelLds &S) {
+    if constexpr (MODE == SEL_NONE) {
+        return sp.mode == SEL_CB0 ? select_token_regs<SEL_CB0>(sp, v, s, S) : select_token_regs<SEL_CP>(sp, v, s, S);
+    } else {
+        SelPre q;
+        sel_prefetch<MODE>(sp, s, q);
+        return select_token_pre<MODE>(sp, q, v, S);
+    }
 }
 
 // agent-scope (sc1) loads of a row published in this launch, exact widths: unconditional, all issued first

@@ -9,7 +9,7 @@ import numpy as np
 R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(R, "qwen3-tts-jetson_amd"), os.path.join(R, "tests")]
 os.environ["Q3T_PERSIST_PROF"] = "1"
-os.environ["Q3T_DEV_LIB"] = "1"   # needs the development build: make -C qwen3-tts-jetson_amd/csrc DEV=1
+os.environ.setdefault("Q3T_DEV_LIB", "1")   # needs the development build: make -C qwen3-tts-jetson_amd/csrc DEV=1
 import q3t  # noqa: E402
 from q3t_testutil import synth_dir  # noqa: E402
 
@@ -34,6 +34,8 @@ for k in range(5):
                 continue
             ph = ps * PPH + 5 * l + k
             prod = ph - 1
+            if k == 2 and not (T[:, prod, 2] >= 0).any():
+                prod = ph - 2   # fused code-predictor attention: C waits on A's QKV rows (no phase B)
             st, arr, pub = T[:, ph, 0], T[:, ph, 1], T[:, ph, 2]
             ok = (arr >= 0) & (pub >= 0)
             if not ok.any() or not (T[:, prod, 2] >= 0).any():
