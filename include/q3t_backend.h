@@ -48,6 +48,9 @@ typedef struct q3t_config {
     int32_t hidden, n_layers, n_heads, n_kv_heads, head_dim, intermediate;
     int32_t codec_vocab, n_codebooks, text_vocab, text_dim, cp_layers, cp_vocab;
     int32_t codec_eos, has_vocoder, sample_rate, max_slots, max_ctx;
+    /* code predictor geometry (tts_transformer.cpp:370-389): equal to the talker's for 0.6B; 1.7B projects every
+     * code-predictor input with code_pred.mtp_proj (has_mtp = 1) */
+    int32_t cp_hidden, cp_intermediate, cp_heads, cp_kv_heads, has_mtp;
 } q3t_config;
 
 /* tts_params (src/qwen3_tts.h:18-43) + generate() arguments; top_p / n_threads are unused by the reference */

@@ -260,6 +260,9 @@ struct q3o_model {
     mat16 text_embd, fc1, fc2, codec_embd, codec_head;
     const float *fc1_b, *fc2_b, *out_norm, *cp_out_norm;
     layer_t *L, *CP;
+    q3o_config cpc;          /* the code predictor's layer geometry (hidden / inter / heads of the CP) */
+    mat16 mtp;               /* 1.7B: code_pred.mtp_proj [cp_hidden][hidden] (+ bias, optional) */
+    const float *mtp_b;
     mat16 cp_embd[15], cp_head[15];
     /* vocoder */
     const uint16_t *cb_first, *cb_rest[15];
@@ -489,6 +492,12 @@ static void parse_config(const gguf_t *g, q3o_config *c) {
     c->n_codebooks = kv_u32(g, K("qwen3-tts.talker.num_codebooks", "qwen3-tts.num_code_groups"), 16);
     c->cp_layers = kv_u32(g, K("qwen3-tts.code_pred.layer_count", "qwen3-tts.code_predictor.layer_count"), 5);
     c->cp_vocab = kv_u32(g, K("qwen3-tts.code_pred.vocab_size", "qwen3-tts.code_predictor.vocab_size"), 2048);
+    /* code predictor architecture, falling back to the talker's values (0.6B): tts_transformer.cpp:370-389 */
+    c->cp_hidden = kv_u32(g, K("qwen3-tts.code_predictor.embedding_length"), c->hidden);
+    c->cp_inter = kv_u32(g, K("qwen3-tts.code_predictor.feed_forward_length"), c->inter);
+    c->cp_heads = kv_u32(g, K("qwen3-tts.code_predictor.attention.head_count"), c->n_heads);
+    c->cp_kv = kv_u32(g, K("qwen3-tts.code_predictor.attention.head_count_kv"), c->n_kv);
+    c->cp_head_dim = kv_u32(g, K("qwen3-tts.code_predictor.attention.key_length"), c->head_dim);
     c->codec_pad = kv_u32(g, K("qwen3-tts.codec.pad_id"), 2148);
     c->codec_bos = kv_u32(g, K("qwen3-tts.codec.bos_id"), 2149);
     c->codec_eos = kv_u32(g, K("qwen3-tts.codec.eos_id", "qwen3-tts.codec.eos_token_id"), 2150);
@@ -750,19 +759,31 @@ q3o_model *q3o_load(const char *tts_gguf, const char *tok_gguf, int ggml_roundin
              (m->fc1_b = get_vec(g, "talker.text_proj.fc1.bias", c->text_dim)) &&
              (m->fc2_b = get_vec(g, "talker.text_proj.fc2.bias", H)) &&
              (m->out_norm = get_vec(g, "talker.output_norm.weight", H)) &&
-             (m->cp_out_norm = get_vec(g, "code_pred.output_norm.weight", H));
+             (m->cp_out_norm = get_vec(g, "code_pred.output_norm.weight", c->cp_hidden));
     if (!ok) { q3o_free(m); return NULL; }
-    if (gfind(g, "code_pred.mtp_proj.weight")) { snprintf(g_err, sizeof g_err, "mtp_proj (1.7B) not supported by the oracle"); q3o_free(m); return NULL; }
+    m->cpc = *c;
+    m->cpc.hidden = c->cp_hidden; m->cpc.inter = c->cp_inter; m->cpc.n_heads = c->cp_heads;
+    m->cpc.n_kv = c->cp_kv; m->cpc.head_dim = c->cp_head_dim;
+    /* code_pred.mtp_proj (1.7B, tts_transformer.cpp:611-616, 709-712): applied to every code-predictor input */
+    c->has_mtp = gfind(g, "code_pred.mtp_proj.weight") != NULL;
+    if (c->has_mtp) {
+        if (!get_mat(g, "code_pred.mtp_proj.weight", c->cp_hidden, H, &m->mtp)) { q3o_free(m); return NULL; }
+        m->mtp_b = gfind(g, "code_pred.mtp_proj.bias") ? get_vec(g, "code_pred.mtp_proj.bias", c->cp_hidden) : NULL;
+        if (gfind(g, "code_pred.mtp_proj.bias") && !m->mtp_b) { q3o_free(m); return NULL; }
+    } else if (c->cp_hidden != H) {
+        snprintf(g_err, sizeof g_err, "code predictor hidden %d != talker hidden %d without code_pred.mtp_proj", c->cp_hidden, H);
+        q3o_free(m); return NULL;
+    }
     m->L = calloc((size_t)c->n_layers, sizeof(layer_t));
     m->CP = calloc((size_t)c->cp_layers, sizeof(layer_t));
     for (int i = 0; i < c->n_layers; ++i) if (!load_layer(g, "talker", i, c, &m->L[i])) { q3o_free(m); return NULL; }
-    for (int i = 0; i < c->cp_layers; ++i) if (!load_layer(g, "code_pred", i, c, &m->CP[i])) { q3o_free(m); return NULL; }
+    for (int i = 0; i < c->cp_layers; ++i) if (!load_layer(g, "code_pred", i, &m->cpc, &m->CP[i])) { q3o_free(m); return NULL; }
     for (int i = 0; i < c->n_codebooks - 1 && i < 15; ++i) {
         char b[96];
         snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
         if (!get_mat(g, b, c->cp_vocab, H, &m->cp_embd[i])) { q3o_free(m); return NULL; }
         snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
-        if (!get_mat(g, b, c->cp_vocab, H, &m->cp_head[i])) { q3o_free(m); return NULL; }
+        if (!get_mat(g, b, c->cp_vocab, c->cp_hidden, &m->cp_head[i])) { q3o_free(m); return NULL; }
     }
     if (tok_gguf && tok_gguf[0]) {
         m->gk = gguf_open(tok_gguf);
@@ -893,8 +914,9 @@ struct q3o_kv { int n_layers, n_ctx, n_kv, D; float *k, *v; };   /* [layer][pos]
 
 q3o_kv *q3o_kv_new(const q3o_model *m, int n_ctx, int which) {
     q3o_kv *kv = calloc(1, sizeof *kv);
+    const q3o_config *c = which == 0 ? &m->c : &m->cpc;
     kv->n_layers = which == 0 ? m->c.n_layers : m->c.cp_layers;
-    kv->n_ctx = n_ctx; kv->n_kv = m->c.n_kv; kv->D = m->c.head_dim;
+    kv->n_ctx = n_ctx; kv->n_kv = c->n_kv; kv->D = c->head_dim;
     const size_t n = (size_t)kv->n_layers * n_ctx * kv->n_kv * kv->D;
     kv->k = calloc(n, sizeof(float)); kv->v = calloc(n, sizeof(float));
     return kv;
@@ -904,7 +926,8 @@ void q3o_kv_free(q3o_kv *kv) { if (kv) { free(kv->k); free(kv->v); free(kv); } }
 /* ------------------------------------------------------------------ one Qwen3 decoder layer, one token
  * tts_transformer.cpp:1410-1494 (talker step) == :1721-1811 (CP step).  Attention of the step graph is
  * ggml_flash_attn_ext (Q->f16, K/V f16 from the cache, f32 online softmax); restated with f32 accumulation. */
-static void decoder_layer_block(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos0, int T);
+static void decoder_layer_block(const q3o_model *m, const q3o_config *c, const layer_t *l, q3o_kv *kv, int il, float *x,
+                                int pos0, int T);
 
 /* f32 dot product, 4 x 8-lane accumulators combined in a fixed order (n % 8 == 0 lanes vectorised, tail scalar) */
 static inline float dot_f32(const float *a, const float *b, int n) {
@@ -932,8 +955,8 @@ static inline float dot_f32(const float *a, const float *b, int n) {
 
 /* ggml_flash_attn_ext of one token (q [nH][D], at position pos) over the cached rows 0..pos of layer il: f16-rounded
  * Q, f32 scores and online-softmax sums (double), f32 V accumulation -> att [nH][D].  `par`: heads in parallel. */
-static void attend(const q3o_model *m, const q3o_kv *kv, int il, const float *q, int pos, float *att, int par) {
-    const q3o_config *c = &m->c;
+static void attend(const q3o_model *m, const q3o_config *c, const q3o_kv *kv, int il, const float *q, int pos, float *att,
+                   int par) {
     const int D = c->head_dim, nH = c->n_heads, nKV = c->n_kv, rep = nH / nKV;
     const float *kc = kv->k + (size_t)il * kv->n_ctx * nKV * D, *vc = kv->v + (size_t)il * kv->n_ctx * nKV * D;
     const float scale = 1.0f / sqrtf((float)D);
@@ -964,9 +987,8 @@ static void attend(const q3o_model *m, const q3o_kv *kv, int il, const float *q,
 }
 
 /* head RMSNorms + NEOX RoPE of one token's raw q/k, then its K/V rows written to the cache (ggml_cpy -> F16) */
-static void qk_norm_rope_store(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *q, float *k,
-                               const float *v, int pos) {
-    const q3o_config *c = &m->c;
+static void qk_norm_rope_store(const q3o_model *m, const q3o_config *c, const layer_t *l, q3o_kv *kv, int il, float *q,
+                               float *k, const float *v, int pos) {
     const int D = c->head_dim, nH = c->n_heads, nKV = c->n_kv;
     float cache[512];
     q3o_rope_cache((float)pos, D, c->rope_theta, cache);
@@ -982,15 +1004,15 @@ static void qk_norm_rope_store(const q3o_model *m, const layer_t *l, q3o_kv *kv,
 /* ------------------------------------------------------------------ one Qwen3 decoder layer, one token
  * tts_transformer.cpp:1410-1494 (talker step) == :1721-1811 (CP step).  Attention of the step graph is
  * ggml_flash_attn_ext (Q->f16, K/V f16 from the cache, f32 online softmax); restated with f32 accumulation. */
-static void decoder_layer(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos) {
-    decoder_layer_block(m, l, kv, il, x, pos, 1);
+static void decoder_layer(const q3o_model *m, const q3o_config *c, const layer_t *l, q3o_kv *kv, int il, float *x, int pos) {
+    decoder_layer_block(m, c, l, kv, il, x, pos, 1);
 }
 
 /* the same layer over T consecutive tokens at positions pos0..pos0+T-1 (x [T][H] in place): every weight row is read
  * once per block and reused by the T tokens, each token computed exactly as decoder_layer computes it alone (the
  * teacher-forced replay of q3o_generate_forced_from uses it for the frames it does not trace) */
-static void decoder_layer_block(const q3o_model *m, const layer_t *l, q3o_kv *kv, int il, float *x, int pos0, int T) {
-    const q3o_config *c = &m->c;
+static void decoder_layer_block(const q3o_model *m, const q3o_config *c, const layer_t *l, q3o_kv *kv, int il, float *x,
+                                int pos0, int T) {
     const int H = c->hidden, D = c->head_dim, nH = c->n_heads, nKV = c->n_kv, I = c->inter;
     float *xn = malloc(sizeof(float) * (size_t)T * (H > I ? H : I));
     float *q = malloc(sizeof(float) * (size_t)T * nH * D), *k = malloc(sizeof(float) * (size_t)T * nKV * D);
@@ -1002,12 +1024,12 @@ static void decoder_layer_block(const q3o_model *m, const layer_t *l, q3o_kv *kv
     mul_mat_rows(m, &l->k, xn, T, k);
     mul_mat_rows(m, &l->v, xn, T, v);
     for (int t = 0; t < T; ++t)
-        qk_norm_rope_store(m, l, kv, il, q + (size_t)t * nH * D, k + (size_t)t * nKV * D, v + (size_t)t * nKV * D, pos0 + t);
+        qk_norm_rope_store(m, c, l, kv, il, q + (size_t)t * nH * D, k + (size_t)t * nKV * D, v + (size_t)t * nKV * D, pos0 + t);
     if (T == 1) {
-        attend(m, kv, il, q, pos0, att, 1);
+        attend(m, c, kv, il, q, pos0, att, 1);
     } else {
 #pragma omp parallel for schedule(dynamic)
-        for (int t = 0; t < T; ++t) attend(m, kv, il, q + (size_t)t * nH * D, pos0 + t, att + (size_t)t * nH * D, 0);
+        for (int t = 0; t < T; ++t) attend(m, c, kv, il, q + (size_t)t * nH * D, pos0 + t, att + (size_t)t * nH * D, 0);
     }
     mul_mat_rows(m, &l->o, att, T, y);
     for (size_t i = 0; i < (size_t)T * H; ++i) x[i] += y[i];
@@ -1026,7 +1048,7 @@ int q3o_talker_step_n(const q3o_model *m, q3o_kv *kv, const float *embd, int pos
     if (n_layers <= 0 || n_layers > c->n_layers) n_layers = c->n_layers;
     float *x = malloc(sizeof(float) * (size_t)c->hidden);
     memcpy(x, embd, sizeof(float) * (size_t)c->hidden);
-    for (int il = 0; il < n_layers; ++il) decoder_layer(m, &m->L[il], kv, il, x, pos);
+    for (int il = 0; il < n_layers; ++il) decoder_layer(m, c, &m->L[il], kv, il, x, pos);
     rms_norm_w(x, m->out_norm, hidden, c->hidden, c->eps);                  /* :1498-1499 */
     if (logits) mul_mat_vec(m, &m->codec_head, hidden, logits);             /* :1503 */
     free(x);
@@ -1103,11 +1125,18 @@ int q3o_prefill_embd(const q3o_model *m, const int32_t *toks, int n, const float
 }
 
 /* ------------------------------------------------------------------ code predictor */
+/* xin: the pass input in talker space [hidden]; with code_pred.mtp_proj (1.7B) it is projected first,
+ * x = mtp_proj . f16(xin) + bias (ggml_mul_mat + ggml_add, tts_transformer.cpp:1554-1560 / :1709-1714) */
 int q3o_cp_pass(const q3o_model *m, q3o_kv *kv, const float *xin, int pos, int head, float *hidden_out, float *logits) {
-    const q3o_config *c = &m->c;
+    const q3o_config *c = &m->cpc;
     float *x = malloc(sizeof(float) * (size_t)c->hidden), *hn = malloc(sizeof(float) * (size_t)c->hidden);
-    memcpy(x, xin, sizeof(float) * (size_t)c->hidden);
-    for (int il = 0; il < c->cp_layers; ++il) decoder_layer(m, &m->CP[il], kv, il, x, pos);
+    if (m->c.has_mtp) {
+        mul_mat_vec(m, &m->mtp, xin, x);
+        if (m->mtp_b) for (int i = 0; i < c->hidden; ++i) x[i] += m->mtp_b[i];
+    } else {
+        memcpy(x, xin, sizeof(float) * (size_t)c->hidden);
+    }
+    for (int il = 0; il < c->cp_layers; ++il) decoder_layer(m, c, &m->CP[il], kv, il, x, pos);
     rms_norm_w(x, m->cp_out_norm, hn, c->hidden, c->eps);                  /* :1815-1816 */
     if (hidden_out) memcpy(hidden_out, hn, sizeof(float) * (size_t)c->hidden);
     if (head >= 0 && logits) mul_mat_vec(m, &m->cp_head[head], hn, logits); /* :1818 */
@@ -1320,7 +1349,7 @@ static int generate_impl(const q3o_model *m, const int32_t *toks, int n, const f
                 const float *tr = f < tlen ? trailing + (size_t)f * H : pad;
                 for (int h = 0; h < H; ++h) xt[h] += tr[h];
             }
-            for (int il = 0; il < c->n_layers; ++il) decoder_layer_block(m, &m->L[il], kv, il, X, n_past, T);
+            for (int il = 0; il < c->n_layers; ++il) decoder_layer_block(m, c, &m->L[il], kv, il, X, n_past, T);
             n_past += T;
             if (f0 + T == F0) {   /* :1496-1505 on the last token */
                 rms_norm_w(X + (size_t)(T - 1) * H, m->out_norm, hidden, H, c->eps);

@@ -30,6 +30,9 @@ typedef struct {
     int codec_pad, codec_bos, codec_eos, tts_bos, tts_eos, tts_pad, think, nothink, think_bos, think_eos;
     int has_vocoder, cb_dim, cb_size, voc_hidden, voc_latent, voc_heads, voc_layers, voc_ffn, dec_dim, up_k;
     int conv_t_k[4], rates[4];
+    /* code predictor geometry (1.7B: cp_hidden != hidden, code_pred.mtp_proj projects talker-space inputs;
+     * tts_transformer.cpp:370-389, 611-616, 1554-1560, 1709-1714); the 0.6B defaults are the talker's values */
+    int cp_hidden, cp_inter, cp_heads, cp_kv, cp_head_dim, has_mtp;
 } q3o_config;
 
 typedef struct q3o_model q3o_model;

@@ -152,6 +152,8 @@ int q3t_get_config(const q3t_ctx *ctx, q3t_config *o) {
     o->sample_rate = 24000;
     o->max_slots = ctx->engine.max_slots();
     o->max_ctx = ctx->engine.max_ctx();
+    o->cp_hidden = c.cp_hidden; o->cp_intermediate = c.cp_inter; o->cp_heads = c.cp_heads; o->cp_kv_heads = c.cp_kv;
+    o->has_mtp = c.has_mtp ? 1 : 0;
     return Q3T_OK;
 }
 

@@ -177,14 +177,27 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     c_.nothink = (int)g.get_int({"qwen3-tts.codec.nothink_id", "qwen3-tts.codec_nothink_id"}, 2155);
     c_.think_bos = (int)g.get_int({"qwen3-tts.codec.think_bos_id", "qwen3-tts.codec_think_bos_id"}, 2156);
     c_.think_eos = (int)g.get_int({"qwen3-tts.codec.think_eos_id", "qwen3-tts.codec_think_eos_id"}, 2157);
-    const int cp_hidden = (int)g.get_int({"qwen3-tts.code_predictor.embedding_length"}, c_.hidden);
-    if (cp_hidden != c_.hidden || g.find("code_pred.mtp_proj.weight")) {
-        set_error("code predictor hidden != talker hidden (1.7B mtp_proj) is not supported");
+    // code predictor architecture (falls back to the talker's values: 0.6B), tts_transformer.cpp:370-389
+    c_.cp_hidden = (int)g.get_int({"qwen3-tts.code_predictor.embedding_length"}, c_.hidden);
+    c_.cp_inter = (int)g.get_int({"qwen3-tts.code_predictor.feed_forward_length"}, c_.inter);
+    c_.cp_heads = (int)g.get_int({"qwen3-tts.code_predictor.attention.head_count"}, c_.n_heads);
+    c_.cp_kv = (int)g.get_int({"qwen3-tts.code_predictor.attention.head_count_kv"}, c_.n_kv);
+    const int cp_head_dim = (int)g.get_int({"qwen3-tts.code_predictor.attention.key_length"}, c_.head_dim);
+    c_.has_mtp = g.find("code_pred.mtp_proj.weight") != nullptr;
+    if (c_.cp_hidden != c_.hidden && !c_.has_mtp) {
+        set_error("code predictor hidden != talker hidden without code_pred.mtp_proj");
         return false;
     }
+    if (cp_head_dim != c_.head_dim) { set_error("code predictor head_dim must equal the talker's (shared RoPE table)"); return false; }
+    cpc_ = c_;
+    cpc_.hidden = c_.cp_hidden; cpc_.inter = c_.cp_inter; cpc_.n_heads = c_.cp_heads; cpc_.n_kv = c_.cp_kv;
+    // the batched matrix-core stack (hoisted norms, k_resid_norm) is built for widths <= 1024 and the 0.6B layout;
+    // other models (1.7B) run every projection on the vector kernels with a 1-slot K split at any batch size
+    mm_ok_ = !c_.has_mtp && c_.hidden <= 1024 && c_.cp_hidden <= 1024;
+    fam1_ = mm_ok_ ? 0 : 1;
     if (c_.n_codebooks != 16) { set_error("n_codebooks must be 16"); return false; }
     // the fused code-predictor attention prologue is specialised to the 0.6B head layout (16 q / 8 kv heads x 128)
-    cp_fused_attn_ = cp_fused_attn_ && c_.n_heads == 16 && c_.n_kv == 8 && c_.head_dim == 128;
+    cp_fused_attn_ = cp_fused_attn_ && c_.cp_heads == 16 && c_.cp_kv == 8 && c_.head_dim == 128 && c_.cp_hidden == 1024;
     if (!upload_weights(g)) return false;
     if (!alloc_state()) return false;
 #ifdef Q3T_DEV
@@ -229,8 +242,7 @@ std::vector<WeightArena *> Engine::weight_arenas() {
 }
 
 bool Engine::upload_weights(const Gguf &g) {
-    const int H = c_.hidden, D = c_.head_dim, Dq = c_.n_heads * D, Dkv = c_.n_kv * D, I = c_.inter;
-    if (I % 16 != 0 || H % 8 != 0) { set_error("unsupported hidden/intermediate size"); return false; }
+    const int H = c_.hidden, D = c_.head_dim;
     // every weight goes into the arena (one blob: the unit of the RCCL broadcast); receiving ranks touch only the
     // GGUF headers, never the tensor bytes
     size_t total = 0;
@@ -257,7 +269,9 @@ bool Engine::upload_weights(const Gguf &g) {
         if (!recv) std::memcpy(dst.data() + at, t->data, t->nbytes());
         return true;
     };
-    auto layer = [&](const char *pfx, int i, DevLayer &l) -> bool {
+    auto layer = [&](const char *pfx, int i, DevLayer &l, const Config &lc) -> bool {
+        const int H = lc.hidden, Dq = lc.n_heads * D, Dkv = lc.n_kv * D, I = lc.inter;
+        if (I % 16 != 0 || H % 8 != 0) { set_error("unsupported hidden/intermediate size"); return false; }
         char b[160];
         auto nm = [&](const char *s) { snprintf(b, sizeof b, "%s.blk.%d.%s", pfx, i, s); return std::string(b); };
         // fused [Wq; Wk; Wv] rows
@@ -287,8 +301,12 @@ bool Engine::upload_weights(const Gguf &g) {
     };
     L_.resize(c_.n_layers);
     CP_.resize(c_.cp_layers);
-    for (int i = 0; i < c_.n_layers; ++i) if (!layer("talker", i, L_[i])) return false;
-    for (int i = 0; i < c_.cp_layers; ++i) if (!layer("code_pred", i, CP_[i])) return false;
+    for (int i = 0; i < c_.n_layers; ++i) if (!layer("talker", i, L_[i], c_)) return false;
+    for (int i = 0; i < c_.cp_layers; ++i) if (!layer("code_pred", i, CP_[i], cpc_)) return false;
+    if (c_.has_mtp) {   // code_pred.mtp_proj (1.7B): tts_transformer.cpp:611-616, 709-712
+        if (!(mtp_ = up16("code_pred.mtp_proj.weight", H, c_.cp_hidden))) return false;
+        if (g.find("code_pred.mtp_proj.bias") && !(mtp_b_ = up32("code_pred.mtp_proj.bias", c_.cp_hidden))) return false;
+    }
     if (!(text_embd_ = up16("talker.text_embd.weight", c_.text_dim, c_.text_vocab))) return false;
     if (!(fc1_ = up16("talker.text_proj.fc1.weight", c_.text_dim, c_.text_dim))) return false;
     if (!(fc2_ = up16("talker.text_proj.fc2.weight", c_.text_dim, H))) return false;
@@ -297,7 +315,7 @@ bool Engine::upload_weights(const Gguf &g) {
     if (!(codec_embd_ = up16("talker.codec_embd.weight", H, c_.codec_vocab))) return false;
     if (!(codec_head_ = up16("talker.codec_head.weight", H, c_.codec_vocab))) return false;
     if (!(out_norm_ = up32("talker.output_norm.weight", H))) return false;
-    if (!(cp_out_norm_ = up32("code_pred.output_norm.weight", H))) return false;
+    if (!(cp_out_norm_ = up32("code_pred.output_norm.weight", c_.cp_hidden))) return false;
     cp_embd_.resize(15);
     cp_head_.resize(15);
     for (int i = 0; i < 15; ++i) {
@@ -305,7 +323,7 @@ bool Engine::upload_weights(const Gguf &g) {
         snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
         if (!(cp_embd_[i] = up16(b, H, c_.cp_vocab))) return false;
         snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
-        if (!(cp_head_[i] = up16(b, H, c_.cp_vocab))) return false;
+        if (!(cp_head_[i] = up16(b, c_.cp_hidden, c_.cp_vocab))) return false;
     }
     // speaker encoder (ECAPA-TDNN, audio_tokenizer_encoder.cpp): optional, the GGUF's spk_enc.* tensors
     if (g.find("spk_enc.conv0.weight")) {
@@ -337,27 +355,27 @@ bool Engine::upload_weights(const Gguf &g) {
 
 bool Engine::alloc_state() {
     const int S = max_slots_, H = c_.hidden, D = c_.head_dim;
-    const int QKV = (c_.n_heads + 2 * c_.n_kv) * D;
+    const int QKV = std::max(c_.n_heads + 2 * c_.n_kv, c_.cp_heads + 2 * c_.cp_kv) * D;   // talker / code predictor
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
     max_trailing_ = 512;
     x_ = dalloc<float>((size_t)S * H);
     qkv_ = dalloc<float>((size_t)S * QKV);
     logits_ = dalloc<float>((size_t)S * c_.codec_vocab);
     hidden_ = dalloc<float>((size_t)S * H);
-    cpx_ = dalloc<float>((size_t)S * H);
+    cpx_ = dalloc<float>((size_t)S * c_.cp_hidden);
     cp_in1_ = dalloc<float>((size_t)S * H);
     cp_logits_ = dalloc<float>((size_t)S * c_.cp_vocab);
     part_ = dalloc<float>((size_t)S * c_.n_heads * max_splits * (D + 2));
     ticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
     sel_ticket_ = dalloc<unsigned>((size_t)S);
-    attn_ = dalloc<uint16_t>((size_t)S * c_.n_heads * D);
-    hmlp_ = dalloc<uint16_t>((size_t)S * c_.inter);
+    attn_ = dalloc<uint16_t>((size_t)S * std::max(c_.n_heads, c_.cp_heads) * D);
+    hmlp_ = dalloc<uint16_t>((size_t)S * std::max(c_.inter, c_.cp_inter));
     xn_ = dalloc<uint16_t>((size_t)S * H);
     parts_ = dalloc<float>((size_t)4 * S * H);
     const size_t kv_layer = (size_t)S * c_.n_kv * max_ctx_ * D;
     kc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
     vc_ = dalloc<uint16_t>(kv_layer * c_.n_layers);
-    const size_t cpkv_layer = (size_t)S * c_.n_kv * 16 * D;
+    const size_t cpkv_layer = (size_t)S * c_.cp_kv * 16 * D;
     cpkc_ = dalloc<uint16_t>(cpkv_layer * c_.cp_layers);
     cpvc_ = dalloc<uint16_t>(cpkv_layer * c_.cp_layers);
     pos_ = dalloc<int>(S);
@@ -404,7 +422,8 @@ bool Engine::setup_persist() {
     Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
     persist_ = persist_ && fused_select_ &&
                persist_supported(c_.hidden, c_.n_heads, c_.n_kv, c_.head_dim, c_.inter, c_.codec_vocab, max_ctx_, n_cu);
-    const bool cp_ok = opt_.persist_cp && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15;
+    const bool cp_ok = opt_.persist_cp && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15 &&
+                       !c_.has_mtp && c_.cp_hidden == 1024 && c_.cp_inter == 3072 && c_.cp_heads == 16 && c_.cp_kv == 8;
     // every instantiation must fit one workgroup per CU on this device (occupancy query with its LDS request)
     persist_ = persist_ && persist_resident(device_, max_ctx_, cp_ok);
     if (!persist_) return true;
@@ -442,7 +461,7 @@ bool Engine::setup_persist() {
 // phase A reproduces bit for bit.  The persistent frame then reads the row instead of running layer 0's norm + QKV
 // phase and its all-to-all edge (persist.hip).  520 MB of f32.
 bool Engine::build_cp_qkv_table() {
-    const int H = c_.hidden, QKV = (c_.n_heads + 2 * c_.n_kv) * c_.head_dim;
+    const int H = cpc_.hidden, QKV = (cpc_.n_heads + 2 * cpc_.n_kv) * cpc_.head_dim;
     if (c_.codec_vocab != 3072 || c_.cp_vocab != 2048 || (int)cp_embd_.size() < 14) return true;   // shapes persist.hip supports
     const size_t rows = persist_qkv_table_rows();
     cp_qkvtab_ = dalloc<float>(rows * QKV);
@@ -667,7 +686,9 @@ static bool decoder_stack(const Config &c, const std::vector<DevLayer> &layers, 
         g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
         g.pro = PRO_RMS; g.x = x; g.ldx = H; g.nw = l.attn_norm; g.eps = c.eps;
         if (il == 0 && in0) {
-            if (mm && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
+            // the gather as its own launch: batched path (no gather prologue in the GEMM), or rows wider than the
+            // GEMV's gather prologue (K > 1024: the 1.7B talker) -- the same summation order either way
+            if ((mm || H > 1024) && (in0->pro == PRO_RMS_G1 || in0->pro == PRO_RMS_G16)) {
                 if (!gather_sum(in0->gs, in0->pro == PRO_RMS_G16 ? 16 : 1, S, H, x, H, s)) return false;
             } else {
                 g.pro = in0->pro; g.x = in0->x; g.gs = in0->gs; g.raw_out = x;
@@ -759,20 +780,20 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         in0.gs.tr_ld = max_trailing_ * H; in0.gs.pad = tts_pad_;
         in0.prenormed = prenormed;
     }
-    const bool mm = S >= gemm_mfma_min_batch();   // batched: one selection workgroup per slot after the head
+    const bool mm = use_mm(S);   // batched: one selection workgroup per slot after the head
     if (mm) {
         if (!decoder_stack_mm(c_, opt_.attn_split, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
                               rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_, policy_slots_))
             return false;
     } else if (!decoder_stack(c_, L_, S, x_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_, rope_, part_,
-                              ticket_, s, gather_input ? &in0 : nullptr)) {
+                              ticket_, s, gather_input ? &in0 : nullptr, false, nullptr, fam1_)) {
         return false;
     }
     // final RMSNorm (hidden_states, side output) + codec_head -> logits  (:1496-1505); batched: the stack's last
     // resid_norm already normalised x into xn (and wrote hidden_)
     GemvParams h;
     h.W = codec_head_; h.N = c_.codec_vocab; h.K = H; h.B = S;
-    h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_;
+    h.pro = PRO_RMS; h.x = x_; h.ldx = H; h.nw = out_norm_; h.eps = c_.eps; h.side_out = hidden_; h.family_b = fam1_;
     if (mm) { h.pro = PRO_F16; h.x = xn_; h.nw = nullptr; h.side_out = nullptr; }
     h.out_f32 = logits_; h.ldo = c_.codec_vocab;
     if (select_next && !mm) h.sel = select_spec(SEL_CB0, gp_, 1, 0);
@@ -785,9 +806,18 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
 // Pass inputs are assembled by layer 0's QKV prologue: pass 0 the talker hidden state, pass 1 codec_embd[code 0],
 // pass p >= 2 code_pred.codec_embd[p-2][code p-1]; the raw row lands in cpx_ (the pass's residual stream).
 // logits_host (tests only, never captured): every head's logits copied out after its GEMV.
+bool Engine::cp_project(int S, const float *x_talker, int ldx, hipStream_t s) {
+    GemvParams g;   // ggml_mul_mat(mtp_proj, cur) + ggml_add(bias): f16-rounded input, f32 accumulation
+    g.W = mtp_; g.N = c_.cp_hidden; g.K = c_.hidden; g.B = S;
+    g.pro = PRO_F32; g.x = x_talker; g.ldx = ldx;
+    g.bias = mtp_b_;
+    g.out_f32 = cpx_; g.ldo = c_.cp_hidden; g.family_b = fam1_;
+    return gemv(g, s);
+}
+
 bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool talker_next) {
-    const int H = c_.hidden;
-    const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * 16 * c_.head_dim;
+    const int H = cpc_.hidden;   // code-predictor width (the talker's for 0.6B)
+    const size_t kv_layer = (size_t)max_slots_ * cpc_.n_kv * 16 * cpc_.head_dim;
     std::vector<float> lg;
     // vector path with fused selection: heads 0..13 only produce logits; the next pass's QKV launch selects the token
     // in every workgroup while its weights stream (PRO_SEL_G1), so the head's 256 -> 1 arrival chain and the serial
@@ -805,14 +835,28 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         p.prof = pprof_;
         return persist_cp_frame(p, s);
     }
-    const bool fsel_all = fused_select_ && S < gemm_mfma_min_batch();
-    const bool defer = fsel_all && defer_cp_select_;
+    const bool fsel_all = fused_select_ && !use_mm(S);
+    // deferred selection gathers the next pass's table row inside its QKV launch: not with a projected input (1.7B)
+    const bool defer = fsel_all && defer_cp_select_ && !c_.has_mtp;
     bool next_prenormed = false;   // batched: this pass's input was prepared by the previous selection launch
     for (int p = 0; p < 16; ++p) {
         StackInput in0;
         in0.prenormed = next_prenormed;
         next_prenormed = false;
-        if (p == 0) {
+        if (c_.has_mtp) {
+            // 1.7B: the pass input (talker hidden / table row, talker space) projected into cpx_ by code_pred.mtp_proj
+            // (tts_transformer.cpp:1554-1560, :1709-1714); layer 0 then normalises cpx_ like any later layer
+            const float *src = hidden_;
+            if (p > 0) {
+                GatherSum gs;
+                gs.tok = tokens_; gs.tok_ld = 16; gs.tok_col0 = p - 1;
+                gs.tab0 = p == 1 ? codec_embd_ : cp_embd_[p - 2];
+                if (!gather_sum(gs, 1, S, c_.hidden, cp_in1_, c_.hidden, s)) return false;
+                src = cp_in1_;
+            }
+            if (!cp_project(S, src, c_.hidden, s)) return false;
+            in0.pro = PRO_RMS; in0.x = cpx_;
+        } else if (p == 0) {
             in0.pro = PRO_RMS; in0.x = hidden_;
         } else {
             in0.pro = PRO_RMS_G1;
@@ -824,21 +868,22 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
                 in0.sel_logits = cp_logits_;
             }
         }
-        const bool mm = S >= gemm_mfma_min_batch();
+        const bool mm = use_mm(S);
         if (mm) {
-            if (!decoder_stack_mm(c_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
+            if (!decoder_stack_mm(cpc_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
                                   p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_, true))
                 return false;
-        } else if (!decoder_stack(c_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
-                                  cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0, cp_fused_attn_)) {
+        } else if (!decoder_stack(cpc_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
+                                  cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, c_.has_mtp ? nullptr : &in0,
+                                  cp_fused_attn_, nullptr, fam1_)) {
             return false;
         }
         if (p == 0) continue;
         const int step = p - 1;
         GemvParams h;
         h.W = cp_head_[step]; h.N = c_.cp_vocab; h.K = H; h.B = S;
-        h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps;
+        h.pro = PRO_RMS; h.x = cpx_; h.ldx = H; h.nw = cp_out_norm_; h.eps = c_.eps; h.family_b = fam1_;
         if (mm) { h.pro = PRO_F16; h.x = xn_; h.nw = nullptr; }
         h.out_f32 = cp_logits_; h.ldo = c_.cp_vocab;
         const bool fsel = fsel_all && (!defer || step == 14);
@@ -868,7 +913,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
                 en.gs.frame = frame_; en.gs.tr_ld = max_trailing_ * H; en.gs.pad = tts_pad_;
                 en.x = x_; en.nw = L_[0].attn_norm;
             }
-            en.xn = xn_; en.eps = c_.eps; en.H = H;
+            en.xn = xn_; en.eps = c_.eps; en.H = c_.hidden;   // (mm: no projection, code predictor width == talker's)
             if (!select_embed_norm(select_spec(SEL_CP, gp_, 0, step), cp_logits_, en, S, s)) return false;
             next_prenormed = true;
             continue;
@@ -886,7 +931,7 @@ bool Engine::enqueue_frame(int S, hipStream_t s) {
 #ifdef Q3T_NO_SELFUSE
     const bool mm = false;
 #else
-    const bool mm = S >= gemm_mfma_min_batch();
+    const bool mm = use_mm(S);
 #endif
     if (!enqueue_cp_frame(S, s, nullptr, mm)) return false;
     if (!enqueue_talker(S, s, true, fused_select_, mm)) return false;
@@ -957,7 +1002,7 @@ bool Engine::enqueue_prefill_rows(int key, hipStream_t s) {
     pf.slot = pf_slot_; pf.n_utt = n_utt; pf.plen = plen;
     GemvParams h;   // final RMSNorm (hidden side output) + codec head over every row, as the S_main-slot step
     h.W = codec_head_; h.N = V; h.K = H; h.B = rows; h.out_f32 = pf_logits_; h.ldo = V;
-    if (S_main >= gemm_mfma_min_batch()) {
+    if (use_mm(S_main)) {
         if (!decoder_stack_mm(c_, opt_.attn_split, L_, rows, pf_x_, pf_xn_, pf_parts_, pf_qkv_, pf_attn_, pf_hmlp_, kc_, vc_,
                               kv_layer, max_ctx_, max_splits, pos_, rope_, part_, ticket_, s, nullptr, out_norm_, pf_hid_,
                               S_main, false, &pf))
@@ -980,6 +1025,7 @@ bool Engine::prefill(int n_utt, int plen, const float *src, int S_main, hipStrea
         return false;
     }
     if (!ensure_prefill()) return false;
+    if (!mm_ok_) S_main = 1;   // every step of this model runs the 1-slot vector kernels (fam1_)
     Q3T_HIP(hipMemcpy2DAsync(pf_x_, (size_t)plen * H * 4, src, (size_t)10 * H * 4, (size_t)plen * H * 4, n_utt,
                              hipMemcpyDeviceToDevice, s));
     const int key = (S_main * 1024 + n_utt) * 16 + plen;
@@ -1579,7 +1625,7 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
     // frame graph over slots [0, S_eff): S_eff = the highest busy slot + 1, rounded up to 8, never below the smallest
     // batch that keeps the S-slot kernel family (matrix cores from 4 slots, k_attn_seq from 16), whose per-token
     // arithmetic the graph reproduces (policy_slots_ = S): a draining queue stops paying for parked slots
-    const int fam = S >= 16 ? 16 : S >= gemm_mfma_min_batch() ? gemm_mfma_min_batch() : S;
+    const int fam = !mm_ok_ ? 1 : S >= 16 ? 16 : S >= gemm_mfma_min_batch() ? gemm_mfma_min_batch() : S;
     policy_slots_ = S;
     auto frame_graph = [&](hipGraphExec_t *g) -> bool {
         int hi = 0;

@@ -18,6 +18,10 @@ struct Config {
     int hidden = 1024, n_layers = 28, n_heads = 16, n_kv = 8, head_dim = 128, inter = 3072;
     int codec_vocab = 3072, n_codebooks = 16, text_vocab = 151936, text_dim = 2048;
     int cp_layers = 5, cp_vocab = 2048;
+    // code predictor geometry (tts_transformer.cpp:370-389): the talker's values for 0.6B; 1.7B has its own hidden /
+    // FFN width behind code_pred.mtp_proj (talker space -> code-predictor space, applied to every pass input)
+    int cp_hidden = 1024, cp_inter = 3072, cp_heads = 16, cp_kv = 8;
+    bool has_mtp = false;
     float eps = 1e-6f, rope_theta = 1e6f;
     int codec_pad = 2148, codec_bos = 2149, codec_eos = 2150;
     int tts_bos = 151672, tts_eos = 151673, tts_pad = 151671;
@@ -194,6 +198,13 @@ private:
     int q_slots_ = 0;              // slot count of the running queue (the batch the admissions reproduce)
 
     Config c_;
+    Config cpc_;                         // the code predictor's layer geometry (c_ with the cp_* values)
+    bool mm_ok_ = true;                  // the batched matrix-core stack supports this model's shapes
+    int fam1_ = 0;                       // !mm_ok_: every projection runs the vector kernels with a 1-slot K split
+    bool use_mm(int S) const { return mm_ok_ && S >= gemm_mfma_min_batch(); }
+    uint16_t *mtp_ = nullptr;            // code_pred.mtp_proj [cp_hidden][hidden] (1.7B)
+    float *mtp_b_ = nullptr;             // its bias (optional)
+    bool cp_project(int S, const float *x_talker, int ldx, hipStream_t s);   // cpx_ = mtp_proj . x + b
     std::string tts_path_, tok_path_;
     bool talker_ = true;   // false: vocoder-only context
     int device_ = 0, max_slots_ = 0, max_ctx_ = 0, max_trailing_ = 0;

@@ -27,8 +27,8 @@ bool select_tokens(const SelectSpec &sp, const float *logits, int S, hipStream_t
 // sums as gemv.hip's issue_x_gather, so both paths see bit-identical activation rows.
 template <int NT>
 __global__ void __launch_bounds__(256) k_gather_sum(const GatherSum gs, int K, float *out, int ldo) {
-    const int b = blockIdx.x, k = threadIdx.x * 4;
-    if (k >= K) return;
+    const int b = blockIdx.x;
+    for (int k = threadIdx.x * 4; k < K; k += 1024) {   // K > 1024 (1.7B talker rows): one 1024-wide chunk per pass
     const uint16_t *row[NT];
     const float *extra = nullptr;
     if constexpr (NT == 1) {
@@ -55,9 +55,10 @@ __global__ void __launch_bounds__(256) k_gather_sum(const GatherSum gs, int K, f
         a[0] += e.x; a[1] += e.y; a[2] += e.z; a[3] += e.w;
     }
     *reinterpret_cast<float4 *>(out + (size_t)b * ldo + k) = make_float4(a[0], a[1], a[2], a[3]);
+    }
 }
 bool gather_sum(const GatherSum &gs, int nt, int S, int K, float *out, int ldo, hipStream_t s) {
-    if (K > 1024 || K % 4 != 0 || (nt != 1 && nt != 16)) { set_error("gather_sum: unsupported shape"); return false; }
+    if (K % 4 != 0 || (nt != 1 && nt != 16)) { set_error("gather_sum: unsupported shape"); return false; }
     if (S <= 0) return true;
     if (nt == 1) hipLaunchKernelGGL(k_gather_sum<1>, dim3(S), dim3(256), 0, s, gs, K, out, ldo);
     else hipLaunchKernelGGL(k_gather_sum<16>, dim3(S), dim3(256), 0, s, gs, K, out, ldo);

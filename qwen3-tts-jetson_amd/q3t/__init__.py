@@ -34,7 +34,7 @@ class Config(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "hidden", "n_layers", "n_heads", "n_kv_heads", "head_dim", "intermediate", "codec_vocab", "n_codebooks",
         "text_vocab", "text_dim", "cp_layers", "cp_vocab", "codec_eos", "has_vocoder", "sample_rate", "max_slots",
-        "max_ctx")]
+        "max_ctx", "cp_hidden", "cp_intermediate", "cp_heads", "cp_kv_heads", "has_mtp")]
 
 
 class GenParams(C.Structure):

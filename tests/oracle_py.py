@@ -21,7 +21,8 @@ _CFG_FIELDS = [
 
 class OracleConfig(C.Structure):
     _fields_ = [(n, C.c_float if n in ("eps", "rope_theta") else C.c_int) for n in _CFG_FIELDS] + [
-        ("conv_t_k", C.c_int * 4), ("rates", C.c_int * 4)]
+        ("conv_t_k", C.c_int * 4), ("rates", C.c_int * 4)] + [
+        (n, C.c_int) for n in ("cp_hidden", "cp_inter", "cp_heads", "cp_kv", "cp_head_dim", "has_mtp")]
 
 
 def build_oracle():
@@ -95,6 +96,8 @@ class Oracle:
         self.cfg = {n: getattr(c, n) for n in _CFG_FIELDS}
         self.cfg["conv_t_k"] = list(c.conv_t_k)
         self.cfg["rates"] = list(c.rates)
+        for n in ("cp_hidden", "cp_inter", "cp_heads", "cp_kv", "cp_head_dim", "has_mtp"):
+            self.cfg[n] = getattr(c, n)
 
     def close(self):
         if self.h:
@@ -158,7 +161,7 @@ class Oracle:
         return lg
 
     def cp_pass(self, kv, x, pos, head=-1):
-        H = self.cfg["hidden"]
+        H = self.cfg["cp_hidden"] or self.cfg["hidden"]   # x: talker space; the hidden output: code-predictor space
         hid = np.zeros(H, np.float32)
         lg = np.zeros(self.cfg["cp_vocab"], np.float32)
         lib().q3o_cp_pass(self.h, kv, np.ascontiguousarray(x, np.float32), pos, head, _ptr(hid), _ptr(lg))

@@ -37,7 +37,7 @@ def synth_dir(cfg, seed=SEED, variant=""):
 
 
 def prompt(cfg):
-    return list(PROMPT_FULL if cfg == "full" else PROMPT_TINY)
+    return list(PROMPT_FULL if cfg.startswith("full") else PROMPT_TINY)
 
 
 def rel_err(a, b):

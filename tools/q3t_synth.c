@@ -56,6 +56,9 @@ typedef struct {
     int cb_size, cb_dim, voc_hidden, voc_latent, voc_layers, voc_heads, voc_ffn, dec_dim;
     int up_ratio, convnext_mult;
     int rates[4];
+    // code predictor geometry when it differs from the talker's (1.7B: 0 = the talker's values); cp_hidden != hidden
+    // adds code_pred.mtp_proj.{weight,bias} (tts_transformer.cpp:370-389, 611-616)
+    int cp_hidden, cp_inter, cp_heads, cp_kv;
 } cfg_t;
 
 static const cfg_t CFG_FULL = {
@@ -66,6 +69,16 @@ static const cfg_t CFG_TINY1 = {
     "tiny1", 1024, 128, 256, 1, 4, 2, 64, 512, 3072, 16,
     1, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
     2048, 32, 64, 128, 2, 2, 128, 96, 2, 4, {8, 5, 4, 3}};
+// 1.7B-shaped: talker hidden 2048 / FFN 6144, code predictor 1024 / 3072 behind code_pred.mtp_proj
+static const cfg_t CFG_FULL17 = {
+    "full17", 151936, 2048, 2048, 28, 16, 8, 128, 6144, 3072, 16,
+    5, 2048, 1e-6f, 1000000.0f, 151672, 151673, 151671,
+    2048, 256, 512, 1024, 8, 16, 1024, 1536, 2, 4, {8, 5, 4, 3}, 1024, 3072, 16, 8};
+// the same relation at test size: talker 512 wide, code predictor 256 wide (different head counts too)
+static const cfg_t CFG_TINY17 = {
+    "tiny17", 1024, 128, 512, 3, 8, 2, 64, 1024, 3072, 16,
+    3, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
+    2048, 32, 64, 128, 2, 2, 128, 96, 2, 4, {8, 5, 4, 3}, 256, 512, 4, 2};
 static const cfg_t CFG_TINY = {
     "tiny", 1024, 128, 256, 5, 4, 2, 64, 512, 3072, 16,
     5, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
@@ -113,9 +126,13 @@ static void addconv(const char *n, int64_t oc, int64_t ic, int64_t k, double gai
     add_t(n, 3, k, ic, oc, 0.0, gain / sqrt((double)(ic * k)));
 }
 
+static int cp_h(const cfg_t *c) { return c->cp_hidden ? c->cp_hidden : c->hidden; }
+
 static void build_talker(const cfg_t *c) {
     char b[96];
-    const int H = c->hidden, Dq = c->n_heads * c->head_dim, Dkv = c->n_kv * c->head_dim;
+    const int H0 = c->hidden;
+    {
+    const int H = H0;
     addw("talker.text_embd.weight", c->text_vocab, c->text_dim, 0.02 * sqrt((double)c->text_dim));
     addw("talker.text_proj.fc1.weight", c->text_dim, c->text_dim, 1.0);
     add1("talker.text_proj.fc1.bias", c->text_dim, 0.0, 0.02);
@@ -124,9 +141,15 @@ static void build_talker(const cfg_t *c) {
     addw("talker.codec_embd.weight", c->codec_vocab, H, 0.02 * sqrt((double)H) * 8.0);
     addw("talker.codec_head.weight", c->codec_vocab, H, 4.0);
     add1("talker.output_norm.weight", H, 1.0, 0.1);
+    }
     for (int L = 0; L < 2; ++L) {
         const int nl = L == 0 ? c->n_layers : c->cp_layers;
         const char *p = L == 0 ? "talker" : "code_pred";
+        // layer geometry: the talker's, or the code predictor's own (1.7B)
+        const int H = L == 0 ? H0 : cp_h(c);
+        const int nh = L == 1 && c->cp_heads ? c->cp_heads : c->n_heads, nkv = L == 1 && c->cp_kv ? c->cp_kv : c->n_kv;
+        const int Dq = nh * c->head_dim, Dkv = nkv * c->head_dim;
+        const int I = L == 1 && c->cp_inter ? c->cp_inter : c->inter;
         for (int i = 0; i < nl; ++i) {
 #define NM(suf) (snprintf(b, sizeof b, "%s.blk.%d.%s", p, i, suf), b)
             add1(NM("attn_norm.weight"), H, 1.0, 0.1);
@@ -137,13 +160,18 @@ static void build_talker(const cfg_t *c) {
             add1(NM("attn_q_norm.weight"), c->head_dim, 1.0, 0.1);
             add1(NM("attn_k_norm.weight"), c->head_dim, 1.0, 0.1);
             add1(NM("ffn_norm.weight"), H, 1.0, 0.1);
-            addw(NM("ffn_gate.weight"), c->inter, H, 1.0);
-            addw(NM("ffn_up.weight"), c->inter, H, 1.0);
-            addw(NM("ffn_down.weight"), H, c->inter, 0.25);
+            addw(NM("ffn_gate.weight"), I, H, 1.0);
+            addw(NM("ffn_up.weight"), I, H, 1.0);
+            addw(NM("ffn_down.weight"), H, I, 0.25);
 #undef NM
         }
     }
-    add1("code_pred.output_norm.weight", H, 1.0, 0.1);
+    add1("code_pred.output_norm.weight", cp_h(c), 1.0, 0.1);
+    const int H = H0;
+    if (c->cp_hidden && c->cp_hidden != H) {   // talker space -> code-predictor space (every code-predictor input)
+        addw("code_pred.mtp_proj.weight", c->cp_hidden, H, 1.0);
+        add1("code_pred.mtp_proj.bias", c->cp_hidden, 0.0, 0.02);
+    }
     // speaker encoder (ECAPA-TDNN) in the TTS file, as the converter writes it (convert_tts_to_gguf.py:58-124;
     // loader audio_tokenizer_encoder.cpp:185-241): conv weights [OC, IC, K] -> ne [K, IC, OC], F32 biases
 #define SPK(nm, oc, ic, k, g) do { snprintf(b, sizeof b, "spk_enc.%s.weight", nm); addconv(b, oc, ic, k, g); \
@@ -166,7 +194,7 @@ static void build_talker(const cfg_t *c) {
         snprintf(b, sizeof b, "code_pred.codec_embd.%d.weight", i);
         addw(b, c->cp_vocab, H, 0.02 * sqrt((double)H) * 8.0);
         snprintf(b, sizeof b, "code_pred.lm_head.%d.weight", i);
-        addw(b, c->cp_vocab, H, 4.0);
+        addw(b, c->cp_vocab, cp_h(c), 4.0);
     }
 }
 
@@ -596,8 +624,9 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s full|tiny <out_dir> [seed]\n", argv[0]); return 2; }
-    const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : strcmp(argv[1], "tiny1") == 0 ? &CFG_TINY1 : NULL;
+    if (argc < 3) { fprintf(stderr, "usage: %s full|tiny|tiny1|tiny17|full17 <out_dir> [seed]\n", argv[0]); return 2; }
+    const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : strcmp(argv[1], "tiny1") == 0 ? &CFG_TINY1
+                   : strcmp(argv[1], "tiny17") == 0 ? &CFG_TINY17 : strcmp(argv[1], "full17") == 0 ? &CFG_FULL17 : NULL;
     if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
     uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
     g_usage = argc > 4 && strcmp(argv[4], "usage") == 0;
@@ -626,10 +655,10 @@ int main(int argc, char **argv) {
         {"qwen3-tts.num_code_groups", GV_U32, (uint32_t)c->n_codebooks, 0, 0, 0, 0},
         {"qwen3-tts.code_predictor.layer_count", GV_U32, (uint32_t)c->cp_layers, 0, 0, 0, 0},
         {"qwen3-tts.code_predictor.vocab_size", GV_U32, (uint32_t)c->cp_vocab, 0, 0, 0, 0},
-        {"qwen3-tts.code_predictor.embedding_length", GV_U32, (uint32_t)c->hidden, 0, 0, 0, 0},
-        {"qwen3-tts.code_predictor.feed_forward_length", GV_U32, (uint32_t)c->inter, 0, 0, 0, 0},
-        {"qwen3-tts.code_predictor.attention.head_count", GV_U32, (uint32_t)c->n_heads, 0, 0, 0, 0},
-        {"qwen3-tts.code_predictor.attention.head_count_kv", GV_U32, (uint32_t)c->n_kv, 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.embedding_length", GV_U32, (uint32_t)cp_h(c), 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.feed_forward_length", GV_U32, (uint32_t)(c->cp_inter ? c->cp_inter : c->inter), 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.attention.head_count", GV_U32, (uint32_t)(c->cp_heads ? c->cp_heads : c->n_heads), 0, 0, 0, 0},
+        {"qwen3-tts.code_predictor.attention.head_count_kv", GV_U32, (uint32_t)(c->cp_kv ? c->cp_kv : c->n_kv), 0, 0, 0, 0},
         {"qwen3-tts.code_predictor.attention.key_length", GV_U32, (uint32_t)c->head_dim, 0, 0, 0, 0},
         {"qwen3-tts.codec.pad_id", GV_U32, 2148, 0, 0, 0, 0},
         {"qwen3-tts.codec.bos_id", GV_U32, 2149, 0, 0, 0, 0},
