@@ -562,10 +562,24 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
         for (int ri = 0; ri < 3; ++ri) {
             const Res &R = D.res[ri];
             const Snake *next = ri < 2 ? &D.res[ri + 1].a1 : d < 3 ? &dec_[d + 1].snake : &dec5_;
+            // the last unit of the last block feeds only the output conv's f16 input: no f32 residual stream out
+            float *xout = d == 3 && ri == 2 ? nullptr : cur;
+            if (fuse_res_ && R.c1.ic == 96 && R.c1.oc == 96 && R.c1.k == 7 && R.c2.ic == 96 && R.c2.oc == 96 && R.c2.k == 1 &&
+                R.dil <= 9 && R.c1.b && R.c2.b) {
+                // the whole unit in one launch (vocoder_resunit.hip): h stays on chip, bit-identical to the two convs
+                ResUnitParams u;
+                u.xh = ha; u.x = cur; u.y = xout; u.y16 = hb; u.T = (int)T; u.dil = R.dil;
+                u.w1 = R.c1.w; u.b1 = R.c1.b; u.a2 = R.a2.a; u.ib2 = R.a2.ib;
+                u.w2 = R.c2.w; u.b2 = R.c2.b; u.an = next->a; u.ibn = next->ib;
+                u.nb = nb_; u.bs = T;
+                if (!resunit96(u, s)) return false;
+                std::swap(ha, hb);
+                continue;
+            }
             // h1 = conv1(snake1(x)) with causal pad 6*dil -> only snake2(h1) in f16; x += conv2(snake2(h1)) (f32, in
             // place) plus the next conv's f16 input
             if (!conv16(R.c1, ha, (int)T, 6 * R.dil, R.dil, nullptr, nullptr, hb, &R.a2, s)) return false;
-            if (!conv16(R.c2, hb, (int)T, 0, 1, cur, cur, ha, next, s)) return false;
+            if (!conv16(R.c2, hb, (int)T, 0, 1, xout, cur, ha, next, s)) return false;
         }
     }
     // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790): ha holds f16(snake(dec5)) of the stream

@@ -1,6 +1,7 @@
 // vocoder.h — MI355X-native Qwen3-TTS tokenizer decoder ("vocoder"), replacing TRTVocoderDecoder
 // (src/trt_vocoder.cpp) and the GGML AudioTokenizerDecoder (src/audio_tokenizer_decoder.cpp).
 #pragma once
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -85,6 +86,8 @@ private:
     int cap_frames_ = 0, batch_frames_ = 4096;
     size_t cap_big_ = 0, cap_ftot_ = 0, cap_pcm_ = 0;
     int nb_ = 1;   // utterances of the decode in flight (conv launches carry it as grid z)
+    // the 96-channel residual units as one launch each (vocoder_resunit.hip); Q3T_VOC_FUSE=0: the two-conv form
+    bool fuse_res_ = [] { const char *e = std::getenv("Q3T_VOC_FUSE"); return !(e && e[0] == '0'); }();
     float *buf_[3] = {nullptr, nullptr, nullptr};
     uint16_t *xh_ = nullptr;   // f16 (snake'd) conv input, one activation
     uint16_t *xh2_ = nullptr;  // second f16 activation: the decoder blocks ping-pong conv inputs written by epilogues

@@ -5,6 +5,19 @@
 namespace q3t {
 
 constexpr int CONV_MAX_TAPS = 7;
+
+// SnakeBeta x + exp(-beta) sin^2(exp(alpha) x) with a = exp(alpha), ib = exp(-beta) (audio_tokenizer_decoder.cpp
+// SnakeBeta).  The sine: reduce to [-0.5, 0.5] revolutions (v_rndne) and use the hardware v_sin_f32 -- ocml's sinf is
+// ~30 VALU instructions with a range-reduction branch and ran twice per activation element of every residual unit;
+// its result is rounded to f16 right after, so the ~1e-6 difference flips an f16 rounding only rarely.  Every kernel
+// that applies SnakeBeta calls this one function, rounding each operation as written (no contraction), so a fused
+// and an unfused launch sequence produce the same bits.
+__device__ __forceinline__ float snake_apply(float z, float a, float ib) {
+#pragma clang fp contract(off)
+    const float r = (z * a) * 0.15915494309189535f;   // 1 / (2 pi)
+    const float sn = __builtin_amdgcn_sinf(r - __builtin_rintf(r));
+    return z + (sn * sn) * ib;
+}
 struct ConvTap { const uint16_t *w; int dj; };   // w: [C_out][C_in] f16 of one kernel tap; input row offset dj
 // y[m*so + ob][co] = act(bias[co] + resid + sum_j sum_ci w_j[co][ci] * f16(snake(x[m + dj][ci])))
 // x: [T_in][C_in] f32 (rows outside [0,T_in) read as 0 = causal zero padding); y: [T_out][C_out] f32
@@ -39,6 +52,22 @@ struct ConvParams {
     int dev_skip = 0;   // development builds only (timing experiments): 1 weight loads, 2 window loads, 4 epilogue
 };
 bool conv(const ConvParams &p, hipStream_t s);
+// one 96-channel decoder residual unit as one launch (vocoder_resunit.hip), bit-identical to its two conv launches:
+//   h = f16(snake2(conv7_dil(xh) + b1)) (kept on chip);  y = x + conv1(h) + b2;  y16 = f16(snake_next(y))
+// xh / y16 are f16 [T][96] (different buffers: a tile's causal window reads rows of its neighbours), x / y f32 (may
+// alias: in place; y null skips the f32 output); w1 [7][96][96], w2 [96][96] f16; nb utterances bs rows apart
+struct ResUnitParams {
+    const uint16_t *xh = nullptr;
+    const float *x = nullptr;
+    float *y = nullptr;
+    uint16_t *y16 = nullptr;
+    int T = 0, dil = 1;
+    const uint16_t *w1 = nullptr, *w2 = nullptr;
+    const float *b1 = nullptr, *a2 = nullptr, *ib2 = nullptr, *b2 = nullptr, *an = nullptr, *ibn = nullptr;
+    int nb = 1;
+    int64_t bs = 0;
+};
+bool resunit96(const ResUnitParams &p, hipStream_t s);
 // out[t][c] = f16( snake(x[t][c]) ) (SnakeBeta x + exp(-beta) sin^2(exp(alpha) x), or plain rounding when a is null):
 // the conv input computed ONCE per element instead of once per (output tile, tap window) inside k_conv
 bool snake_f16(const float *x, const float *a, const float *ib, uint16_t *out, int64_t T, int C, hipStream_t s);

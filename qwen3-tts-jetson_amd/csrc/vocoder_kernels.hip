@@ -16,16 +16,6 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 // Tile 64 (m) x 64 (co); 4 waves as 2 x 2 of 32 x 32; K-chunk = 32 input channels.
 constexpr int CT_M = 64, CT_N = 64, CT_K = 32, CT_LD = CT_K + 8;   // LDS row: 32 f16 + 16 B pad
 
-// sin for SnakeBeta: reduce to [-0.5, 0.5] revolutions (v_rndne) and use the hardware v_sin_f32.  ocml's sinf is
-// ~30 VALU instructions with a range-reduction branch; the vocoder evaluates it twice per activation element of every
-// residual unit (~190 M per unit at 512 frames), which made it a quarter of the narrow blocks' time.  Its result is
-// rounded to f16 right after (x + sin^2 * ib), so the ~1e-6 absolute difference flips an f16 rounding only rarely
-// (PCM parity vs the oracle's sinf stays within the test's 1e-2 / RMS bar).
-__device__ __forceinline__ float snake_sin(float v) {
-    const float r = v * 0.15915494309189535f;   // 1 / (2 pi)
-    return __builtin_amdgcn_sinf(r - __builtin_rintf(r));
-}
-
 __device__ __forceinline__ float conv_act(float v, int act) {
     if (act == 1) return tanhf(v);
     if (act == 2) return fmaxf(v, 0.0f);
@@ -88,8 +78,7 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if (ci + q < p.C_in) {
-                            const float sn = snake_sin(v[q] * p.snake_a[ci + q]);
-                            v[q] = v[q] + (sn * sn) * p.snake_ib[ci + q];
+                            v[q] = snake_apply(v[q], p.snake_a[ci + q], p.snake_ib[ci + q]);
                         }
                     }
                 }
@@ -147,8 +136,7 @@ __global__ void __launch_bounds__(256) k_conv(const ConvParams p) {
         if (py16) {
             float z = v;
             if (p.y16_a) {
-                const float sn = snake_sin(z * sa);
-                z = z + (sn * sn) * sib;
+                z = snake_apply(z, sa, sib);
             }
             py16[t * p.C_out + co] = f2h(z);
         }
@@ -388,10 +376,7 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
                     const float4 sb = *reinterpret_cast<const float4 *>(prm + 3 * NT + q4);
                     const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float sn = snake_sin(z[q] * av[q]);
-                        z[q] = z[q] + (sn * sn) * bv[q];
-                    }
+                    for (int q = 0; q < 4; ++q) z[q] = snake_apply(z[q], av[q], bv[q]);
                 }
                 uint2 hv;
                 hv.x = (uint32_t)f2h(z[0]) | ((uint32_t)f2h(z[1]) << 16);
@@ -513,10 +498,7 @@ __global__ void __launch_bounds__(256) k_snake_f16(const float *x, const float *
     float y[4] = {v.x, v.y, v.z, v.w};
     if (a) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {   // the k_conv staging expression, term for term
-            const float sn = snake_sin(y[q] * a[c + q]);
-            y[q] = y[q] + (sn * sn) * ib[c + q];
-        }
+        for (int q = 0; q < 4; ++q) y[q] = snake_apply(y[q], a[c + q], ib[c + q]);
     }
     uint2 h;
     h.x = (uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16);

@@ -102,3 +102,33 @@ def test_vocoder_batch_chunk40(pair):
         assert float(np.abs(g - s).max()) < 2e-3
     o = orc.vocoder(codes[0], 1)
     assert float(np.abs(outs[0] - o).max()) < PCM_TOL[cfg]
+
+
+@pytest.mark.parametrize("F,nutt", [(40, 1), (200, 1), (33, 3)])
+def test_fused_residual_unit_bit_exact(F, nutt):
+    """the 96-channel residual units as one launch each (vocoder_resunit.hip) against their two-conv form
+    (Q3T_VOC_FUSE=0): bit-identical PCM, single decodes and an utterance batch"""
+    import q3t
+    tts, tok = synth_dir("full")
+    old = os.environ.get("Q3T_VOC_FUSE")
+    os.environ["Q3T_VOC_FUSE"] = "0"
+    try:
+        ref = q3t.Engine(None, tok, device=0)
+    finally:
+        if old is None:
+            del os.environ["Q3T_VOC_FUSE"]
+        else:
+            os.environ["Q3T_VOC_FUSE"] = old
+    fused = q3t.Engine(None, tok, device=0)
+    try:
+        cl = [_codes(F + 7 * u, 100 + u) for u in range(nutt)]
+        if nutt == 1:
+            a, b = [fused.vocoder(cl[0], 0)], [ref.vocoder(cl[0], 0)]
+        else:
+            a, b = fused.vocoder_batch(cl, 0), ref.vocoder_batch(cl, 0)
+        for x, y in zip(a, b):
+            assert x.shape == y.shape
+            assert np.array_equal(x, y), float(np.abs(x - y).max())
+    finally:
+        fused.close()
+        ref.close()
