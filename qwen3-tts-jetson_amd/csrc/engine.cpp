@@ -446,7 +446,9 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
         std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
-        if (opt_.cp_qkv_table && !build_cp_qkv_table()) return false;
+        // (a context for few slots: the batched serving contexts do not pay the table's 520 MB; their rare 1-slot calls
+        // run the persistent frame without it)
+        if (opt_.cp_qkv_table && max_slots_ <= 4 && !build_cp_qkv_table()) return false;
     }
     // (pstate_ was zeroed on the context stream by dalloc)
 #ifdef Q3T_DEV

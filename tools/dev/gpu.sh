@@ -64,7 +64,7 @@ fetch)
     SLOTS=${*:-1 64}
     prof_dir "fetch_$TAG"
     for B in $SLOTS; do
-        timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$P/pmc$B" -o pmc -- python3 "$R/tools/dev/stage_only.py" 0 $B 266 10 > "$R/gpurun_out/pmc_${TAG}_b$B.log" 2>&1 || { echo "pmc failed"; tail -20 "$R/gpurun_out/pmc_${TAG}_b$B.log"; exit 1; }
+        Q3T_CP_QKV_TABLE=0 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$P/pmc$B" -o pmc -- python3 "$R/tools/dev/stage_only.py" 0 $B 266 10 > "$R/gpurun_out/pmc_${TAG}_b$B.log" 2>&1 || { echo "pmc failed"; tail -20 "$R/gpurun_out/pmc_${TAG}_b$B.log"; exit 1; }
         C=$(find "$P/pmc$B" -name '*counter_collection.csv' | head -1)
         python3 "$R/tools/dev/pmc_sum.py" "$C" 11 > "$R/gpurun_out/pmc_${TAG}_b${B}_summary.txt"
         head -8 "$R/gpurun_out/pmc_${TAG}_b${B}_summary.txt"
