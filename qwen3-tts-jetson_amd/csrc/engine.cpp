@@ -420,22 +420,28 @@ bool Engine::alloc_state() {
 bool Engine::setup_persist() {
     int n_cu = 0;
     Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
-    persist_ = persist_ && fused_select_ &&
-               persist_supported(c_.hidden, c_.n_heads, c_.n_kv, c_.head_dim, c_.inter, c_.codec_vocab, max_ctx_, n_cu);
-    const bool cp_ok = opt_.persist_cp && c_.cp_vocab == 2048 && CP_.size() >= 1 && CP_.size() <= 32 && cp_head_.size() == 15 &&
-                       !c_.has_mtp && c_.cp_hidden == 1024 && c_.cp_inter == 3072 && c_.cp_heads == 16 && c_.cp_kv == 8;
+    const bool use = persist_ && fused_select_;
+    persist_ = use && persist_supported(c_.hidden, c_.n_heads, c_.n_kv, c_.head_dim, c_.inter, c_.codec_vocab, max_ctx_, n_cu);
+    // the code-predictor frame needs the 0.6B code-predictor shapes only: the 1.7B one (a 2,048-wide talker) runs it
+    // too, on projected table rows (build_cp_proj_table) with a projected pass-0 input
+    const bool cp_ok = use && opt_.persist_cp && c_.cp_vocab == 2048 && c_.codec_vocab == 3072 && CP_.size() >= 1 &&
+                       CP_.size() <= 32 && cp_head_.size() == 15 && c_.cp_hidden == 1024 && c_.cp_inter == 3072 &&
+                       c_.cp_heads == 16 && c_.cp_kv == 8 && c_.head_dim == 128 && n_cu >= 256;
     // every instantiation must fit one workgroup per CU on this device (occupancy query with its LDS request)
     persist_ = persist_ && persist_resident(device_, max_ctx_, cp_ok);
-    if (!persist_) return true;
-    std::vector<PLayerW> pl(L_.size());
-    for (size_t i = 0; i < L_.size(); ++i)
-        pl[i] = PLayerW{L_[i].qkv, L_[i].o, L_[i].gu, L_[i].down, L_[i].attn_norm, L_[i].ffn_norm, L_[i].qn, L_[i].kn};
-    pl_dev_ = dalloc<PLayerW>(pl.size());
+    persist_cp_ = cp_ok && persist_resident_cp(device_);
+    if (!persist_ && !persist_cp_) return true;
     pstate_ = dalloc<uint8_t>(persist_state_bytes());
-    if (!pl_dev_ || !pstate_) { set_error("device allocation failed"); return false; }
-    Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+    if (!pstate_) { set_error("device allocation failed"); return false; }
+    if (persist_) {
+        std::vector<PLayerW> pl(L_.size());
+        for (size_t i = 0; i < L_.size(); ++i)
+            pl[i] = PLayerW{L_[i].qkv, L_[i].o, L_[i].gu, L_[i].down, L_[i].attn_norm, L_[i].ffn_norm, L_[i].qn, L_[i].kn};
+        pl_dev_ = dalloc<PLayerW>(pl.size());
+        if (!pl_dev_) { set_error("device allocation failed"); return false; }
+        Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+    }
     // the code-predictor frame (persist_cp_frame): its 5 layers and 15 lm_heads
-    persist_cp_ = cp_ok;
     if (persist_cp_) {
         std::vector<PLayerW> cpl(CP_.size());
         for (size_t i = 0; i < CP_.size(); ++i)
@@ -448,6 +454,7 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
         // (a context for few slots: the batched serving contexts do not pay the table's 520 MB; their rare 1-slot calls
         // run the persistent frame without it)
+        if (c_.has_mtp && !build_cp_proj_table()) return false;
         if (opt_.cp_qkv_table && max_slots_ <= 4 && !build_cp_qkv_table()) return false;
     }
     // (pstate_ was zeroed on the context stream by dalloc)
@@ -480,8 +487,44 @@ bool Engine::build_cp_qkv_table() {
         g.pro = PRO_RMS_G1; g.nw = CP_[0].attn_norm; g.eps = c_.eps;
         g.gs.tok = iota; g.gs.tok_ld = 1; g.gs.tok_col0 = 0;
         g.gs.tab0 = t == 0 ? codec_embd_ : cp_embd_[t - 1];
+        if (cp_projtab_) {   // 1.7B: layer 0 normalises the projected row (the per-op path's PRO_RMS on cpx_)
+            g.pro = PRO_RMS; g.x = cp_projtab_ + row0 * H; g.ldx = H;
+        }
         g.out_f32 = cp_qkvtab_ + row0 * QKV; g.ldo = QKV;
         g.family_b = 1;
+        if (!gemv(g, stream_)) return false;
+        row0 += V;
+    }
+    Q3T_HIP(hipStreamSynchronize(stream_));
+    return true;
+}
+
+// 1.7B: every code-predictor pass input is mtp_proj . f16(row) + b of a talker-space row; for passes 1..15 the row is a
+// table row, so the projected input is a function of the token: computed once here for the 15 tables with the per-op
+// path's own launches (k_gather_sum + the mtp_proj GEMV with a 1-slot K split), the persistent frame then reads it
+// (130 MB of f32).
+bool Engine::build_cp_proj_table() {
+    const int H = c_.hidden, CH = c_.cp_hidden;
+    const size_t rows = persist_qkv_table_rows();
+    cp_projtab_ = dalloc<float>(rows * CH);
+    int *iota = dalloc<int>(c_.codec_vocab);
+    float *rowbuf = dalloc<float>((size_t)c_.codec_vocab * H);
+    if (!cp_projtab_ || !iota || !rowbuf) { set_error("device allocation failed (code-predictor projected table)"); return false; }
+    std::vector<int> ih(c_.codec_vocab);
+    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
+    Q3T_HIP(hipMemcpyAsync(iota, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+    size_t row0 = 0;
+    for (int t = 0; t < 15; ++t) {
+        const int V = t == 0 ? c_.codec_vocab : c_.cp_vocab;
+        GatherSum gs;
+        gs.tok = iota; gs.tok_ld = 1; gs.tok_col0 = 0;
+        gs.tab0 = t == 0 ? codec_embd_ : cp_embd_[t - 1];
+        if (!gather_sum(gs, 1, V, H, rowbuf, H, stream_)) return false;
+        GemvParams g;
+        g.W = mtp_; g.N = CH; g.K = H; g.B = V;
+        g.pro = PRO_F32; g.x = rowbuf; g.ldx = H;
+        g.bias = mtp_b_;
+        g.out_f32 = cp_projtab_ + row0 * CH; g.ldo = CH; g.family_b = 1;
         if (!gemv(g, stream_)) return false;
         row0 += V;
     }
@@ -541,7 +584,7 @@ bool Engine::debug_read(int which, void *dst, size_t bytes) {
 // with the abort word already set, exactly as if one of its hand-off waits had given up.  Host-side on purpose: a
 // device-side launch counter in k_persist's prologue cost 32 us per talker step in code generation alone.
 bool Engine::persist_fault_hook(int S, int n_launches) {
-    if (!opt_.persist_fault_at || S != 1 || !persist_ || !pstate_) return true;
+    if (!opt_.persist_fault_at || S != 1 || !persist_enabled() || !pstate_) return true;
     const unsigned before = persist_launches_;
     persist_launches_ += (unsigned)n_launches;
     if (before < opt_.persist_fault_at && opt_.persist_fault_at <= persist_launches_) {
@@ -553,7 +596,7 @@ bool Engine::persist_fault_hook(int S, int n_launches) {
 }
 
 bool Engine::persist_error() {
-    if (!persist_ || !pstate_) return false;
+    if (!persist_enabled() || !pstate_) return false;
     PersistParams p;
     persist_carve(pstate_, p);
     unsigned e = 0;
@@ -824,11 +867,16 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
     // vector path with fused selection: heads 0..13 only produce logits; the next pass's QKV launch selects the token
     // in every workgroup while its weights stream (PRO_SEL_G1), so the head's 256 -> 1 arrival chain and the serial
     // selection leave the critical path.  Head 14 (its token feeds the next talker step) keeps the fused selection.
-    if (S == 1 && persist_ && persist_cp_ && !logits_host) {   // the whole frame as one persistent launch
+    if (S == 1 && persist_cp_ && !logits_host) {   // the whole frame as one persistent launch
         PersistParams p;
         persist_carve(pstate_, p);
         p.L = pl_cp_dev_; p.n_layers = c_.cp_layers; p.eps = c_.eps;
         p.x_in = hidden_;
+        if (c_.has_mtp) {   // 1.7B: pass 0's projected input by the per-op GEMV, passes 1..15 from the projected table
+            if (!cp_project(1, hidden_, c_.hidden, s)) return false;
+            p.x_in = cpx_;
+            p.xtab = cp_projtab_;
+        }
         p.gs.tok = tokens_; p.gs.tok_ld = 16; p.gs.tabs = tabs16_dev_;
         p.rope = rope_; p.kc = cpkc_; p.vc = cpvc_; p.kv_layer = kv_layer; p.n_ctx = 16;
         p.heads = heads_dev_; p.out_norm = cp_out_norm_; p.logits = cp_logits_;
@@ -1181,7 +1229,7 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
     // only single-slot runs launch the persistent kernels: batched contexts on one device run concurrently
-    DeviceLock lk(persist_ && n_utt == 1, device_);
+    DeviceLock lk(persist_enabled() && n_utt == 1, device_);
     StreamState st;
     st.delivered.assign(n_utt, 0);
     st.stop_at.assign(n_utt, -1);
@@ -1339,7 +1387,7 @@ bool Engine::generate_once(int n_utt, const int32_t *const *tokens, const int *n
     };
     bool all_done = false;
     for (int f = 0; f < gp.max_len && !all_done && n_live > 0; ++f) {
-        if (!persist_fault_hook(S, persist_cp_ ? 2 : 1)) return false;
+        if (!persist_fault_hook(S, (persist_ ? 1 : 0) + (persist_cp_ ? 1 : 0))) return false;
         Q3T_HIP(hipGraphLaunch(g_frame_[S], stream_));
         if (dbg) { fprintf(stderr, "[q3t] frame %d launched\n", f); fflush(stderr); }
         if (stream_cb && (f + 1) % interval == 0) {
@@ -1550,7 +1598,7 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
     if (!alloc_admission()) return false;
     q_slots_ = S;
     // the single-slot context runs persistent kernels, which need the whole device: admissions go on the main stream
-    hipStream_t as = (S == 1 && persist_) ? stream_ : astream_;
+    hipStream_t as = (S == 1 && persist_enabled()) ? stream_ : astream_;
     if (!(gp.temperature == gp_.temperature && gp.top_k == gp_.top_k && gp.rep_penalty == gp_.rep_penalty)) {
         for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
         g_frame_.clear();
@@ -1650,7 +1698,7 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
         }
         hipGraphExec_t fg = nullptr;
         if (!frame_graph(&fg)) { cleanup(); return false; }
-        if (!persist_fault_hook(S, persist_cp_ ? 2 : 1)) { cleanup(); return false; }
+        if (!persist_fault_hook(S, (persist_ ? 1 : 0) + (persist_cp_ ? 1 : 0))) { cleanup(); return false; }
         Q3T_HIP(hipGraphLaunch(fg, stream_));
         ++f;
         if (polled) {
@@ -1693,7 +1741,7 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
 bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
                             const GenParams &gp, int32_t *codes, int *n_frames, int max_active) {
     const int S = std::min(max_slots_, std::max(n_utt, 1));
-    DeviceLock lk(persist_ && S == 1, device_);
+    DeviceLock lk(persist_enabled() && S == 1, device_);
     bool fault = false;
     if (generate_queue_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, max_active, &fault)) return true;
     if (!fault) return false;
@@ -1705,7 +1753,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
-    DeviceLock lk(persist_ && S == 1, device_);
+    DeviceLock lk(persist_enabled() && S == 1, device_);
     std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
@@ -1757,7 +1805,7 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
     const int H = c_.hidden;
-    DeviceLock lk(persist_ && S == 1, device_);
+    DeviceLock lk(persist_enabled() && S == 1, device_);
     for (int attempt = 0; attempt < 2; ++attempt) {
         Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
         Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
@@ -1778,7 +1826,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int H = c_.hidden;
     for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
-    DeviceLock lk(persist_ && S == 1, device_);
+    DeviceLock lk(persist_enabled() && S == 1, device_);
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;

@@ -131,7 +131,7 @@ public:
     bool persist_fault_hook(int S, int n_launches);   // Q3T_PERSIST_FAULT_AT test hook (host side)
     unsigned persist_launches_ = 0;
     bool persist_error();
-    bool persist_enabled() const { return persist_; }
+    bool persist_enabled() const { return persist_ || persist_cp_; }
     bool persist_fell_back() const { return persist_fallback_; }
 #ifdef Q3T_DEV
     // development hook: copy a device state buffer to the host (0 K cache, 1 V cache, 2 qkv, 3 attention output)
@@ -259,6 +259,8 @@ private:
     PLayerW *pl_dev_ = nullptr, *pl_cp_dev_ = nullptr;
     const uint16_t **heads_dev_ = nullptr;
     float *cp_qkvtab_ = nullptr;         // persistent code-predictor frame: layer 0's QKV row per table token
+    float *cp_projtab_ = nullptr;        // 1.7B: mtp_proj . f16(table row) + b per table token (f32, code-predictor space)
+    bool build_cp_proj_table();
     bool build_cp_qkv_table();
     bool persist_cp_ = false;
     uint8_t *pstate_ = nullptr;

@@ -52,6 +52,9 @@ struct PersistParams {
     // codec_embd rows, pass p >= 2: code_pred.codec_embd[p-2] rows), computed with the per-op QKV GEMV's arithmetic
     // (persist_qkv_table_rows): passes 1..15 then skip layer 0's norm + QKV phase and its edge
     const float *qkvtab = nullptr;
+    // code-predictor frame (1.7B): the pass inputs of passes 1..15 as projected f32 rows [3072 + 14 * 2048][1024] in
+    // place of the f16 table rows (gs.tabs), same row order as qkvtab; x_in is then the projected pass-0 input
+    const float *xtab = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
 };
@@ -63,6 +66,7 @@ bool persist_supported(int hidden, int n_heads, int n_kv, int head_dim, int inte
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor with the kernel's LDS request) and the device has >= 256 CUs, so the
 // 256-workgroup grid is co-resident when nothing else occupies the device (MI355X_MICROARCH.md, Residency)
 bool persist_resident(int device, int n_ctx, bool cp_frame);
+bool persist_resident_cp(int device);   // the code-predictor frame alone (a talker the step kernel does not cover)
 size_t persist_state_bytes();                    // granule buffers + counters (zeroed once at allocation)
 void persist_carve(uint8_t *base, PersistParams &p);   // point the hand-off buffers into a zeroed state block
 bool persist_talker_step(const PersistParams &p, hipStream_t s);

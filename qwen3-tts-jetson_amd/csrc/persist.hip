@@ -266,8 +266,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 const size_t row = (size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok;
                 traw = ld8(p.qkvtab + row * QKVN + gi);
             }
-            const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);   // the residual row
-            x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
+            if (p.xtab) {   // 1.7B: the projected row
+                x = ldf4(p.xtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok) * H + 4 * t);
+            } else {        // the residual row
+                const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
+                x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
+            }
         } else if (l == 0) {
             if (MODE == 0 && p.gather) {
                 const GatherSum &gs = p.gs;
@@ -292,8 +296,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                     g_wait<1>(p.gtok + pass - 1, TAG(ph0 - 1), u1, c);
                     tok = min((int)u1[0], p.sel.V - 1);   // an aborted wait returns a stale payload: keep it in the table
                 }
-                const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
-                x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
+                if (p.xtab) {
+                    x = ldf4(p.xtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok) * H + 4 * t);
+                } else {
+                    const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
+                    x = make_float4(h2f(hv.x & 0xffff), h2f(hv.x >> 16), h2f(hv.y & 0xffff), h2f(hv.y >> 16));
+                }
             }
         } else {
             uint32_t u[4];
@@ -749,6 +757,14 @@ bool persist_resident(int device, int n_ctx, bool cp_frame) {
     }
     if (!fits(k)) return false;
     return !cp_frame || fits(reinterpret_cast<const void *>(&k_persist<1, 16>));
+}
+
+bool persist_resident_cp(int device) {
+    int n_cu = 0, blocks = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < G) return false;
+    const void *k = reinterpret_cast<const void *>(&k_persist<1, 16>);
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds()) != hipSuccess) return false;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, persist_lds()) == hipSuccess && blocks >= 1;
 }
 
 void persist_carve(uint8_t *base, PersistParams &p) {

@@ -42,7 +42,7 @@ def test_config_reports_code_predictor_geometry(tiny17):
     assert (c["hidden"], c["cp_hidden"], c["cp_intermediate"], c["cp_heads"], c["cp_kv_heads"], c["has_mtp"]) == \
         (orc.cfg["hidden"], orc.cfg["cp_hidden"], orc.cfg["cp_inter"], orc.cfg["cp_heads"], orc.cfg["cp_kv"], 1)
     assert c["cp_hidden"] != c["hidden"]
-    assert eng.persist_status() == -1   # launch-per-op graphs
+    assert eng.persist_status() == -1   # launch-per-op graphs (a 256-wide code predictor: no persistent frame)
 
 
 def test_talker_step_matches_oracle(tiny17):
@@ -116,3 +116,41 @@ def test_full17_shapes_generate_and_vocoder():
     finally:
         eng.close()
         orc.close()
+
+
+def test_full17_persistent_code_predictor_bit_exact():
+    """1.7B at one slot: the code-predictor frame runs as the persistent launch (its code predictor has the 0.6B
+    shapes) on projected table rows and a projected pass-0 input; it must equal the launch-per-op frame bit for bit
+    (the per-op code predictor with its attention as its own launch, the arithmetic the persistent frame reproduces)"""
+    import q3t
+    tts, tok = synth_dir("full17")
+    env = {"Q3T_PERSIST": "0", "Q3T_CP_FUSED_ATTN": "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ref = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=64)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=64)
+    try:
+        assert eng.persist_status() == 0 and ref.persist_status() == -1
+        H = eng.cfg["hidden"]
+        rng = np.random.default_rng(9)
+        for frame in range(6):
+            hid = (rng.standard_normal(H) * 1.5).astype(np.float32)
+            cb0 = int(rng.integers(0, 2048))
+            for T in (0.0, 0.9):
+                a = eng.codepred_frame(hid[None], [cb0], temperature=T, top_k=50, seed=3, frame=frame)
+                b = ref.codepred_frame(hid[None], [cb0], temperature=T, top_k=50, seed=3, frame=frame)
+                assert np.array_equal(a, b), (frame, T, a, b)
+        toks = prompt("full17")
+        kw = dict(speakers=[np.zeros(H, np.float32)], max_len=16, temperature=0.9, top_k=50, seed=5, force_frames=16)
+        assert np.array_equal(eng.generate([toks], **kw)[0], ref.generate([toks], **kw)[0])
+        assert eng.persist_status() == 0
+    finally:
+        eng.close()
+        ref.close()
