@@ -178,6 +178,7 @@ __device__ __forceinline__ void issue_rows_ks4(const uint16_t *W, int K, int row
 // position q (16-position cache, always one split), pass q >= 1 ends with lm_head[q-1] + token selection by the last
 // workgroup, whose token (a granule) feeds the next pass's embedding gather.  K/V rows written by an earlier pass of
 // the same launch are read back by the same workgroup with sc1 loads (no stale L1 line).
+// MODE 2: MODE 1 with the pass inputs of passes 1..15 read as projected f32 rows (p.xtab, the 1.7B layout).
 template <int MODE, int CH>
 __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -198,10 +199,10 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     // code-predictor frame with the layer-0 QKV table: the 8 attention workgroups select each pass's token themselves
     // (no hand-off before the next pass's attention), workgroup 0 records it and hands it to the others (they need it
     // only for layer 0's residual row, off the chain); otherwise SELW selects and hands the token to everyone
-    const bool tab = MODE == 1 && p.qkvtab != nullptr;
+    const bool tab = MODE >= 1 && p.qkvtab != nullptr;
     const bool selector = tab ? att : w == SELW;
     const bool committer = tab ? w == 0 : w == SELW;
-    int cur_tok = MODE == 1 ? p.gs.tok[0] : 0;   // tab: this attention workgroup's token of the previous pass
+    int cur_tok = MODE >= 1 ? p.gs.tok[0] : 0;   // tab: this attention workgroup's token of the previous pass
     const int pg = t >> 4, li = t & 15;          // attention: position group, 8-dim chunk
 
     // development timeline (p.prof): wall clock at wait start / input arrived / output published, per phase
@@ -221,7 +222,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
             const int j = min(j0 + pi * 16 + pg, kpos);
-            if constexpr (MODE == 1) {
+            if constexpr (MODE >= 1) {
                 kr[pi] = ld16_sc1(p.kc + o + (size_t)j * D + li * 8);
                 vr[pi] = ld16_sc1(p.vc + o + (size_t)j * D + li * 8);
             } else {
@@ -231,12 +232,12 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         }
     };
     if (t < p.n_layers) S.layers[t] = p.L[t];
-    if (MODE == 1 && t < 15) S.heads[t] = p.heads[t];
+    if (MODE >= 1 && t < 15) S.heads[t] = p.heads[t];
     // the selection's per-slot inputs (done, frame, seed, utterance, CB0 seen bytes) loaded before any wait, so that
     // none of these dependent loads sits between the last logits and the token
     SelPre spre;
     constexpr int SELM = MODE == 0 ? SEL_CB0 : SEL_CP;
-    constexpr bool HOIST = MODE == 1 ? Q3T_SEL_HOIST1 : Q3T_SEL_HOIST0;
+    constexpr bool HOIST = MODE >= 1 ? Q3T_SEL_HOIST1 : Q3T_SEL_HOIST0;
     if (HOIST && p.sel.mode != SEL_NONE && selector) sel_prefetch<SELM>(p.sel, 0, spre);
     issue_rows_k1024(p.L[0].qkv, w * 16 + grp, wq);
     if (att) issue_kv(0, pos);
@@ -246,7 +247,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     __syncthreads();   // layer / head tables visible
     for (int pass = 0, ph0 = 0; pass < npass; ++pass, ph0 += PPH) {
     const bool head_here = MODE == 0 || pass > 0;
-    if (MODE == 1) pos = pass;
+    if (MODE >= 1) pos = pass;
     for (int l = 0; l < nl; ++l) {
         const PLayerW Lw = S.layers[l];
         const size_t kvo = (size_t)l * p.kv_layer + (size_t)ag * p.n_ctx * D;
@@ -266,7 +267,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 const size_t row = (size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok;
                 traw = ld8(p.qkvtab + row * QKVN + gi);
             }
-            if (p.xtab) {   // 1.7B: the projected row
+            if constexpr (MODE == 2) {   // 1.7B: the projected row
                 x = ldf4(p.xtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok) * H + 4 * t);
             } else {        // the residual row
                 const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                     g_wait<1>(p.gtok + pass - 1, TAG(ph0 - 1), u1, c);
                     tok = min((int)u1[0], p.sel.V - 1);   // an aborted wait returns a stale payload: keep it in the table
                 }
-                if (p.xtab) {
+                if constexpr (MODE == 2) {
                     x = ldf4(p.xtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * 2048) + tok) * H + 4 * t);
                 } else {
                     const uint2 hv = ld8(p.gs.tabs[pass - 1] + (size_t)tok * H + 4 * t);
@@ -646,7 +647,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         uint4 wh[8];
 #pragma unroll
         for (int tt = 0; tt < 8; ++tt) wh[tt] = wq[tt];
-        if (MODE == 1 && pass + 1 < npass) {
+        if (MODE >= 1 && pass + 1 < npass) {
             if (!tab) {
                 nwA = ldf4(S.layers[0].attn_norm + 4 * t);
                 issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
@@ -671,7 +672,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         if (selector) {
             int tok = -1;
             SelectSpec sp = p.sel;
-            if (MODE == 1) sp.step = pass - 1;
+            if (MODE >= 1) sp.step = pass - 1;
             const bool rec = p.prof && t == 0 && w == (tab ? 1 : SELW);   // one selector records its timeline
             if (rec) p.prof[((size_t)w * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection start
             if (sp.mode != SEL_NONE) {
@@ -686,11 +687,11 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             }
             if (rec) p.prof[((size_t)0 * PROF_PH + hph) * 4 + 3] = wall_clock64();   // selection end (row 0)
             if (committer && t == 0) {
-                if (MODE == 1 && pass + 1 < npass) g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
+                if (MODE >= 1 && pass + 1 < npass) g_put(p.gtok + pass, (uint32_t)max(tok, 0), TAG(hph));
                 if (tok >= 0) select_commit(sp, 0, tok);
                 if (pass + 1 == npass) __hip_atomic_store(p.seq, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (MODE == 1) cur_tok = max(tok, 0);
+            if (MODE >= 1) cur_tok = max(tok, 0);
         }
     }
     }   // passes
@@ -756,15 +757,18 @@ bool persist_resident(int device, int n_ctx, bool cp_frame) {
         default: return false;
     }
     if (!fits(k)) return false;
-    return !cp_frame || fits(reinterpret_cast<const void *>(&k_persist<1, 16>));
+    return !cp_frame || (fits(reinterpret_cast<const void *>(&k_persist<1, 16>)) &&
+                         fits(reinterpret_cast<const void *>(&k_persist<2, 16>)));
 }
 
 bool persist_resident_cp(int device) {
     int n_cu = 0, blocks = 0;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < G) return false;
-    const void *k = reinterpret_cast<const void *>(&k_persist<1, 16>);
-    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds()) != hipSuccess) return false;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, persist_lds()) == hipSuccess && blocks >= 1;
+    for (const void *k : {reinterpret_cast<const void *>(&k_persist<1, 16>), reinterpret_cast<const void *>(&k_persist<2, 16>)}) {
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds()) != hipSuccess) return false;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, persist_lds()) != hipSuccess || blocks < 1) return false;
+    }
+    return true;
 }
 
 void persist_carve(uint8_t *base, PersistParams &p) {
@@ -821,7 +825,9 @@ bool persist_cp_frame(const PersistParams &p, hipStream_t s) {
         set_error("persist_cp_frame: bad parameters");
         return false;
     }
-    return launch_ch<1, 16>(p, s);
+    // MODE 2: the pass inputs as projected f32 rows (1.7B); its own instantiation, so the 0.6B frame's register
+    // allocation does not see the branch (+22 us per frame when it did)
+    return p.xtab ? launch_ch<2, 16>(p, s) : launch_ch<1, 16>(p, s);
 }
 
 }  // namespace q3t
