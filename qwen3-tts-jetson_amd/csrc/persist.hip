@@ -32,6 +32,9 @@ constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgro
 #ifndef Q3T_SEL_HOIST0
 #define Q3T_SEL_HOIST0 1        // talker step: SELW loads the selection's per-slot inputs at launch start
 #endif
+#ifndef Q3T_BPROF
+#define Q3T_BPROF 0             // development timeline: where phase B's mid stamp goes (0 after the q/k norm, 1 after
+#endif                          // the score max, 2 after the P.V reduction; tools/dev/persist_timeline*.py)
 #ifndef Q3T_SEL_HOIST1
 #define Q3T_SEL_HOIST1 1        // code-predictor frame: the selectors load them at launch start
 #endif
@@ -342,6 +345,9 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             nwD = ldf4(Lw.ffn_norm + 4 * t);
             issue_rows_k1024(Lw.gu, gu_row, wg);
             issue_rows_k1024(Lw.gu, gu_row + 16, wu);
+            // talker step: the down rows too (they land while the attention runs, so that D's poll does not wait
+            // for them behind C; 0.570 -> 0.560 ms A/B; no gain in the code-predictor frame, whose B is short)
+            if (MODE == 0) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
         } else {
             {
                 uint32_t u[2];
@@ -350,7 +356,6 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 if (from_tab) { u[0] = traw.x; u[1] = traw.y; }
                 else g_wait<2>(p.gqkv + gi, TAG(ph0 + 5 * l + 0), u, c);
                 PROF(ph0 + 5 * l + 1, 1);
-                nwD = ldf4(Lw.ffn_norm + 4 * t);
                 S.raw[2 * t] = __uint_as_float(u[0]);
                 S.raw[2 * t + 1] = __uint_as_float(u[1]);
             }
@@ -379,6 +384,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 }
             }
             __syncthreads();
+            if (Q3T_BPROF == 0) PROF(ph0 + 5 * l + 1, 3);
             if (has_pos && t < D) {   // KV append at pos (read by later launches only)
                 p.kc[kvo + (size_t)pos * D + t] = f2h(S.kn_s[t]);
                 p.vc[kvo + (size_t)pos * D + t] = f2h(S.vn_s[t]);
@@ -427,6 +433,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 #pragma unroll
             for (int h = 0; h < R; ++h) M[h] = fmaxf(fmaxf(S.wred[0][h], S.wred[1][h]), fmaxf(S.wred[2][h], S.wred[3][h]));
             __syncthreads();
+            if (Q3T_BPROF == 1) PROF(ph0 + 5 * l + 1, 3);
             float pr[NP][R];
 #pragma unroll
             for (int h = 0; h < R; ++h) {
@@ -469,6 +476,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                     if (lane < 16) S.ared[wave][h][li * 8 + e] = a;
                 }
             __syncthreads();
+            if (Q3T_BPROF == 2) PROF(ph0 + 5 * l + 1, 3);
 #pragma unroll
             for (int h = 0; h < R; ++h) Lsum[h] = (S.wred[0][h] + S.wred[1][h]) + (S.wred[2][h] + S.wred[3][h]);
             uint64_t *gout = p.gattn + (size_t)ag * R * (D / 2);
@@ -539,7 +547,9 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             }
         }
         PROF(ph0 + 5 * l + 1, 2);
-        if (att) {   // (the streams of the other workgroups are in flight since A / B)
+        if (att) {   // (the streams of the other workgroups are in flight since A / B; ffn_norm too: a load issued
+                     // after B's input poll would hold the attention body's K/V waits, vmcnt order)
+            nwD = ldf4(Lw.ffn_norm + 4 * t);
             issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
             issue_rows_k1024(Lw.gu, gu_row, wg);
             issue_rows_k1024(Lw.gu, gu_row + 16, wu);
@@ -550,7 +560,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             PROF(ph0 + 5 * l + 2, 0);
             g_wait<4>(p.gattn + 4 * t, TAG(ph0 + 5 * l + 1), u, c);
             PROF(ph0 + 5 * l + 2, 1);
-            issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
+            if (MODE != 0 || att) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
             __syncthreads();
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
             __syncthreads();

@@ -54,4 +54,12 @@ for k, n in ((0, "A"), (3, "D")):
     pre = [np.median(T[:, 5 * l + k, 3] - T[:, 5 * l + k, 1]) for l in range(1, L)]
     post = [np.median(T[:, 5 * l + k, 2] - T[:, 5 * l + k, 3]) for l in range(1, L)]
     print(f"{n} body split: arrive -> after RMS {np.mean(pre):.2f} us, -> published {np.mean(post):.2f} us")
+pre, post = [], []
+for l in range(L):
+    ph = 5 * l + 1
+    ok = (T[:, ph, 3] >= 0) & (T[:, ph, 1] >= 0) & (T[:, ph, 2] >= 0)
+    if ok.any():
+        pre.append(np.median(T[ok, ph, 3] - T[ok, ph, 1]))
+        post.append(np.median(T[ok, ph, 2] - T[ok, ph, 3]))
+print(f"B body split: arrive -> q/k normed + RoPE {np.mean(pre):.2f} us, -> published {np.mean(post):.2f} us")
 eng.close()

@@ -44,6 +44,15 @@ for k in range(5):
             edges.append(np.median(arr[ok]) - T[:, prod, 2][T[:, prod, 2] >= 0].max())
             bodies.append(np.median(pub[ok] - arr[ok]))
     print(f"{names[k]:10s} {np.mean(waits):11.2f} {np.mean(edges):15.2f} {np.mean(bodies):11.2f}")
+pre, post = [], []
+for ps in range(16):
+    for l in range(NL):
+        ph = ps * PPH + 5 * l + 1
+        ok = (T[:, ph, 3] >= 0) & (T[:, ph, 1] >= 0) & (T[:, ph, 2] >= 0)
+        if ok.any():
+            pre.append(np.median(T[ok, ph, 3] - T[ok, ph, 1]))
+            post.append(np.median(T[ok, ph, 2] - T[ok, ph, 3]))
+print(f"B body split: arrive -> q/k normed + RoPE {np.mean(pre):.2f} us, -> published {np.mean(post):.2f} us")
 hd = []
 for ps in range(1, 16):
     h = ps * PPH + 25
