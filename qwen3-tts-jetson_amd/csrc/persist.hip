@@ -340,6 +340,24 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             PROF(ph0 + 5 * l + 0, 2);
         }
         }
+        // code-predictor frame: the non-attention workgroups issue the next QKV (or head) rows here, as soon as A has
+        // consumed the registers, instead of at D: D's input poll then no longer waits behind them (vmcnt order), and
+        // they land while B runs on the attention workgroups (1.364 -> 1.336 ms per frame, A/B).  Not in the talker
+        // step, whose code generation this perturbs (0.558 -> 0.586 ms).
+        if constexpr (MODE >= 1) {
+            if (!att) {
+                if (l + 1 < nl) {
+                    nwA = ldf4(S.layers[l + 1].attn_norm + 4 * t);
+                    issue_rows_k1024(S.layers[l + 1].qkv, w * 16 + grp, wq);
+                } else if (head_here) {
+                    nwA = ldf4(p.out_norm + 4 * t);
+                    issue_rows_k1024(S.heads[pass - 1], w * RPW + min(grp, RPW - 1), wq);
+                } else if (!tab) {
+                    nwA = ldf4(S.layers[0].attn_norm + 4 * t);
+                    issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
+                }
+            }
+        }
         // ================= B: attention (kv group ag, split as)
         if (!att) {
             nwD = ldf4(Lw.ffn_norm + 4 * t);
@@ -584,7 +602,9 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             PROF(ph0 + 5 * l + 3, 0);
             g_wait<4>(p.gx2 + 4 * t, TAG(ph0 + 5 * l + 2), u, c);
             PROF(ph0 + 5 * l + 3, 1);
-            if (l + 1 < nl) {
+            if (MODE >= 1 && !att) {
+                // (issued at A)
+            } else if (l + 1 < nl) {
                 nwA = ldf4(S.layers[l + 1].attn_norm + 4 * t);
                 issue_rows_k1024(S.layers[l + 1].qkv, w * 16 + grp, wq);
             } else if (head_here) {
