@@ -612,39 +612,62 @@ __global__ void __launch_bounds__(256) k_prefill_attn(const PrefillAttnParams p)
     const int u = blockIdx.x, g = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int plen = p.plen, QKV = (p.nH + 2 * p.nKV) * D;
     const size_t head_off = ((size_t)p.slot[u] * p.nKV + g) * p.n_ctx * D;
-    // ---- prologue: vectors (row i, v) with v < R the q heads, v == R the k row, v == R + 1 the v row
-    for (int task = wave; task < plen * (R + 2); task += 4) {
+    // ---- prologue: vectors (row i, v) with v < R the q heads, v == R the k row, v == R + 1 the v row; task
+    // wave + 4k.  Every operand of the wave's tasks is loaded first (one memory round trip instead of one per task:
+    // with one workgroup per kv head the serial loads were ~17 us of an 18 us launch)
+    constexpr int MAXT = (PMAX * (R + 2) + 3) / 4;
+    const int ntask = plen * (R + 2);
+    float xv[MAXT][E], rc[MAXT], rs[MAXT], qw[E], kw[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { qw[e] = p.qn[lane + 64 * e]; kw[e] = p.kn[lane + 64 * e]; }
+#pragma unroll
+    for (int k = 0; k < MAXT; ++k) {
+        const int task = wave + 4 * k;
+        rc[k] = rs[k] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) xv[k][e] = 0.0f;
+        if (task < ntask) {
+            const int i = task / (R + 2), v = task % (R + 2);
+            const float *qkv = p.qkv + (size_t)(u * plen + i) * QKV;
+            const float *src = v == R + 1 ? qkv + (size_t)(p.nH + p.nKV + g) * D : v == R ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
+#pragma unroll
+            for (int e = 0; e < E; ++e) xv[k][e] = src[lane + 64 * e];
+            const float *rope = p.rope + (size_t)i * D;
+            const int ri = D == 128 ? lane : (lane & 31);
+            rc[k] = rope[2 * ri];
+            rs[k] = rope[2 * ri + 1];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < MAXT; ++k) {
+        const int task = wave + 4 * k;
+        if (task >= ntask) break;
         const int i = task / (R + 2), v = task % (R + 2);
-        const float *qkv = p.qkv + (size_t)(u * plen + i) * QKV;
         if (v == R + 1) {
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const float y = f16r(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
+                const float y = f16r(xv[k][e]);
                 v_s[i][lane + 64 * e] = y;
                 p.vc[head_off + (size_t)i * D + lane + 64 * e] = f2h(y);
             }
             continue;
         }
         const bool isk = v == R;
-        const float *src = isk ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
-        const float *w = isk ? p.kn : p.qn;
-        const float *rope = p.rope + (size_t)i * D;
         float x[E];
         double ss = 0.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { x[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(x[e], x[e]); }
+        for (int e = 0; e < E; ++e) { x[e] = xv[k][e]; ss += (double)__fmul_rn(x[e], x[e]); }
         ss = wave_sum_d(ss);
         const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
 #pragma unroll
-        for (int e = 0; e < E; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+        for (int e = 0; e < E; ++e) x[e] = (x[e] * scale) * (isk ? kw[e] : qw[e]);
         float y[E];
         if constexpr (D == 128) {
-            const float c = rope[2 * lane], sn = rope[2 * lane + 1];
+            const float c = rc[k], sn = rs[k];
             y[0] = opaque(opaque(x[0] * c) - opaque(x[1] * sn));
             y[1] = opaque(opaque(x[0] * sn) + opaque(x[1] * c));
         } else {
-            const int ii = lane & 31;
-            const float c = rope[2 * ii], sn = rope[2 * ii + 1];
+            const float c = rc[k], sn = rs[k];
             const float other = __shfl_xor(x[0], 32, 64);
             y[0] = lane < 32 ? x[0] * c - other * sn : other * sn + x[0] * c;
         }

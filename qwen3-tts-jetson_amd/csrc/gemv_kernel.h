@@ -302,6 +302,8 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
                         *reinterpret_cast<uint4 *>(xs + (size_t)b * Kp + k) = (b < nb && k < K) ? xh[b][t] : make_uint4(0, 0, 0, 0);
                 }
         } else {
+            // unrolled over the tile's rows: every row's loads are in flight before the first LDS store
+#pragma unroll
             for (int b = 0; b < BT; ++b) {
                 uint16_t *xr = xs + (size_t)b * Kp;
                 const int src_row = b < nb ? (p.x_idx ? p.x_idx[b0 + b] : b0 + b) : 0;
@@ -313,12 +315,15 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
             }
         }
     } else {
+        // rows bb + XB.. are loaded while rows bb.. reduce (one row's load latency per tile instead of one per row)
+        float4 rn[BT > XB ? XB : 1][4];
         for (int bb = 0; bb < BT; bb += XB) {
-            if (bb > 0)
+            if (BT > XB && bb + XB < BT)
 #pragma unroll
                 for (int q = 0; q < XB; ++q) {
-                    if constexpr (kGather) issue_x_gather<NT>(p, b0 + min(bb + q, nb - 1), r[q], kSelG ? sel_tok[min(bb + q, nb - 1)] : -1);
-                    else issue_x_plain(p, b0 + min(bb + q, nb - 1), r[q]);
+                    const int b = bb + XB + q;
+                    if constexpr (kGather) issue_x_gather<NT>(p, b0 + min(b, nb - 1), rn[q], kSelG ? sel_tok[min(b, nb - 1)] : -1);
+                    else issue_x_plain(p, b0 + min(b, nb - 1), rn[q]);
                 }
 #pragma unroll
             for (int q = 0; q < XB; ++q) mask_x(K, bb + q < nb, r[q]);
@@ -399,6 +404,12 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
                     h.y = (uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16);
                     *reinterpret_cast<uint2 *>(xr + k) = h;
                 }
+            }
+            if constexpr (BT > XB) {
+#pragma unroll
+                for (int q = 0; q < XB; ++q)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) r[q][t] = rn[q][t];
             }
         }
     }
