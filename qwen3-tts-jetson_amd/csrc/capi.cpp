@@ -99,7 +99,8 @@ int q3t_ctx_create_shared(const char *tts_gguf, const char *tokenizer_gguf, int 
     q3t_ctx *c = new q3t_ctx();
     if (!q3t::comm_init(&c->comm, world, rank, id, device) ||
         !c->engine.load(tts_gguf, tokenizer_gguf ? tokenizer_gguf : "", device, max_slots, max_ctx, rank != 0) ||
-        !q3t::comm_bcast_arenas(c->comm, c->engine.weight_arenas(), c->engine.stream())) {
+        !q3t::comm_bcast_arenas(c->comm, c->engine.weight_arenas(), c->engine.stream()) ||
+        (rank != 0 && !c->engine.finish_weights())) {
         delete c;
         return Q3T_ERR;
     }

@@ -6,8 +6,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <condition_variable>
 #include <mutex>
-#include <shared_mutex>
 
 #include "devlock.h"
 #include "speaker.h"
@@ -18,7 +19,40 @@ namespace q3t {
 Engine::Engine() = default;
 
 namespace {
-std::shared_mutex g_device_rw[64];
+// writer-preferring reader/writer lock: once an exclusive holder waits, no new shared hold is granted, so a
+// single-slot generate is never starved by overlapping shared holds (vocoder + batched contexts in a serving loop;
+// glibc's std::shared_mutex prefers readers)
+class WPLock {
+public:
+    void lock() {
+        std::unique_lock<std::mutex> g(m_);
+        ++waiting_w_;
+        cv_.wait(g, [&] { return !writer_ && readers_ == 0; });
+        --waiting_w_;
+        writer_ = true;
+    }
+    void unlock() {
+        { std::lock_guard<std::mutex> g(m_); writer_ = false; }
+        cv_.notify_all();
+    }
+    void lock_shared() {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return !writer_ && waiting_w_ == 0; });
+        ++readers_;
+    }
+    void unlock_shared() {
+        bool wake;
+        { std::lock_guard<std::mutex> g(m_); wake = --readers_ == 0; }
+        if (wake) cv_.notify_all();
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int readers_ = 0, waiting_w_ = 0;
+    bool writer_ = false;
+};
+WPLock g_device_rw[64];
 thread_local int t_device_depth[64];
 }  // namespace
 
@@ -48,6 +82,7 @@ Options Options::from_env() {
     o.persist_cp = env_flag("Q3T_PERSIST_CP", true);
     o.cp_fused_attn = env_flag("Q3T_CP_FUSED_ATTN", true);
     o.cp_qkv_table = env_flag("Q3T_CP_QKV_TABLE", true);
+    o.cp_roles = env_flag("Q3T_CP_ROLES", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
     o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
@@ -88,6 +123,13 @@ T *Engine::dalloc(size_t n) {
         return nullptr;
     }
     return static_cast<T *>(p);
+}
+
+void Engine::dfree(void *p) {
+    if (!p) return;
+    auto it = std::find(allocs_.begin(), allocs_.end(), p);
+    if (it != allocs_.end()) allocs_.erase(it);
+    hipFree(p);
 }
 
 // the pinned / device scratch of generate() and generate_queue(), kept across calls: a per-call hipFree or
@@ -365,8 +407,9 @@ bool Engine::alloc_state() {
     cpx_ = dalloc<float>((size_t)S * c_.cp_hidden);
     cp_in1_ = dalloc<float>((size_t)S * H);
     cp_logits_ = dalloc<float>((size_t)S * c_.cp_vocab);
-    part_ = dalloc<float>((size_t)S * c_.n_heads * max_splits * (D + 2));
-    ticket_ = dalloc<unsigned>((size_t)S * c_.n_kv);
+    // (the code-predictor stack runs attn_decode on these too: sized for the wider of the two head layouts)
+    part_ = dalloc<float>((size_t)S * std::max(c_.n_heads, c_.cp_heads) * max_splits * (D + 2));
+    ticket_ = dalloc<unsigned>((size_t)S * std::max(c_.n_kv, c_.cp_kv));
     sel_ticket_ = dalloc<unsigned>((size_t)S);
     attn_ = dalloc<uint16_t>((size_t)S * std::max(c_.n_heads, c_.cp_heads) * D);
     hmlp_ = dalloc<uint16_t>((size_t)S * std::max(c_.inter, c_.cp_inter));
@@ -430,6 +473,7 @@ bool Engine::setup_persist() {
     // every instantiation must fit one workgroup per CU on this device (occupancy query with its LDS request)
     persist_ = persist_ && persist_resident(device_, max_ctx_, cp_ok);
     persist_cp_ = cp_ok && persist_resident_cp(device_);
+    cp_roles_ = persist_cp_ && opt_.cp_roles && c_.cp_layers == 5 && persist_cp_roles_resident(device_);
     if (!persist_ && !persist_cp_) return true;
     pstate_ = dalloc<uint8_t>(persist_state_bytes());
     if (!pstate_) { set_error("device allocation failed"); return false; }
@@ -452,16 +496,32 @@ bool Engine::setup_persist() {
         Q3T_HIP(hipMemcpy(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
         std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
         Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
-        // (a context for few slots: the batched serving contexts do not pay the table's 520 MB; their rare 1-slot calls
-        // run the persistent frame without it)
-        if (c_.has_mtp && !build_cp_proj_table()) return false;
-        if (opt_.cp_qkv_table && max_slots_ <= 4 && !build_cp_qkv_table()) return false;
+        // the per-token tables are computed from the weights: a receiving context (replica, non-root rank) builds
+        // them once its arena has been filled (finish_weights, after copy_weights_from / the RCCL broadcast)
+        if (!wa_.recv && !build_persist_tables()) return false;
     }
     // (pstate_ was zeroed on the context stream by dalloc)
 #ifdef Q3T_DEV
     if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
 #endif
     return true;
+}
+
+// the persistent code-predictor frame's per-token tables (a context for few slots only: the batched serving contexts
+// do not pay the QKV table's 520 MB; their rare 1-slot calls run the persistent frame without it)
+bool Engine::build_persist_tables() {
+    if (!persist_cp_ || tables_built_) return true;
+    if (c_.has_mtp && !build_cp_proj_table()) return false;
+    if (opt_.cp_qkv_table && max_slots_ <= 4 && !build_cp_qkv_table()) return false;
+    tables_built_ = true;
+    return true;
+}
+
+bool Engine::finish_weights() {
+    DeviceLock lk(false, device_);
+    Q3T_HIP(hipSetDevice(device_));
+    Q3T_HIP(hipStreamSynchronize(stream_));   // the arena fill (copy or broadcast) ran on this stream
+    return build_persist_tables();
 }
 
 // Layer 0 of code-predictor passes 1..15 starts from a table row (codec_embd / code_pred.codec_embd[p-2]), so its
@@ -496,6 +556,7 @@ bool Engine::build_cp_qkv_table() {
         row0 += V;
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
+    dfree(iota);
     return true;
 }
 
@@ -529,6 +590,8 @@ bool Engine::build_cp_proj_table() {
         row0 += V;
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
+    dfree(rowbuf);
+    dfree(iota);
     return true;
 }
 
@@ -542,7 +605,10 @@ bool Engine::persist_recover() {
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
-    persist_ = persist_cp_ = false;
+    persist_ = persist_cp_ = cp_roles_ = false;
+    dfree(cp_qkvtab_);   // the tables serve only the persistent frame
+    dfree(cp_projtab_);
+    cp_qkvtab_ = cp_projtab_ = nullptr;
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
     // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
     cp_fused_attn_ = false;
@@ -883,6 +949,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         p.qkvtab = cp_qkvtab_;
         p.sel = select_spec(SEL_CP, gp_, 0, 0);
         p.prof = pprof_;
+        if (cp_roles_ && p.qkvtab && !p.xtab) return persist_cp_roles(p, s);
         return persist_cp_frame(p, s);
     }
     const bool fsel_all = fused_select_ && !use_mm(S);
@@ -1221,7 +1288,7 @@ bool Engine::copy_weights_from(Engine &src) {
         if (a[i]->used) Q3T_HIP(hipMemcpyPeerAsync(a[i]->base, device_, b[i]->base, src.device_, a[i]->used, stream_));
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
-    return true;
+    return build_persist_tables();   // the tables derived from the weights, now that they are in place
 }
 
 bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,

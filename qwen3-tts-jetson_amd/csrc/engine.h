@@ -61,6 +61,7 @@ struct PLayerW;
 struct Options {
     bool persist = true, persist_cp = true, cp_fused_attn = true, fused_select = true, defer_cp_select = true;
     bool cp_qkv_table = true;   // Q3T_CP_QKV_TABLE: the persistent code-predictor frame reads layer 0's QKV rows from a table
+    bool cp_roles = true;       // Q3T_CP_ROLES: that frame on role-specialised workgroups (persist_cp.hip)
     bool attn_split = false;
     unsigned persist_fault_at = 0;
     int poll_every = 16;   // frames between done-flag polls
@@ -111,6 +112,9 @@ public:
                         const GenParams &gp, int32_t *codes, int *n_frames, int max_active);
     // fill this context's weight arenas (laid out with recv_weights) from another context's, device to device
     bool copy_weights_from(Engine &src);
+    // after the weight arenas of a receiving context were filled by a broadcast: build what is derived from the weights
+    // (the persistent code-predictor frame's per-token tables)
+    bool finish_weights();
 
     // ---- stage entry points (host buffers) used by the parity tests
     bool talker_prefill(int n_utt, int n_rows, const float *embd, int family_slots, float *hidden, float *logits);
@@ -212,6 +216,7 @@ private:
     std::vector<void *> allocs_;
     WeightArena wa_;
     template <class T> T *dalloc(size_t n);
+    void dfree(void *p);   // free a dalloc allocation early (one-off build buffers)
 
     // weights
     std::vector<DevLayer> L_, CP_;
@@ -262,7 +267,10 @@ private:
     float *cp_projtab_ = nullptr;        // 1.7B: mtp_proj . f16(table row) + b per table token (f32, code-predictor space)
     bool build_cp_proj_table();
     bool build_cp_qkv_table();
+    bool build_persist_tables();
+    bool tables_built_ = false;
     bool persist_cp_ = false;
+    bool cp_roles_ = false;    // the 1-slot code-predictor frame runs persist_cp.hip
     uint8_t *pstate_ = nullptr;
     uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline
 

@@ -75,6 +75,10 @@ bool persist_talker_step(const PersistParams &p, hipStream_t s);
 // tables, kc/vc = the 16-position code-predictor caches, heads = lm_head[0..14], out_norm, logits [2048],
 // sel = SEL_CP (step set per pass)
 bool persist_cp_frame(const PersistParams &p, hipStream_t s);
+// the same frame with role-specialised workgroups (persist_cp.hip): 0.6B shapes with the layer-0 QKV table
+// (p.qkvtab) and 5 code-predictor layers; bit-identical to persist_cp_frame and the launch-per-op graph
+bool persist_cp_roles(const PersistParams &p, hipStream_t s);
+bool persist_cp_roles_resident(int device);
 int persist_chunk(int n_ctx);                    // positions per attention split workgroup
 size_t persist_qkv_table_rows();                 // rows of PersistParams::qkvtab (3072 + 14 * 2048)
 

@@ -10,6 +10,7 @@
 //   head: RMSNorm(output_norm) + codec head 12 rows / wg, CB0 selection by the last workgroup (fused head select)
 // Reference semantics: src/tts_transformer.cpp:1376-1512 (build_step_graph), :2416-2499 (CB0 processing).
 #include "persist.h"
+#include "persist_dev.h"
 #include "select.h"
 
 #include <algorithm>
@@ -25,7 +26,6 @@ constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, IN
 constexpr int G = 256;          // workgroups (one per CU)
 constexpr int MAXSPLIT = G / NKV;
 constexpr int R = NH / NKV;     // q heads per kv head
-constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
 constexpr int MAXL = 32;        // layers (pointer table in LDS)
 constexpr int PSLOT = 264;      // granules per attention split partial: acc [2][128], m [2], l [2], pad to 4
 constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgroup only at 32 splits)
@@ -35,82 +35,23 @@ constexpr int SELW = G - 1;     // the selecting workgroup (an attention workgro
 #ifndef Q3T_BPROF
 #define Q3T_BPROF 0             // development timeline: where phase B's mid stamp goes (0 after the q/k norm, 1 after
 #endif                          // the score max, 2 after the P.V reduction; tools/dev/persist_timeline*.py)
+#ifndef Q3T_NOSTREAM
+#define Q3T_NOSTREAM 0          // development experiment: weight rows streamed only for the first layer (timing only)
+#endif
 #ifndef Q3T_SEL_HOIST1
 #define Q3T_SEL_HOIST1 1        // code-predictor frame: the selectors load them at launch start
 #endif
 
-template <class V>
-__device__ __forceinline__ V ldgv(const void *p) {
-    typedef const __attribute__((address_space(1))) V gV;
-    return *(gV *)(p);
-}
-__device__ __forceinline__ uint4 ld16(const void *p) {
-    const u32x4_t v = ldgv<u32x4_t>(p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float4 ldf4(const float *p) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v v = ldgv<f4v>(p);
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint2 ld8(const void *p) {
-    typedef unsigned u2v __attribute__((ext_vector_type(2)));
-    const u2v v = ldgv<u2v>(p);
-    return make_uint2(v.x, v.y);
-}
-
-// ---------------------------------------------------------------- granules
-__device__ __forceinline__ void g_put(uint64_t *p, uint32_t payload, uint32_t tag) {
-    __hip_atomic_store(p, ((uint64_t)tag << 32) | payload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t g_ld(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two agent-scope (L1-bypassing) 8-B loads
-    uint64_t *q = reinterpret_cast<uint64_t *>(const_cast<uint16_t *>(p));
-    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-}
-
-struct Ctl {
-    unsigned *err;
-    bool abort;
-};
-
-// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
-// workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
-template <int N>
-__device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
-    uint64_t v[N];
-    unsigned it = 0;
-    while (true) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) v[i] = g_ld(base + i);
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < N; ++i) ok &= (uint32_t)(v[i] >> 32) == tag;
-        if (ok || c.abort) break;
-        ++it;
-        if ((it & 255u) == 0) {
-            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
-                c.abort = true;
-                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-#ifndef Q3T_POLL_SLEEP
-#define Q3T_POLL_SLEEP 1
-#endif
-        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];
-}
-
-__device__ __forceinline__ float4 f4_of(const uint32_t (&u)[4]) {
-    return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
-}
+using pdev::ldgv;
+using pdev::ld16;
+using pdev::ldf4;
+using pdev::ld8;
+using pdev::g_put;
+using pdev::g_ld;
+using pdev::ld16_sc1;
+using pdev::Ctl;
+using pdev::g_wait;
+using pdev::f4_of;
 
 struct Lds {
     uint16_t xs[INTER];          // f16 activation tile of the current phase
@@ -256,6 +197,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
     if (MODE >= 1) pos = pass;
     for (int l = 0; l < nl; ++l) {
         const PLayerW Lw = S.layers[l];
+        const bool st = !(Q3T_NOSTREAM && (pass > 0 || l > 0));
         const size_t kvo = (size_t)l * p.kv_layer + (size_t)ag * p.n_ctx * D;
         const bool from_tab = tab && l == 0 && pass >= 1;   // layer 0's QKV rows come from the table
         uint2 traw = make_uint2(0, 0);                      // from_tab: this thread's two raw QKV values
@@ -324,7 +266,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             rp[0] = p.rope[(size_t)pos * D + 2 * lane];
             rp[1] = p.rope[(size_t)pos * D + 2 * lane + 1];
         }
-        if (!att) issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
+        if (!att && st) issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
         __syncthreads();
         *reinterpret_cast<float4 *>(S.xr + 4 * t) = x;
         if (!from_tab) {
@@ -345,7 +287,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         // they land while B runs on the attention workgroups (1.364 -> 1.336 ms per frame, A/B).  Not in the talker
         // step, whose code generation this perturbs (0.558 -> 0.586 ms).
         if constexpr (MODE >= 1) {
-            if (!att) {
+            if (!att && st) {
                 if (l + 1 < nl) {
                     nwA = ldf4(S.layers[l + 1].attn_norm + 4 * t);
                     issue_rows_k1024(S.layers[l + 1].qkv, w * 16 + grp, wq);
@@ -361,11 +303,11 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         // ================= B: attention (kv group ag, split as)
         if (!att) {
             nwD = ldf4(Lw.ffn_norm + 4 * t);
-            issue_rows_k1024(Lw.gu, gu_row, wg);
-            issue_rows_k1024(Lw.gu, gu_row + 16, wu);
+            if (st) issue_rows_k1024(Lw.gu, gu_row, wg);
+            if (st) issue_rows_k1024(Lw.gu, gu_row + 16, wu);
             // talker step: the down rows too (they land while the attention runs, so that D's poll does not wait
             // for them behind C; 0.570 -> 0.560 ms A/B; no gain in the code-predictor frame, whose B is short)
-            if (MODE == 0) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
+            if (MODE == 0 && st) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
         } else {
             {
                 uint32_t u[2];
@@ -568,9 +510,9 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
         if (att) {   // (the streams of the other workgroups are in flight since A / B; ffn_norm too: a load issued
                      // after B's input poll would hold the attention body's K/V waits, vmcnt order)
             nwD = ldf4(Lw.ffn_norm + 4 * t);
-            issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
-            issue_rows_k1024(Lw.gu, gu_row, wg);
-            issue_rows_k1024(Lw.gu, gu_row + 16, wu);
+            if (st) issue_rows_ks4<4>(Lw.o, NH * D, w * 4 + grp4, wo);
+            if (st) issue_rows_k1024(Lw.gu, gu_row, wg);
+            if (st) issue_rows_k1024(Lw.gu, gu_row + 16, wu);
         }
         // ================= C: O-proj + residual -> x'
         {
@@ -578,7 +520,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             PROF(ph0 + 5 * l + 2, 0);
             g_wait<4>(p.gattn + 4 * t, TAG(ph0 + 5 * l + 1), u, c);
             PROF(ph0 + 5 * l + 2, 1);
-            if (MODE != 0 || att) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
+            if ((MODE != 0 || att) && st) issue_rows_ks4<6>(Lw.down, INTER, w * 4 + grp4, wd);
             __syncthreads();
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
             __syncthreads();
@@ -602,7 +544,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
             PROF(ph0 + 5 * l + 3, 0);
             g_wait<4>(p.gx2 + 4 * t, TAG(ph0 + 5 * l + 2), u, c);
             PROF(ph0 + 5 * l + 3, 1);
-            if (MODE >= 1 && !att) {
+            if ((MODE >= 1 && !att) || !st) {
                 // (issued at A)
             } else if (l + 1 < nl) {
                 nwA = ldf4(S.layers[l + 1].attn_norm + 4 * t);
@@ -684,7 +626,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 #pragma unroll
         for (int tt = 0; tt < 8; ++tt) wh[tt] = wq[tt];
         if (MODE >= 1 && pass + 1 < npass) {
-            if (!tab) {
+            if (!tab && Q3T_NOSTREAM == 0) {
                 nwA = ldf4(S.layers[0].attn_norm + 4 * t);
                 issue_rows_k1024(S.layers[0].qkv, w * 16 + grp, wq);
             }

@@ -1,0 +1,112 @@
+// persist_dev.h — device helpers shared by the persistent kernels (persist.hip: the talker step and the 1.7B /
+// fallback code-predictor frame; persist_cp.hip: the role-specialised code-predictor frame): global loads that never
+// lower to flat loads, the {payload, tag} granule hand-off (one 8-byte agent-scope store, polled with agent-scope
+// loads until every tag matches; MI355X_MICROARCH.md hand-off rows), the bounded wait and the RMSNorm prologue.
+#pragma once
+#include "kernels.h"
+
+namespace q3t {
+namespace pdev {
+
+constexpr unsigned SPIN_LIMIT = 1u << 21;   // polls before a hand-off wait gives up (sets *err)
+
+template <class V>
+__device__ __forceinline__ V ldgv(const void *p) {
+    typedef const __attribute__((address_space(1))) V gV;
+    return *(gV *)(p);
+}
+__device__ __forceinline__ uint4 ld16(const void *p) {
+    const u32x4_t v = ldgv<u32x4_t>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 ldf4(const float *p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = ldgv<f4v>(p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld8(const void *p) {
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    const u2v v = ldgv<u2v>(p);
+    return make_uint2(v.x, v.y);
+}
+
+// ---------------------------------------------------------------- granules
+__device__ __forceinline__ void g_put(uint64_t *p, uint32_t payload, uint32_t tag) {
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | payload, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t g_ld(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 ld16_sc1(const uint16_t *p) {   // 16 B as two agent-scope (L1-bypassing) 8-B loads
+    uint64_t *q = reinterpret_cast<uint64_t *>(const_cast<uint16_t *>(p));
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
+struct Ctl {
+    unsigned *err;
+    bool abort;
+};
+
+// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
+// workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
+template <int N>
+__device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
+    uint64_t v[N];
+    unsigned it = 0;
+    while (true) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = g_ld(base + i);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < N; ++i) ok &= (uint32_t)(v[i] >> 32) == tag;
+        if (ok || c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                c.abort = true;
+                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+#ifndef Q3T_POLL_SLEEP
+#define Q3T_POLL_SLEEP 1
+#endif
+        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];
+}
+
+__device__ __forceinline__ float4 f4_of(const uint32_t (&u)[4]) {
+    return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+}
+
+
+__device__ __forceinline__ double block_sum_d(double v, double *scr) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_sum_d(v);
+    __syncthreads();
+    if (lane == 0) scr[wave] = v;
+    __syncthreads();
+    return (scr[0] + scr[1]) + (scr[2] + scr[3]);
+}
+
+// RMSNorm of the f32 row held as thread t's elements 4t..4t+3 (K = 1024) -> f16 tile xs; optional f32 side output
+// (gemv.hip prologue: double sums, (x * scale) * w, f16 rounding)
+__device__ __forceinline__ void rms_to_f16(float4 x, float4 w, float eps, uint16_t *xs, double *dscr, float *side) {
+    const int t = threadIdx.x;
+    double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);
+    ss = block_sum_d(ss, dscr);
+    const float scale = 1.0f / sqrtf((float)(ss / 1024) + eps);
+    const float y0 = (x.x * scale) * w.x, y1 = (x.y * scale) * w.y, y2 = (x.z * scale) * w.z, y3 = (x.w * scale) * w.w;
+    if (side) *reinterpret_cast<float4 *>(side + 4 * t) = make_float4(y0, y1, y2, y3);
+    uint2 h;
+    h.x = (uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16);
+    h.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
+    *reinterpret_cast<uint2 *>(xs + 4 * t) = h;
+}
+
+}  // namespace pdev
+}  // namespace q3t

@@ -149,8 +149,17 @@ def test_full17_persistent_code_predictor_bit_exact():
                 assert np.array_equal(a, b), (frame, T, a, b)
         toks = prompt("full17")
         kw = dict(speakers=[np.zeros(H, np.float32)], max_len=16, temperature=0.9, top_k=50, seed=5, force_frames=16)
-        assert np.array_equal(eng.generate([toks], **kw)[0], ref.generate([toks], **kw)[0])
+        want = ref.generate([toks], **kw)[0]
+        assert np.array_equal(eng.generate([toks], **kw)[0], want)
         assert eng.persist_status() == 0
+        # a 1-slot replica (weights copied device to device after its layout) builds its projected table from the
+        # copied weights, not from the empty arena: same codes as its source
+        rep = eng.replica(0, 1, 64)
+        try:
+            assert rep.persist_status() == 0
+            assert np.array_equal(rep.generate([toks], **kw)[0], want)
+        finally:
+            rep.close()
     finally:
         eng.close()
         ref.close()

@@ -98,6 +98,25 @@ def test_replica_decodes_identically(eng):
         rep.close()
 
 
+def test_full_replica_persistent_frame_matches_source():
+    """a 1-slot replica of the full model runs the persistent code-predictor frame with the layer-0 QKV table; the table
+    is derived from the weights, so it must be built after the device-to-device copy (not from the empty arena at
+    layout time): codes identical to the source context's at T = 0.9"""
+    import q3t
+    tts, _ = synth_dir("full")
+    src = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=64)
+    rep = src.replica(0, 1, 64)
+    try:
+        assert src.persist_status() == 0 and rep.persist_status() == 0
+        H = src.cfg["hidden"]
+        kw = dict(speakers=[np.zeros(H, np.float32)], max_len=12, temperature=0.9, top_k=50, seed=11, force_frames=12)
+        toks = prompt("full")
+        np.testing.assert_array_equal(rep.generate([toks], **kw)[0], src.generate([toks], **kw)[0])
+    finally:
+        rep.close()
+        src.close()
+
+
 def test_shared_single_rank_rccl():
     import q3t
     tts, tok = synth_dir("tiny")

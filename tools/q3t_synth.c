@@ -65,6 +65,12 @@ static const cfg_t CFG_FULL = {
     "full", 151936, 2048, 1024, 28, 16, 8, 128, 3072, 3072, 16,
     5, 2048, 1e-6f, 1000000.0f, 151672, 151673, 151671,
     2048, 256, 512, 1024, 8, 16, 1024, 1536, 2, 4, {8, 5, 4, 3}};
+// the full model's widths with its first 5 talker layers only: the generator is counter-based per tensor name, so
+// these are exactly the full model's first 5 layers, which tests/golden/talker5_full.npz pins (5 harness layer slots)
+static const cfg_t CFG_FULL5 = {
+    "full5", 151936, 2048, 1024, 5, 16, 8, 128, 3072, 3072, 16,
+    5, 2048, 1e-6f, 1000000.0f, 151672, 151673, 151671,
+    2048, 256, 512, 1024, 8, 16, 1024, 1536, 2, 4, {8, 5, 4, 3}};
 static const cfg_t CFG_TINY1 = {
     "tiny1", 1024, 128, 256, 1, 4, 2, 64, 512, 3072, 16,
     1, 2048, 1e-6f, 1000000.0f, 1001, 1002, 1000,
@@ -624,9 +630,10 @@ static int write_gguf(const char *path, const kv_t *kvs, int nkv, uint64_t seed)
 }
 
 int main(int argc, char **argv) {
-    if (argc < 3) { fprintf(stderr, "usage: %s full|tiny|tiny1|tiny17|full17 <out_dir> [seed]\n", argv[0]); return 2; }
+    if (argc < 3) { fprintf(stderr, "usage: %s full|full5|tiny|tiny1|tiny17|full17 <out_dir> [seed]\n", argv[0]); return 2; }
     const cfg_t *c = strcmp(argv[1], "full") == 0 ? &CFG_FULL : strcmp(argv[1], "tiny") == 0 ? &CFG_TINY : strcmp(argv[1], "tiny1") == 0 ? &CFG_TINY1
-                   : strcmp(argv[1], "tiny17") == 0 ? &CFG_TINY17 : strcmp(argv[1], "full17") == 0 ? &CFG_FULL17 : NULL;
+                   : strcmp(argv[1], "tiny17") == 0 ? &CFG_TINY17 : strcmp(argv[1], "full17") == 0 ? &CFG_FULL17
+                   : strcmp(argv[1], "full5") == 0 ? &CFG_FULL5 : NULL;
     if (!c) { fprintf(stderr, "unknown config %s\n", argv[1]); return 2; }
     uint64_t seed = argc > 3 ? strtoull(argv[3], NULL, 0) : 0x51E3775ull;
     g_usage = argc > 4 && strcmp(argv[4], "usage") == 0;
