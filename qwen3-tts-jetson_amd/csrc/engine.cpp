@@ -83,6 +83,7 @@ Options Options::from_env() {
     o.cp_fused_attn = env_flag("Q3T_CP_FUSED_ATTN", true);
     o.cp_qkv_table = env_flag("Q3T_CP_QKV_TABLE", true);
     o.cp_roles = env_flag("Q3T_CP_ROLES", true);
+    o.tk_roles = env_flag("Q3T_TK_ROLES", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
     o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
@@ -474,6 +475,8 @@ bool Engine::setup_persist() {
     persist_ = persist_ && persist_resident(device_, max_ctx_, cp_ok);
     persist_cp_ = cp_ok && persist_resident_cp(device_);
     cp_roles_ = persist_cp_ && opt_.cp_roles && c_.cp_layers == 5 && persist_cp_roles_resident(device_);
+    tk_roles_ = persist_ && opt_.tk_roles && persist_chunk(max_ctx_) == 64 && persist_tk_roles_supported(max_ctx_) &&
+                persist_tk_roles_resident(device_, max_ctx_);
     if (!persist_ && !persist_cp_) return true;
     pstate_ = dalloc<uint8_t>(persist_state_bytes());
     if (!pstate_) { set_error("device allocation failed"); return false; }
@@ -502,7 +505,7 @@ bool Engine::setup_persist() {
     }
     // (pstate_ was zeroed on the context stream by dalloc)
 #ifdef Q3T_DEV
-    if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)256 * PROF_PH * 4);
+    if (std::getenv("Q3T_PERSIST_PROF")) pprof_ = dalloc<uint64_t>((size_t)PROF_WG * PROF_PH * 4);
 #endif
     return true;
 }
@@ -605,7 +608,7 @@ bool Engine::persist_recover() {
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
-    persist_ = persist_cp_ = cp_roles_ = false;
+    persist_ = persist_cp_ = cp_roles_ = tk_roles_ = false;
     dfree(cp_qkvtab_);   // the tables serve only the persistent frame
     dfree(cp_projtab_);
     cp_qkvtab_ = cp_projtab_ = nullptr;
@@ -620,7 +623,7 @@ bool Engine::persist_recover() {
 bool Engine::debug_read(int which, void *dst, size_t bytes) {
     if (which == 5 && pprof_) {   // persistent-step timeline (dev)
         Q3T_HIP(hipStreamSynchronize(stream_));
-        Q3T_HIP(hipMemcpy(dst, pprof_, std::min<size_t>(bytes, (size_t)256 * PROF_PH * 4 * 8), hipMemcpyDeviceToHost));
+        Q3T_HIP(hipMemcpy(dst, pprof_, std::min<size_t>(bytes, (size_t)PROF_WG * PROF_PH * 4 * 8), hipMemcpyDeviceToHost));
         return true;
     }
     if (which == 4 && !pstate_) {   // launch-per-phase attention partial buffer (dev dumps)
@@ -881,6 +884,7 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         p.head = codec_head_; p.out_norm = out_norm_; p.hidden = hidden_; p.logits = logits_;
         if (select_next) p.sel = select_spec(SEL_CB0, gp_, 1, 0);
         p.prof = pprof_;
+        if (tk_roles_) return persist_tk_roles(p, s);
         return persist_talker_step(p, s);
     }
     StackInput in0;

@@ -62,6 +62,7 @@ struct Options {
     bool persist = true, persist_cp = true, cp_fused_attn = true, fused_select = true, defer_cp_select = true;
     bool cp_qkv_table = true;   // Q3T_CP_QKV_TABLE: the persistent code-predictor frame reads layer 0's QKV rows from a table
     bool cp_roles = true;       // Q3T_CP_ROLES: that frame on role-specialised workgroups (persist_cp.hip)
+    bool tk_roles = true;       // Q3T_TK_ROLES: the 1-slot talker step on role-specialised workgroups (persist_tk.hip)
     bool attn_split = false;
     unsigned persist_fault_at = 0;
     int poll_every = 16;   // frames between done-flag polls
@@ -271,6 +272,7 @@ private:
     bool tables_built_ = false;
     bool persist_cp_ = false;
     bool cp_roles_ = false;    // the 1-slot code-predictor frame runs persist_cp.hip
+    bool tk_roles_ = false;    // the 1-slot talker step runs persist_tk.hip
     uint8_t *pstate_ = nullptr;
     uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline
 

@@ -15,6 +15,7 @@
 namespace q3t {
 
 constexpr int PROF_PH = 448;   // timeline phases recorded per workgroup (5 per layer + head)
+constexpr int PROF_WG = 512;   // timeline rows (workgroups; persist_tk.hip runs up to 505)
 
 struct PLayerW {
     const uint16_t *qkv, *o, *gu, *down;
@@ -56,6 +57,7 @@ struct PersistParams {
     // place of the f16 table rows (gs.tabs), same row order as qkvtab; x_in is then the projected pass-0 input
     const float *xtab = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
+    int roles_split = 0;           // persist_tk.hip: attention splits per kv group (set by the launcher)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;
 };
 
@@ -79,6 +81,11 @@ bool persist_cp_frame(const PersistParams &p, hipStream_t s);
 // (p.qkvtab) and 5 code-predictor layers; bit-identical to persist_cp_frame and the launch-per-op graph
 bool persist_cp_roles(const PersistParams &p, hipStream_t s);
 bool persist_cp_roles_resident(int device);
+// the talker step with role-specialised workgroups (persist_tk.hip): the 0.6B shapes, contexts up to 64 x 4 x 3
+// positions; bit-identical to persist_talker_step and the launch-per-op graph
+bool persist_tk_roles(const PersistParams &p, hipStream_t s);
+bool persist_tk_roles_supported(int n_ctx);
+bool persist_tk_roles_resident(int device, int n_ctx);
 int persist_chunk(int n_ctx);                    // positions per attention split workgroup
 size_t persist_qkv_table_rows();                 // rows of PersistParams::qkvtab (3072 + 14 * 2048)
 

@@ -75,7 +75,7 @@ struct Ctx {
 
 #define PROF(ph, k)                                                                                           \
     do {                                                                                                      \
-        if (X.p.prof && threadIdx.x == 0) X.p.prof[((size_t)blockIdx.x * PROF_PH + (ph)) * 4 + (k)] = wall_clock64(); \
+        if (X.p.prof && threadIdx.x == 0 && blockIdx.x < PROF_WG) X.p.prof[((size_t)blockIdx.x * PROF_PH + (ph)) * 4 + (k)] = wall_clock64(); \
     } while (0)
 
 __device__ __forceinline__ int ph_of(int pass, int l, int k) { return pass * PPH + 5 * l + k; }

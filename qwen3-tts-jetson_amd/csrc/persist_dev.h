@@ -84,17 +84,20 @@ __device__ __forceinline__ float4 f4_of(const uint32_t (&u)[4]) {
 }
 
 
+// block sum of one double per thread ((w0 + w1) + (w2 + w3) of the wave sums).  ONE barrier: the caller guarantees a
+// workgroup barrier between consecutive calls (the role kernels' f16 tile barrier after every RMSNorm), so no wave can
+// overwrite scr while another still reads the previous sums.
 __device__ __forceinline__ double block_sum_d(double v, double *scr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     v = wave_sum_d(v);
-    __syncthreads();
     if (lane == 0) scr[wave] = v;
     __syncthreads();
     return (scr[0] + scr[1]) + (scr[2] + scr[3]);
 }
 
 // RMSNorm of the f32 row held as thread t's elements 4t..4t+3 (K = 1024) -> f16 tile xs; optional f32 side output
-// (gemv.hip prologue: double sums, (x * scale) * w, f16 rounding)
+// (gemv.hip prologue: double sums, (x * scale) * w, f16 rounding).  The caller runs a workgroup barrier before xs is
+// read and before the next call (block_sum_d).
 __device__ __forceinline__ void rms_to_f16(float4 x, float4 w, float eps, uint16_t *xs, double *dscr, float *side) {
     const int t = threadIdx.x;
     double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);

@@ -1,0 +1,755 @@
+// persist_tk.hip — the Talker decode step of one slot (src/tts_transformer.cpp:1376-1512 build_step_graph, the codec
+// head and the CB0 selection of :2416-2499) as ONE persistent launch of role-specialised workgroups: the design of
+// persist_cp.hip (every hand-off between small disjoint role groups, tools/dev/edgebench.hip) applied to the 28-layer
+// step, whose attention reads a growing HBM-resident KV cache.
+//
+//   role (workgroups)        per layer                                           input edge
+//   DN   [0, 56)             18-19 down rows + residual                           h      96 -> 56
+//   O    [56, 88)            32 O-projection rows + residual                      attn   8 -> 32
+//   GU   [88, 184)           RMSNorm(ffn_norm) + 32 gate/up SwiGLU units          x'     32 -> 96
+//   QKV  [184, 248)          RMSNorm(attn_norm) + 64 QKV rows (4 x 16); codec     x      DN 56 -> 64
+//                            head 48 rows (3 x 16) after the last layer
+//   ATT  [248, 248 + 8S)     kv group g, split s: positions [64 s, 64 s + 64)     QKV    ~8 -> S per group
+//                            (S = ceil(n_ctx / 64)); split 0 combines every
+//                            split's partial in split order
+//   SEL  248 + 8S            CB0 selection of the next frame                      logits QKV 64 -> 1
+//
+// Two workgroups per CU (LDS <= 80 KB, <= 256 registers per wave): the grid of up to 505 workgroups is co-resident,
+// so the attention keeps k_attn's split of 64 positions per workgroup (one chunk's body; a workgroup that ran 2-3
+// chunks took 5-9 us per layer, their waves issue-bound) while the other roles keep the code-predictor frame's sizes.
+// Each chunk's partial is computed with k_attn's per-split arithmetic for chunk 64 and the chunk partials are combined
+// in chunk order exactly as k_attn / k_persist combine their splits, so the step is bit-identical to the launch-per-op
+// graph and to k_persist<0, 64> (tests/test_gpu_persist.py).  Every row keeps the per-op GEMVs' lane split and
+// reduction order.  Each workgroup holds only its role's weights (<= 160 VGPRs) or K/V rows, issued right after its
+// phase for the next layer.  Contexts longer than 64 x 32 positions use k_persist<0, CH>.
+#include "persist.h"
+#include "persist_dev.h"
+#include "select.h"
+
+#include <algorithm>
+
+#pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
+
+namespace q3t {
+
+namespace {
+using namespace pdev;
+
+constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, VOC = 3072;
+constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of positions; partial granules; gpart slots
+// Workgroups b and b + 256 share a CU (observed dispatch, tools/dev/cuprobe.hip; speed only, never correctness): the
+// attention splits >= 1 (workgroups 256..) sit beside the down-projection workgroups, two phases away from the
+// attention: the splits' next-layer K/V stream (issued right after their publish) has landed before the down phase,
+// and the down workgroups' own weight stream (issued after E) before the next attention.  Beside the QKV workgroups,
+// which issue the next layer's rows right at the QKV -> attention edge, a split's poll arrived 2.3 us late; beside the
+// gate/up workgroups the K/V stream slowed the gate/up body (max 2.1 vs 1.2 us).
+constexpr int DW = 0, ND = 56;       // down rows 18-19 (5 x 4)
+constexpr int OW = 56, NO = 32;      // O rows 32 (8 x 4)
+constexpr int UW = 88, NU = 96;      // gate/up units 32 (2 x 16)
+constexpr int QW = 184, NQ = 64;     // QKV rows 64 (4 x 16); codec head rows 48 (3 x 16)
+constexpr int AW = 248;              // attention workgroups (8 per split), then the selecting workgroup
+constexpr int GRID_MAX = 512;        // two workgroups per CU (LDS <= 80 KB, <= 256 registers per wave)
+constexpr int S_MAX = (GRID_MAX - AW - 1) / 8;
+constexpr int MAXL = 32;
+static_assert(DW + ND == OW && OW + NO == UW && UW + NU == QW && QW + NQ == AW, "roles");
+static_assert(NQ * 64 == QKVN && NQ * 48 == VOC && NU * 32 == INTER && NO * 32 == H && ND * 19 >= H, "role rows");
+
+template <int CPW>
+struct TLds {
+    uint16_t xs[INTER];
+    float xr[32];
+    float red[4][32];
+    double dscr[8];
+    float hs[32];
+    // attention
+    float raw[4 * D];
+    float q_s[R][D], kn_s[D], vn_s[D];
+    float wred[4][CPW][R];
+    float mch[CPW][R], lch[CPW][R];   // per-chunk max / sum (split partials)
+    float ared[4][CPW][R][D];
+    float pl[MAXCH * PSLOT];     // split 0: every chunk's partial, chunk order
+    float cm[R], cl[R], sw[MAXCH][R];
+    SelLds sel;
+    PLayerW layers[MAXL];
+};
+
+template <int CPW>
+struct Ctx {
+    const PersistParams &p;
+    TLds<CPW> &S;
+    Ctl c;
+    unsigned seq;
+    int pos, nl;
+    __device__ uint32_t tag(int ph) const { return ((seq * 1024u + (unsigned)ph) << 1) | 1u; }
+};
+
+#define PROF(ph, k)                                                                                           \
+    do {                                                                                                      \
+        if (X.p.prof && threadIdx.x == 0 && blockIdx.x < PROF_WG) X.p.prof[((size_t)blockIdx.x * PROF_PH + (ph)) * 4 + (k)] = wall_clock64(); \
+    } while (0)
+
+// x rows 4t..4t+3 of the layer-0 input (k_persist<0,*>'s prologue, same summation order)
+__device__ __forceinline__ float4 layer0_x4(const PersistParams &p) {
+    const int t = threadIdx.x;
+    if (!p.gather) return ldf4(p.x_in + 4 * t);
+    const GatherSum &gs = p.gs;
+    uint2 hv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) hv[j] = ld8(gs.tabs[j] + (size_t)gs.tok[j] * H + 4 * t);
+    const int fr = gs.frame[0];
+    const float *extra = fr < gs.tr_len[0] ? gs.tr + (size_t)fr * H : gs.pad;
+    const float4 ex = ldf4(extra + 4 * t);
+    auto h4 = [](uint2 u) { return make_float4(h2f(u.x & 0xffff), h2f(u.x >> 16), h2f(u.y & 0xffff), h2f(u.y >> 16)); };
+    float4 x = h4(hv[0]);
+#pragma unroll
+    for (int j = 1; j < 16; ++j) { const float4 b = h4(hv[j]); x = make_float4(x.x + b.x, x.y + b.y, x.z + b.z, x.w + b.w); }
+    return make_float4(x.x + ex.x, x.y + ex.y, x.z + ex.z, x.w + ex.w);
+}
+// one element of the same (the O workgroups' residual rows): identical per-element summation order
+__device__ __forceinline__ float layer0_x1(const PersistParams &p, int e) {
+    if (!p.gather) return p.x_in[e];
+    const GatherSum &gs = p.gs;
+    uint16_t hv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) hv[j] = gs.tabs[j][(size_t)gs.tok[j] * H + e];
+    const int fr = gs.frame[0];
+    const float *extra = fr < gs.tr_len[0] ? gs.tr + (size_t)fr * H : gs.pad;
+    const float ex = extra[e];
+    float x = h2f(hv[0]);
+#pragma unroll
+    for (int j = 1; j < 16; ++j) x = x + h2f(hv[j]);
+    return x + ex;
+}
+
+// ------------------------------------------------------------------ QKV rows (+ codec head after the last layer)
+template <int CPW>
+__device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int i = blockIdx.x - QW, t = threadIdx.x, l16 = t & 15, grp = t >> 4, nl = X.nl;
+    uint4 wq[4][8];
+    float4 nw;
+    auto issue_qkv = [&](int l) {
+        const uint16_t *W = S.layers[l].qkv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint16_t *r = W + (size_t)(64 * i + 16 * j + grp) * H + l16 * 8;
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) wq[j][tt] = ld16(r + tt * 128);
+        }
+        nw = ldf4(S.layers[l].attn_norm + 4 * t);
+    };
+    issue_qkv(0);
+    for (int l = 0; l < nl; ++l) {
+        const int ph = 5 * l;
+        float4 x;
+        if (l == 0) {
+            x = layer0_x4(p);
+        } else {
+            uint32_t u[4];
+            PROF(ph, 0);
+            g_wait<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u, X.c);
+            PROF(ph, 1);
+            x = f4_of(u);
+        }
+        rms_to_f16(x, nw, p.eps, S.xs, S.dscr, nullptr);
+        __syncthreads();
+        float acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc[j] = 0.0f;
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) acc[j] = dot8(wq[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), acc[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc[j] = group_sum<16>(acc[j]);
+            if (l16 == 0) g_put(p.gqkv + 64 * i + 16 * j + grp, __float_as_uint(acc[j]), X.tag(ph));
+        }
+        PROF(ph, 2);
+        if (l + 1 < nl) {
+            issue_qkv(l + 1);
+        } else {   // codec head rows 48i + 16j + grp
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint16_t *r = p.head + (size_t)(48 * i + 16 * j + grp) * H + l16 * 8;
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) wq[j][tt] = ld16(r + tt * 128);
+            }
+            nw = ldf4(p.out_norm + 4 * t);
+        }
+    }
+    // ---- head: RMSNorm(output_norm) -> hidden (side output, workgroup 0) -> codec head logits
+    const int hph = 5 * nl;
+    uint32_t u[4];
+    PROF(hph, 0);
+    g_wait<4>(p.gx + 4 * t, X.tag(5 * (nl - 1) + 4), u, X.c);
+    PROF(hph, 1);
+    rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, i == 0 ? p.hidden : nullptr);
+    __syncthreads();
+    float a0[3], a1[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        a0[j] = 0.0f;
+        a1[j] = 0.0f;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) a0[j] = dot8(wq[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a0[j]);
+#pragma unroll
+        for (int tt = 4; tt < 8; ++tt) a1[j] = dot8(wq[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), a1[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float lg = group_sum<16>(a0[j]) + group_sum<16>(a1[j]);
+        if (l16 == 0) {
+            const int row = 48 * i + 16 * j + grp;
+            p.logits[row] = lg;   // read after the launch only (host, tests)
+            g_put(p.glog + row, __float_as_uint(lg), X.tag(hph));
+        }
+    }
+    PROF(hph, 2);
+}
+
+// ------------------------------------------------------------------ O-projection + residual (39-40 rows)
+template <int CPW>
+__device__ __forceinline__ void tk_o(Ctx<CPW> &X) {
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int i = blockIdx.x - OW, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15, grp4 = lane >> 4, nl = X.nl;
+    const int lo = i * H / NO, n = (i + 1) * H / NO - lo;
+    uint4 wo[8][4];
+    auto issue = [&](int l) {   // row lo + 4j + grp4, K slice = wave (k_gemv<1,1,4,PRO_F16,4>)
+        const uint16_t *W = S.layers[l].o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint16_t *r = W + (size_t)(lo + min(4 * j + grp4, n - 1)) * (NH * D) + wave * 512 + l16 * 8;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) wo[j][tt] = ld16(r + tt * 128);
+        }
+    };
+    issue(0);
+    for (int l = 0; l < nl; ++l) {
+        const int ph = 5 * l + 2;
+        if (t < n) {
+            float xr;
+            if (l == 0) {
+                xr = layer0_x1(p, lo + t);
+            } else {
+                uint32_t u1[1];
+                g_wait<1>(p.gx + lo + t, X.tag(5 * (l - 1) + 4), u1, X.c);
+                xr = __uint_as_float(u1[0]);
+            }
+            S.xr[t] = xr;
+        }
+        uint32_t u[4];
+        PROF(ph, 0);
+        g_wait<4>(p.gattn + 4 * t, X.tag(5 * l + 1), u, X.c);
+        PROF(ph, 1);
+        *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
+        __syncthreads();
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[j] = 0.0f;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+                acc[j] = dot8(wo[j][tt], *reinterpret_cast<const uint4 *>(S.xs + wave * 512 + l16 * 8 + tt * 128), acc[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc[j] = group_sum<16>(acc[j]);
+            if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+        }
+        __syncthreads();
+        // one store instruction publishes the workgroup's rows (whole lines from one wave: scattered single-lane
+        // stores from four waves into the same lines made the next edge 2-5 us slower)
+        if (t < n) {
+            const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
+            g_put(p.gx2 + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
+        }
+        PROF(ph, 2);
+        if (l + 1 < nl) issue(l + 1);
+    }
+}
+
+// ------------------------------------------------------------------ RMSNorm(ffn_norm) + gate/up + SwiGLU (32 units)
+template <int CPW>
+__device__ __forceinline__ void tk_gu(Ctx<CPW> &X) {
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int i = blockIdx.x - UW, t = threadIdx.x, l16 = t & 15, grp = t >> 4, nl = X.nl;
+    uint4 wg[2][8], wu[2][8];
+    float4 nw;
+    auto issue = [&](int l) {
+        const uint16_t *W = S.layers[l].gu;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int unit = 32 * i + 16 * j + grp;
+            const uint16_t *r = W + (size_t)((unit >> 4) * 32 + (unit & 15)) * H + l16 * 8;
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) wg[j][tt] = ld16(r + tt * 128);
+#pragma unroll
+            for (int tt = 0; tt < 8; ++tt) wu[j][tt] = ld16(r + 16 * H + tt * 128);
+        }
+        nw = ldf4(S.layers[l].ffn_norm + 4 * t);
+    };
+    issue(0);
+    for (int l = 0; l < nl; ++l) {
+        const int ph = 5 * l + 3;
+        uint32_t u[4];
+        PROF(ph, 0);
+        g_wait<4>(p.gx2 + 4 * t, X.tag(5 * l + 2), u, X.c);
+        PROF(ph, 1);
+        rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
+        __syncthreads();
+        float a0[2], a1[2], b0[2], b1[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            a0[j] = a1[j] = b0[j] = b1[j] = 0.0f;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const uint4 xv = *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128);
+                a0[j] = dot8(wg[j][tt], xv, a0[j]);
+                b0[j] = dot8(wu[j][tt], xv, b0[j]);
+            }
+#pragma unroll
+            for (int tt = 4; tt < 8; ++tt) {
+                const uint4 xv = *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128);
+                a1[j] = dot8(wg[j][tt], xv, a1[j]);
+                b1[j] = dot8(wu[j][tt], xv, b1[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float ga = group_sum<16>(a0[j]) + group_sum<16>(a1[j]);
+            const float ub = group_sum<16>(b0[j]) + group_sum<16>(b1[j]);
+            if (l16 == 0) S.hs[16 * j + grp] = silu_f(ga) * ub;
+        }
+        __syncthreads();
+        if (t < 16) g_put(p.gh + 16 * i + t, (uint32_t)f2h(S.hs[2 * t]) | ((uint32_t)f2h(S.hs[2 * t + 1]) << 16), X.tag(ph));
+        PROF(ph, 2);
+        if (l + 1 < nl) issue(l + 1);
+    }
+}
+
+// ------------------------------------------------------------------ down + residual (23-24 rows)
+template <int CPW>
+__device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int i = blockIdx.x - DW, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15, grp4 = lane >> 4, nl = X.nl;
+    const int lo = i * H / ND, n = (i + 1) * H / ND - lo;
+    uint4 wd[5][6];
+    auto issue = [&](int l) {   // row lo + 4j + grp4 (clamped), K slice = wave (k_gemv<1,1,4,PRO_F16,8>)
+        const uint16_t *W = S.layers[l].down;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint16_t *r = W + (size_t)(lo + min(4 * j + grp4, n - 1)) * INTER + wave * 768 + l16 * 8;
+#pragma unroll
+            for (int tt = 0; tt < 6; ++tt) wd[j][tt] = ld16(r + tt * 128);
+        }
+    };
+    issue(0);
+    for (int l = 0; l < nl; ++l) {
+        const int ph = 5 * l + 4;
+        if (t < n) {
+            uint32_t u1[1];
+            g_wait<1>(p.gx2 + lo + t, X.tag(5 * l + 2), u1, X.c);
+            S.xr[t] = __uint_as_float(u1[0]);
+        }
+        uint32_t u[6];
+        PROF(ph, 0);
+        g_wait<6>(p.gh + 6 * t, X.tag(5 * l + 3), u, X.c);
+        PROF(ph, 1);
+        *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
+        *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
+        *reinterpret_cast<uint2 *>(S.xs + 12 * t + 8) = make_uint2(u[4], u[5]);
+        __syncthreads();
+        float acc[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            acc[j] = 0.0f;
+#pragma unroll
+            for (int tt = 0; tt < 6; ++tt)
+                acc[j] = dot8(wd[j][tt], *reinterpret_cast<const uint4 *>(S.xs + wave * 768 + l16 * 8 + tt * 128), acc[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            acc[j] = group_sum<16>(acc[j]);
+            if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+        }
+        __syncthreads();
+        if (t < n) {
+            const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
+            g_put(p.gx + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
+        }
+        PROF(ph, 2);
+        if (l + 1 < nl) issue(l + 1);
+    }
+}
+
+// ------------------------------------------------------------------ attention: kv group g, split s (CPW chunks)
+template <int CPW>
+__device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
+    constexpr int NP = CPW * CHK / 16;   // position passes of 16 (16 lanes x 8 dims per position)
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int a = blockIdx.x - AW, g = a & (NKV - 1), s = a >> 3;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t >> 4, li = t & 15, nl = X.nl, pos = X.pos;
+    const int nch = pos / CHK + 1, c0 = s * CPW;
+    const int myc = min(max(nch - c0, 0), CPW);   // chunks of this split in use this step
+    if (myc == 0) return;                           // (uniform over the workgroup)
+    const int j0 = c0 * CHK;
+    const bool has_pos = pos / CHK >= c0 && pos / CHK < c0 + CPW;
+    const int gi = t < 128 ? g * 256 + 2 * t : t < 192 ? NH * D + g * D + 2 * (t - 128) : (NH + NKV) * D + g * D + 2 * (t - 192);
+    uint4 kr[NP], vr[NP];
+    float hn[2];
+    auto issue = [&](int l) {   // this split's cached K/V rows (clamped rows re-read row pos) + head-norm weights
+        const size_t o = (size_t)l * p.kv_layer + (size_t)g * p.n_ctx * D;
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = min(j0 + pi * 16 + pg, pos);
+            kr[pi] = ld16(p.kc + o + (size_t)j * D + li * 8);
+            vr[pi] = ld16(p.vc + o + (size_t)j * D + li * 8);
+        }
+        const float *nwv = wave == 2 ? S.layers[l].kn : S.layers[l].qn;
+        hn[0] = nwv[lane];
+        hn[1] = nwv[lane + 64];
+    };
+    const float rp0 = p.rope[(size_t)pos * D + 2 * lane], rp1 = p.rope[(size_t)pos * D + 2 * lane + 1];
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    issue(0);
+    for (int l = 0; l < nl; ++l) {
+        const int ph = 5 * l + 1;
+        const size_t kvo = (size_t)l * p.kv_layer + (size_t)g * p.n_ctx * D;
+        {
+            uint32_t u[2];
+            PROF(ph, 0);
+            g_wait<2>(p.gqkv + gi, X.tag(5 * l), u, X.c);
+            PROF(ph, 1);
+            S.raw[2 * t] = __uint_as_float(u[0]);
+            S.raw[2 * t + 1] = __uint_as_float(u[1]);
+        }
+        __syncthreads();
+        {   // wave v: q head 0 / q head 1 / k (head norm + RoPE) / v (f16 rounding)
+            const int v = wave;
+            if (v == 3) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) S.vn_s[lane + 64 * e] = f16r(S.raw[3 * D + lane + 64 * e]);
+            } else {
+                const float *src = S.raw + v * D;
+                float xx[2];
+                double ss = 0.0;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) { xx[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(xx[e], xx[e]); }
+                ss = wave_sum_d(ss);
+                const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
+#pragma unroll
+                for (int e = 0; e < 2; ++e) xx[e] = (xx[e] * scale) * hn[e];
+                const float y0 = opaque(opaque(xx[0] * rp0) - opaque(xx[1] * rp1));   // as k_attn: three roundings
+                const float y1 = opaque(opaque(xx[0] * rp1) + opaque(xx[1] * rp0));
+                float *dst = v == 2 ? S.kn_s : S.q_s[v];
+                dst[lane] = f16r(y0);
+                dst[lane + 64] = f16r(y1);
+            }
+        }
+        __syncthreads();
+        PROF(200 + l, 0);   // (development timeline: q/k normed + RoPE)
+        if (has_pos && t < D) {   // KV append at pos (read by later steps only)
+            p.kc[kvo + (size_t)pos * D + t] = f2h(S.kn_s[t]);
+            p.vc[kvo + (size_t)pos * D + t] = f2h(S.vn_s[t]);
+        }
+        float q8[R][8];
+#pragma unroll
+        for (int h = 0; h < R; ++h)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q8[h][e] = S.q_s[h][li * 8 + e];
+        float sc[NP][R];
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = j0 + pi * 16 + pg;
+            const bool ok = j <= pos;
+            float k8[8];
+            if (j == pos) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) k8[e] = S.kn_s[li * 8 + e];
+            } else {
+                const uint32_t ww[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { k8[2 * e] = h2f(ww[e] & 0xffff); k8[2 * e + 1] = h2f(ww[e] >> 16); }
+            }
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                float sv = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sv = __fmaf_rn(k8[e], q8[h][e], sv);   // explicit fma: identical in k_attn
+                sv = group_sum<16>(sv);
+                sc[pi][h] = ok ? __fmul_rn(sv, kq_scale) : -INFINITY;
+            }
+        }
+        // per chunk cc (passes 4cc .. 4cc+3): max, then exp / sum, then P.V, each as k_attn's split of 64 positions
+#pragma unroll
+        for (int cc = 0; cc < CPW; ++cc)
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                float m = sc[4 * cc][h];
+#pragma unroll
+                for (int q = 1; q < 4; ++q) m = fmaxf(m, sc[4 * cc + q][h]);
+                m = rows_max(m);
+                if (lane == 0) S.wred[wave][cc][h] = m;
+            }
+        __syncthreads();
+        float M[CPW][R];
+#pragma unroll
+        for (int cc = 0; cc < CPW; ++cc)
+#pragma unroll
+            for (int h = 0; h < R; ++h)
+                M[cc][h] = fmaxf(fmaxf(S.wred[0][cc][h], S.wred[1][cc][h]), fmaxf(S.wred[2][cc][h], S.wred[3][cc][h]));
+        if (t == 0) {
+#pragma unroll
+            for (int cc = 0; cc < CPW; ++cc)
+#pragma unroll
+                for (int h = 0; h < R; ++h) S.mch[cc][h] = M[cc][h];
+        }
+        __syncthreads();
+        PROF(200 + l, 1);   // (development timeline: scores + max done)
+#pragma unroll
+        for (int cc = 0; cc < CPW; ++cc) {
+            float pr[4][R];
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                float lsum = 0.0f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int pi = 4 * cc + q;
+                    const bool ok = j0 + pi * 16 + pg <= pos;
+                    pr[q][h] = ok ? expf(__fsub_rn(sc[pi][h], M[cc][h])) : 0.0f;
+                    lsum += pr[q][h];
+                }
+                lsum = rows_sum(lsum);
+                if (lane == 0) S.wred[wave][cc][h] = lsum;
+            }
+            float acc[R][8];
+#pragma unroll
+            for (int h = 0; h < R; ++h)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int pi = 4 * cc + q;
+                const int j = j0 + pi * 16 + pg;
+                const bool ok = j <= pos;
+                float v8[8];
+                if (j == pos) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v8[e] = S.vn_s[li * 8 + e];
+                } else {
+                    const uint32_t ww[4] = {vr[pi].x, vr[pi].y, vr[pi].z, vr[pi].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { v8[2 * e] = h2f(ww[e] & 0xffff); v8[2 * e + 1] = h2f(ww[e] >> 16); }
+                }
+#pragma unroll
+                for (int h = 0; h < R; ++h)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr[q][h], ok ? v8[e] : 0.0f, acc[h][e]);
+            }
+#pragma unroll
+            for (int h = 0; h < R; ++h)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float av = rows_sum(acc[h][e]);
+                    if (lane < 16) S.ared[wave][cc][h][li * 8 + e] = av;
+                }
+        }
+        __syncthreads();
+        PROF(200 + l, 2);   // (development timeline: P.V reduced)
+        uint64_t *gout = p.gattn + (size_t)g * R * (D / 2);
+        if (nch == 1) {   // one chunk: k_attn's single-split output
+            if (t < R * D / 2) {
+                const int h = t / (D / 2), d = 2 * (t % (D / 2));
+                const float lsum = (S.wred[0][0][h] + S.wred[1][0][h]) + (S.wred[2][0][h] + S.wred[3][0][h]);
+                const float a0 = (S.ared[0][0][h][d] + S.ared[1][0][h][d]) + (S.ared[2][0][h][d] + S.ared[3][0][h][d]);
+                const float a1 = (S.ared[0][0][h][d + 1] + S.ared[1][0][h][d + 1]) + (S.ared[2][0][h][d + 1] + S.ared[3][0][h][d + 1]);
+                g_put(gout + t, (uint32_t)f2h(a0 / lsum) | ((uint32_t)f2h(a1 / lsum) << 16), X.tag(ph));
+            }
+        } else {
+            uint64_t *gp = p.gpart + (size_t)g * MAXCH * PSLOT;
+            if (s > 0) {   // publish this split's chunk partials (acc [2][128], m [2], l [2]) in their chunk slots
+                for (int cc = 0; cc < myc; ++cc) {
+                    uint64_t *mine = gp + (size_t)(c0 + cc) * PSLOT;
+                    const int h = t / D, d = t % D;
+                    const float av = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
+                    g_put(mine + t, __float_as_uint(av), X.tag(ph));
+                    if (t < PSLOT - R * D) {
+                        const int hh = t % R;
+                        const float lsum = (S.wred[0][cc][hh] + S.wred[1][cc][hh]) + (S.wred[2][cc][hh] + S.wred[3][cc][hh]);
+                        const float v = t < R ? S.mch[cc][hh] : t < 2 * R ? lsum : 0.0f;
+                        g_put(mine + R * D + t, __float_as_uint(v), X.tag(ph));
+                    }
+                }
+            } else {       // split 0: its own chunks from LDS, the others' from their granules, combined in chunk order
+                float *pl = S.pl;
+                for (int cc = 0; cc < myc; ++cc) {
+                    const int h = t / D, d = t % D;
+                    pl[cc * PSLOT + t] = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
+                    if (t < R) {
+                        pl[cc * PSLOT + R * D + t] = S.mch[cc][t];
+                        pl[cc * PSLOT + R * D + R + t] = (S.wred[0][cc][t] + S.wred[1][cc][t]) + (S.wred[2][cc][t] + S.wred[3][cc][t]);
+                    }
+                }
+                const int n = (nch - CPW) * PSLOT;
+                PROF(200 + l, 3);   // (development timeline: own partials staged, remote ones polled next)
+                for (int i0 = 4 * t; i0 < n; i0 += 1024) {
+                    uint32_t u4[4];
+                    g_wait<4>(gp + CPW * PSLOT + i0, X.tag(ph), u4, X.c);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) pl[CPW * PSLOT + i0 + q] = __uint_as_float(u4[q]);
+                }
+                __syncthreads();
+                if (t < R) {
+                    float mx = -INFINITY;
+                    for (int s2 = 0; s2 < nch; ++s2) mx = fmaxf(mx, pl[s2 * PSLOT + R * D + t]);
+                    float lt = 0.0f;
+                    for (int s2 = 0; s2 < nch; ++s2)
+                        lt = __fmaf_rn(pl[s2 * PSLOT + R * D + R + t], expf(pl[s2 * PSLOT + R * D + t] - mx), lt);
+                    S.cm[t] = mx;
+                    S.cl[t] = lt;
+                }
+                __syncthreads();
+                for (int i = t; i < nch * R; i += 256) {
+                    const int s2 = i / R, h = i % R;
+                    S.sw[s2][h] = expf(pl[s2 * PSLOT + R * D + h] - S.cm[h]);
+                }
+                __syncthreads();
+                if (t < R * D / 2) {
+                    const int h = t / (D / 2), d = 2 * (t % (D / 2));
+                    float a2[2];
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        float av = 0.0f;
+                        for (int s2 = 0; s2 < nch; ++s2) av = __fmaf_rn(pl[s2 * PSLOT + h * D + d + q], S.sw[s2][h], av);
+                        a2[q] = av;
+                    }
+                    g_put(gout + t, (uint32_t)f2h(a2[0] / S.cl[h]) | ((uint32_t)f2h(a2[1] / S.cl[h]) << 16), X.tag(ph));
+                }
+            }
+        }
+        PROF(ph, 2);
+        // the next layer's K/V rows, a layer ahead of their use (after the combine: its polls would wait behind them)
+        if (l + 1 < nl) issue(l + 1);
+    }
+}
+
+// ------------------------------------------------------------------ CB0 selection of the next frame
+template <int CPW>
+__device__ __forceinline__ void tk_sel(Ctx<CPW> &X) {
+    const PersistParams &p = X.p;
+    TLds<CPW> &S = X.S;
+    const int t = threadIdx.x, hph = 5 * X.nl;
+    SelPre spre;
+    if (p.sel.mode != SEL_NONE) sel_prefetch<SEL_CB0>(p.sel, 0, spre);
+    // the logits are waited for even without a selection: the launch's seq bump must follow every chain workgroup's
+    // start (each reads seq once, at its start)
+    int tok = -1;
+    // one lane sleeps until the last layer's down projection is under way (its first output granule), then the whole
+    // workgroup sweeps the logits: a 3,072-granule sweep polled for the whole step slowed the workgroup sharing this
+    // CU by ~5 us per phase
+    if (t == 0) {
+        uint32_t u1[1];
+        Ctl c1 = X.c;
+        for (int k = 0; k < 1 << 14 && !c1.abort; ++k) {   // bounded (~14 ms)
+            const uint64_t v = g_ld(p.gh);   // gate/up output of the last layer (published before the down phase)
+            if ((uint32_t)(v >> 32) == X.tag(5 * (X.nl - 1) + 3)) break;
+            __builtin_amdgcn_s_sleep(32);
+        }
+        (void)u1;
+    }
+    __syncthreads();
+    uint32_t u[VOC / 256];
+    PROF(hph, 0);
+    g_wait<VOC / 256>(p.glog + t * (VOC / 256), X.tag(hph), u, X.c);
+    PROF(hph, 1);
+    if (p.sel.mode != SEL_NONE) {
+        float v[SEL_VPT_MAX];
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = e < VOC / 256 ? __uint_as_float(u[e]) : -INFINITY;
+        tok = select_token_pre<SEL_CB0>(p.sel, spre, v, S.sel);
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (tok >= 0) select_commit(p.sel, 0, tok);
+        __hip_atomic_store(p.seq, X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    PROF(hph, 2);
+}
+
+template <int CPW>
+__global__ void __launch_bounds__(256, 2) k_tk_roles(const PersistParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    TLds<CPW> &S = *reinterpret_cast<TLds<CPW> *>(smem);
+    const int t = threadIdx.x, w = blockIdx.x;
+    Ctx<CPW> X{p, S, Ctl{p.err, false}, __hip_atomic_load(p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), p.pos[0], p.n_layers};
+    if (t < p.n_layers) S.layers[t] = p.L[t];
+    __syncthreads();
+    const int sel_w = AW + 8 * p.roles_split;
+    if (w < OW) tk_dn(X);
+    else if (w < UW) tk_o(X);
+    else if (w < QW) tk_gu(X);
+    else if (w < AW) tk_qkv(X);
+    else if (w < sel_w) tk_att(X);
+    else tk_sel(X);
+}
+
+template <int CPW>
+size_t tk_lds() { return sizeof(TLds<CPW>); }   // <= 80 KB: two workgroups per CU
+
+template <int CPW>
+const void *tk_fn() { return reinterpret_cast<const void *>(&k_tk_roles<CPW>); }
+
+// chunks of 64 positions per attention workgroup for a context, 0 if the role kernel does not cover it
+int tk_cpw(int n_ctx) {
+    const int nch = (n_ctx + CHK - 1) / CHK;
+    return nch <= S_MAX && nch <= MAXCH ? 1 : 0;
+}
+
+}  // namespace
+
+bool persist_tk_roles_supported(int n_ctx) { return tk_cpw(n_ctx) != 0; }
+
+bool persist_tk_roles_resident(int device, int n_ctx) {
+    int n_cu = 0, blocks = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 256) return false;
+    const int cpw = tk_cpw(n_ctx);
+    if (!cpw) return false;
+    const void *k = tk_fn<1>();
+    const size_t lds = tk_lds<1>();
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
+    // the grid (up to 505 workgroups) must be co-resident: two per CU
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, lds) == hipSuccess && blocks >= 2;
+}
+
+template <int CPW>
+static bool tk_launch(PersistParams p, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        Q3T_HIP(hipFuncSetAttribute(tk_fn<CPW>(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)tk_lds<CPW>()));
+        attr = true;
+    }
+    const int nch = (p.n_ctx + CHK - 1) / CHK;
+    p.roles_split = (nch + CPW - 1) / CPW;
+    hipLaunchKernelGGL((k_tk_roles<CPW>), dim3(AW + 8 * p.roles_split + 1), dim3(256), tk_lds<CPW>(), s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+bool persist_tk_roles(const PersistParams &p, hipStream_t s) {
+    if (!p.L || p.n_layers <= 0 || p.n_layers > MAXL || !p.head || !p.logits || !p.hidden || !p.pos || !p.rope || !p.kc ||
+        !p.vc || !p.gx || (p.gather && !(p.gs.tok && p.gs.tabs && p.gs.frame && p.gs.tr && p.gs.tr_len && p.gs.pad)) ||
+        (!p.gather && !p.x_in) || (p.sel.mode != SEL_NONE && (p.sel.mode != SEL_CB0 || p.sel.V != VOC))) {
+        set_error("persist_tk_roles: bad parameters");
+        return false;
+    }
+    if (tk_cpw(p.n_ctx) != 1) { set_error("persist_tk_roles: context too long"); return false; }
+    return tk_launch<1>(p, s);
+}
+
+}  // namespace q3t
