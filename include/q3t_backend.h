@@ -126,6 +126,11 @@ int q3t_time_stage(q3t_ctx *ctx, int stage, int n_slots, int pos, int iters, dou
  * Q3T_PERSIST=0), 0 = in use, 1 = a launch gave up waiting on an in-launch hand-off (protocol fault; the next call
  * falls back), 2 = disabled after such a fault: the context runs the bit-identical launch-per-op graphs */
 int q3t_persist_status(q3t_ctx *ctx);
+/* which single-slot persistent kernels the context launches (bit mask, 0 when none): 1 = talker step on
+ * role-specialised workgroups (persist_tk.hip), 2 = talker step on all-role workgroups (persist.hip k_persist<0,CH>),
+ * 4 = code-predictor frame on role-specialised workgroups (persist_cp.hip), 8 = code-predictor frame on all-role
+ * workgroups (persist.hip k_persist<1|2,16>) */
+int q3t_persist_kernels(q3t_ctx *ctx);
 
 /* ---- vocoder */
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode);

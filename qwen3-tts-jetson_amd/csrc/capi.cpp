@@ -236,6 +236,11 @@ int q3t_persist_status(q3t_ctx *ctx) {
     return ctx->engine.persist_error() ? 1 : 0;
 }
 
+int q3t_persist_kernels(q3t_ctx *ctx) {
+    if (!ctx || !ctx->engine.has_talker()) return 0;
+    return ctx->engine.persist_kernels();
+}
+
 int64_t q3t_vocoder_num_samples(const q3t_ctx *ctx, int32_t n_frames, int mode) {
     if (!ctx) return -1;
     q3t::Vocoder *v = const_cast<q3t::Engine &>(ctx->engine).vocoder();

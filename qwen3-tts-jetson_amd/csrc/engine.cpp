@@ -510,12 +510,12 @@ bool Engine::setup_persist() {
     return true;
 }
 
-// the persistent code-predictor frame's per-token tables (a context for few slots only: the batched serving contexts
-// do not pay the QKV table's 520 MB; their rare 1-slot calls run the persistent frame without it)
+// the persistent code-predictor frame's per-token tables
 bool Engine::build_persist_tables() {
     if (!persist_cp_ || tables_built_) return true;
     if (c_.has_mtp && !build_cp_proj_table()) return false;
-    if (opt_.cp_qkv_table && max_slots_ <= 4 && !build_cp_qkv_table()) return false;
+    // (520 MB of f32 for any slot count: a serving context's rare 1-slot calls run the frame with it too)
+    if (opt_.cp_qkv_table && !build_cp_qkv_table()) return false;
     tables_built_ = true;
     return true;
 }

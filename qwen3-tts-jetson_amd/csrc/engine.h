@@ -137,6 +137,9 @@ public:
     unsigned persist_launches_ = 0;
     bool persist_error();
     bool persist_enabled() const { return persist_ || persist_cp_; }
+    int persist_kernels() const {   // q3t_persist_kernels
+        return (persist_ ? (tk_roles_ ? 1 : 2) : 0) | (persist_cp_ ? (cp_roles_ && cp_qkvtab_ && !cp_projtab_ ? 4 : 8) : 0);
+    }
     bool persist_fell_back() const { return persist_fallback_; }
 #ifdef Q3T_DEV
     // development hook: copy a device state buffer to the host (0 K cache, 1 V cache, 2 qkv, 3 attention output)

@@ -50,11 +50,11 @@ struct CLds {
     uint16_t xs[INTER];          // f16 activation tile of the current phase
     float xr[32];                // residual rows of this workgroup (O / DN)
     float red[4][32];            // K-slice partial sums [wave][row] (O / DN)
+    float outv[64];              // QKV / head rows staged for one whole-line publish
     double dscr[8];
     float hs[32];                // SwiGLU outputs (GU)
-    float raw[4 * D];            // ATT: q head 2g, q head 2g+1, k, v (raw QKV values)
     float q_s[2][D];
-    float wred[4][2];
+    float wred[4][2], wsum[4][2];   // per-wave softmax max / sum (apart: no barrier between them)
     float ared[4][2][D];
     uint16_t kc[NLC][16][D], vc[NLC][16][D];   // ATT: this kv group's 16-position K/V cache (f16), the whole frame
     float qn[NLC][D], kn[NLC][D];              // ATT: head-norm weights
@@ -133,8 +133,12 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 acc[j] = group_sum<16>(acc[j]);
-                if (l16 == 0) g_put(p.gqkv + 64 * i + 16 * j + grp, __float_as_uint(acc[j]), X.tag(ph));
+                if (l16 == 0) S.outv[16 * j + grp] = acc[j];
             }
+            __syncthreads();
+            // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four
+            // waves into shared lines make the next edge slower
+            if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
             PROF(ph, 2);
             if (l + 1 < NLC) issue_qkv(l + 1);
             else if (pass >= 1) issue_head(pass);
@@ -162,11 +166,12 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const float lg = group_sum<16>(a0[j]) + group_sum<16>(a1[j]);
-            if (l16 == 0) {
-                const int row = 32 * i + 16 * j + grp;
-                g_put(p.glog + row, __float_as_uint(lg), X.tag(hph));
-                p.logits[row] = lg;   // read after the launch only (host, tests)
-            }
+            if (l16 == 0) S.outv[16 * j + grp] = lg;
+        }
+        __syncthreads();
+        if (t < 32) {
+            g_put(p.glog + 32 * i + t, __float_as_uint(S.outv[t]), X.tag(hph));
+            p.logits[32 * i + t] = S.outv[t];   // read after the launch only (host, tests)
         }
         PROF(hph, 2);
         if (pass + 1 < NPASS) issue_qkv(1);
@@ -179,8 +184,10 @@ __device__ __forceinline__ void role_att(Ctx &X) {
     CLds &S = X.S;
     const int g = blockIdx.x - AW, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int pg = t >> 4, li = t & 15;   // attention: position, 8-dim chunk
-    // this thread's two raw QKV values (q heads 2g, 2g+1 | k | v of group g)
-    const int gi = t < 128 ? g * 256 + 2 * t : t < 192 ? NH * D + g * D + 2 * (t - 128) : (NH + NKV) * D + g * D + 2 * (t - 192);
+    // wave v takes elements lane and lane + 64 of its head (q head 2g, q head 2g+1, k, v of group g): the pair its head
+    // norm and NEOX RoPE work on, polled straight from the granules (no LDS staging or barrier before the norm)
+    const int hb = wave == 0 ? g * 256 : wave == 1 ? g * 256 + D : wave == 2 ? NH * D + g * D : (NH + NKV) * D + g * D;
+    const int gi = hb + lane;
     for (int e = t; e < NLC * D; e += 256) {
         S.qn[e / D][e % D] = S.layers[e / D].qn[e % D];
         S.kn[e / D][e % D] = S.layers[e / D].kn[e % D];
@@ -189,37 +196,36 @@ __device__ __forceinline__ void role_att(Ctx &X) {
     SelPre spre;
     sel_prefetch<SEL_CP>(p.sel, 0, spre);
     int tok = p.gs.tok[0];   // CB0: the input of pass 1
-    uint2 traw = ld8(p.qkvtab + (size_t)tok * QKVN + gi);
+    float traw[2] = {ldgv<float>(p.qkvtab + (size_t)tok * QKVN + gi), ldgv<float>(p.qkvtab + (size_t)tok * QKVN + gi + 64)};
     const float kq_scale = 1.0f / sqrtf((float)D);
     __syncthreads();
     for (int pass = 0; pass < NPASS; ++pass) {
         const int pos = pass;
         for (int l = 0; l < NLC; ++l) {
             const int ph = ph_of(pass, l, 1);
-            uint32_t u[2];
+            float xr[2];
             if (pass >= 1 && l == 0) {
-                u[0] = traw.x;
-                u[1] = traw.y;
+                xr[0] = traw[0];
+                xr[1] = traw[1];
             } else {
+                uint32_t u[2];
                 PROF(ph, 0);
-                g_wait<2>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
+                g_wait<2, 64>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
                 PROF(ph, 1);
+                xr[0] = __uint_as_float(u[0]);
+                xr[1] = __uint_as_float(u[1]);
             }
-            S.raw[2 * t] = __uint_as_float(u[0]);
-            S.raw[2 * t + 1] = __uint_as_float(u[1]);
-            __syncthreads();
             {   // wave v: q head 0 / q head 1 / k (head norm + RoPE, K append) / v (f16 rounding, V append)
                 const int v = wave;
                 if (v == 3) {
 #pragma unroll
-                    for (int e = 0; e < 2; ++e) S.vc[l][pos][lane + 64 * e] = f2h(S.raw[3 * D + lane + 64 * e]);
+                    for (int e = 0; e < 2; ++e) S.vc[l][pos][lane + 64 * e] = f2h(xr[e]);
                 } else {
-                    const float *src = S.raw + v * D;
                     const float *hn = v == 2 ? S.kn[l] : S.qn[l];
                     float xx[2];
                     double ss = 0.0;
 #pragma unroll
-                    for (int e = 0; e < 2; ++e) { xx[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(xx[e], xx[e]); }
+                    for (int e = 0; e < 2; ++e) { xx[e] = xr[e]; ss += (double)__fmul_rn(xx[e], xx[e]); }
                     ss = wave_sum_d(ss);
                     const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
 #pragma unroll
@@ -269,12 +275,11 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             __syncthreads();
 #pragma unroll
             for (int h = 0; h < 2; ++h) M[h] = fmaxf(fmaxf(S.wred[0][h], S.wred[1][h]), fmaxf(S.wred[2][h], S.wred[3][h]));
-            __syncthreads();
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 pr[h] = ok ? expf(__fsub_rn(sc[h], M[h])) : 0.0f;
                 const float lsum = rows_sum(pr[h]);
-                if (lane == 0) S.wred[wave][h] = lsum;
+                if (lane == 0) S.wsum[wave][h] = lsum;
             }
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -286,7 +291,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             __syncthreads();
             if (t < 128) {
                 const int h = t / (D / 2), d = 2 * (t % (D / 2));
-                const float lsum = (S.wred[0][h] + S.wred[1][h]) + (S.wred[2][h] + S.wred[3][h]);
+                const float lsum = (S.wsum[0][h] + S.wsum[1][h]) + (S.wsum[2][h] + S.wsum[3][h]);
                 const float a0 = (S.ared[0][h][d] + S.ared[1][h][d]) + (S.ared[2][h][d] + S.ared[3][h][d]);
                 const float a1 = (S.ared[0][h][d + 1] + S.ared[1][h][d + 1]) + (S.ared[2][h][d + 1] + S.ared[3][h][d + 1]);
                 g_put(p.gattn + g * 128 + t, (uint32_t)f2h(a0 / lsum) | ((uint32_t)f2h(a1 / lsum) << 16), X.tag(ph));
@@ -308,6 +313,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         SelectSpec sp = p.sel;
         sp.step = pass - 1;
         const int sel = select_token_pre<SEL_CP>(sp, spre, v, S.sel);
+        PROF(hph, 3);   // (development timeline: token selected)
         if (g == 0 && t == 0) {
             if (pass + 1 < NPASS) g_put(p.gtok + pass, (uint32_t)max(sel, 0), X.tag(hph));
             if (sel >= 0) select_commit(sp, 0, sel);
@@ -315,7 +321,11 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         }
         PROF(hph, 2);
         tok = max(sel, 0);
-        if (pass + 1 < NPASS) traw = ld8(p.qkvtab + ((size_t)(VOC + (pass - 1) * CPV) + tok) * QKVN + gi);
+        if (pass + 1 < NPASS) {
+            const float *row = p.qkvtab + ((size_t)(VOC + (pass - 1) * CPV) + tok) * QKVN + gi;
+            traw[0] = ldgv<float>(row);
+            traw[1] = ldgv<float>(row + 64);
+        }
     }
 }
 

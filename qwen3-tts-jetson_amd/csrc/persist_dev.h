@@ -51,13 +51,13 @@ struct Ctl {
 
 // spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
 // workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
-template <int N>
+template <int N, int STRIDE = 1>
 __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
     uint64_t v[N];
     unsigned it = 0;
     while (true) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) v[i] = g_ld(base + i);
+        for (int i = 0; i < N; ++i) v[i] = g_ld(base + i * STRIDE);
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < N; ++i) ok &= (uint32_t)(v[i] >> 32) == tag;

@@ -4,9 +4,9 @@
 // step, whose attention reads a growing HBM-resident KV cache.
 //
 //   role (workgroups)        per layer                                           input edge
-//   DN   [0, 56)             18-19 down rows + residual                           h      96 -> 56
-//   O    [56, 88)            32 O-projection rows + residual                      attn   8 -> 32
-//   GU   [88, 184)           RMSNorm(ffn_norm) + 32 gate/up SwiGLU units          x'     32 -> 96
+//   O    [0, 32)             32 O-projection rows + residual                      attn   8 -> 32
+//   GU   [32, 128)           RMSNorm(ffn_norm) + 32 gate/up SwiGLU units          x'     32 -> 96
+//   DN   [128, 184)          18-19 down rows + residual                           h      96 -> 56
 //   QKV  [184, 248)          RMSNorm(attn_norm) + 64 QKV rows (4 x 16); codec     x      DN 56 -> 64
 //                            head 48 rows (3 x 16) after the last layer
 //   ATT  [248, 248 + 8S)     kv group g, split s: positions [64 s, 64 s + 64)     QKV    ~8 -> S per group
@@ -38,20 +38,29 @@ using namespace pdev;
 constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, VOC = 3072;
 constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of positions; partial granules; gpart slots
 // Workgroups b and b + 256 share a CU (observed dispatch, tools/dev/cuprobe.hip; speed only, never correctness): the
-// attention splits >= 1 (workgroups 256..) sit beside the down-projection workgroups, two phases away from the
-// attention: the splits' next-layer K/V stream (issued right after their publish) has landed before the down phase,
-// and the down workgroups' own weight stream (issued after E) before the next attention.  Beside the QKV workgroups,
-// which issue the next layer's rows right at the QKV -> attention edge, a split's poll arrived 2.3 us late; beside the
-// gate/up workgroups the K/V stream slowed the gate/up body (max 2.1 vs 1.2 us).
-constexpr int DW = 0, ND = 56;       // down rows 18-19 (5 x 4)
-constexpr int OW = 56, NO = 32;      // O rows 32 (8 x 4)
-constexpr int UW = 88, NU = 96;      // gate/up units 32 (2 x 16)
+// attention splits >= 1 (workgroups 256..) sit beside the O-projection workgroups (then gate/up), whose weight stream
+// (issued right after their phase) has landed long before the next attention, and the splits issue their own next-layer
+// K/V rows only once the O projection is done.  Beside the QKV workgroups, which issue the next layer's rows right at
+// the QKV -> attention edge, a split's poll arrived 2.3 us late; beside the down workgroups 0.7 us.
+#ifndef Q3T_TK_PAIR
+#define Q3T_TK_PAIR 0   // development: 0 = O, gate/up, down, QKV (the splits beside O); 1 = down, O, gate/up, QKV
+#endif
+#if Q3T_TK_PAIR == 0
+constexpr int OW = 0, NO = 32;       // O rows 32 (8 x 4)
+constexpr int UW = 32, NU = 96;      // gate/up units 32 (2 x 16)
+constexpr int DW = 128, ND = 56;     // down rows 18-19 (5 x 4)
 constexpr int QW = 184, NQ = 64;     // QKV rows 64 (4 x 16); codec head rows 48 (3 x 16)
+#else
+constexpr int DW = 0, ND = 56;
+constexpr int OW = 56, NO = 32;
+constexpr int UW = 88, NU = 96;
+constexpr int QW = 184, NQ = 64;
+#endif
 constexpr int AW = 248;              // attention workgroups (8 per split), then the selecting workgroup
 constexpr int GRID_MAX = 512;        // two workgroups per CU (LDS <= 80 KB, <= 256 registers per wave)
 constexpr int S_MAX = (GRID_MAX - AW - 1) / 8;
 constexpr int MAXL = 32;
-static_assert(DW + ND == OW && OW + NO == UW && UW + NU == QW && QW + NQ == AW, "roles");
+static_assert(NO + NU + ND + NQ == AW && QW + NQ == AW, "roles");
 static_assert(NQ * 64 == QKVN && NQ * 48 == VOC && NU * 32 == INTER && NO * 32 == H && ND * 19 >= H, "role rows");
 
 template <int CPW>
@@ -59,12 +68,12 @@ struct TLds {
     uint16_t xs[INTER];
     float xr[32];
     float red[4][32];
+    float outv[64];              // QKV / head rows staged for one whole-line publish
     double dscr[8];
     float hs[32];
     // attention
-    float raw[4 * D];
     float q_s[R][D], kn_s[D], vn_s[D];
-    float wred[4][CPW][R];
+    float wred[4][CPW][R], wsum[4][CPW][R];   // per-wave softmax max / sum per chunk
     float mch[CPW][R], lch[CPW][R];   // per-chunk max / sum (split partials)
     float ared[4][CPW][R][D];
     float pl[MAXCH * PSLOT];     // split 0: every chunk's partial, chunk order
@@ -164,8 +173,12 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             acc[j] = group_sum<16>(acc[j]);
-            if (l16 == 0) g_put(p.gqkv + 64 * i + 16 * j + grp, __float_as_uint(acc[j]), X.tag(ph));
+            if (l16 == 0) S.outv[16 * j + grp] = acc[j];
         }
+        __syncthreads();
+        // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four waves
+        // into shared lines make the next edge slower
+        if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
         PROF(ph, 2);
         if (l + 1 < nl) {
             issue_qkv(l + 1);
@@ -200,11 +213,12 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const float lg = group_sum<16>(a0[j]) + group_sum<16>(a1[j]);
-        if (l16 == 0) {
-            const int row = 48 * i + 16 * j + grp;
-            p.logits[row] = lg;   // read after the launch only (host, tests)
-            g_put(p.glog + row, __float_as_uint(lg), X.tag(hph));
-        }
+        if (l16 == 0) S.outv[16 * j + grp] = lg;
+    }
+    __syncthreads();
+    if (t < 48) {
+        g_put(p.glog + 48 * i + t, __float_as_uint(S.outv[t]), X.tag(hph));
+        p.logits[48 * i + t] = S.outv[t];   // read after the launch only (host, tests)
     }
     PROF(hph, 2);
 }
@@ -400,7 +414,9 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
     if (myc == 0) return;                           // (uniform over the workgroup)
     const int j0 = c0 * CHK;
     const bool has_pos = pos / CHK >= c0 && pos / CHK < c0 + CPW;
-    const int gi = t < 128 ? g * 256 + 2 * t : t < 192 ? NH * D + g * D + 2 * (t - 128) : (NH + NKV) * D + g * D + 2 * (t - 192);
+    // wave v polls elements lane and lane + 64 of its head (q head 2g, q head 2g+1, k, v of group g): the pair its
+    // head norm and NEOX RoPE work on (no LDS staging or barrier before the norm)
+    const int gi = (wave == 0 ? g * 256 : wave == 1 ? g * 256 + D : wave == 2 ? NH * D + g * D : (NH + NKV) * D + g * D) + lane;
     uint4 kr[NP], vr[NP];
     float hn[2];
     auto issue = [&](int l) {   // this split's cached K/V rows (clamped rows re-read row pos) + head-norm weights
@@ -421,26 +437,25 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
     for (int l = 0; l < nl; ++l) {
         const int ph = 5 * l + 1;
         const size_t kvo = (size_t)l * p.kv_layer + (size_t)g * p.n_ctx * D;
+        float xr[2];
         {
             uint32_t u[2];
             PROF(ph, 0);
-            g_wait<2>(p.gqkv + gi, X.tag(5 * l), u, X.c);
+            g_wait<2, 64>(p.gqkv + gi, X.tag(5 * l), u, X.c);
             PROF(ph, 1);
-            S.raw[2 * t] = __uint_as_float(u[0]);
-            S.raw[2 * t + 1] = __uint_as_float(u[1]);
+            xr[0] = __uint_as_float(u[0]);
+            xr[1] = __uint_as_float(u[1]);
         }
-        __syncthreads();
         {   // wave v: q head 0 / q head 1 / k (head norm + RoPE) / v (f16 rounding)
             const int v = wave;
             if (v == 3) {
 #pragma unroll
-                for (int e = 0; e < 2; ++e) S.vn_s[lane + 64 * e] = f16r(S.raw[3 * D + lane + 64 * e]);
+                for (int e = 0; e < 2; ++e) S.vn_s[lane + 64 * e] = f16r(xr[e]);
             } else {
-                const float *src = S.raw + v * D;
                 float xx[2];
                 double ss = 0.0;
 #pragma unroll
-                for (int e = 0; e < 2; ++e) { xx[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(xx[e], xx[e]); }
+                for (int e = 0; e < 2; ++e) { xx[e] = xr[e]; ss += (double)__fmul_rn(xx[e], xx[e]); }
                 ss = wave_sum_d(ss);
                 const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
 #pragma unroll
@@ -510,7 +525,6 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
 #pragma unroll
                 for (int h = 0; h < R; ++h) S.mch[cc][h] = M[cc][h];
         }
-        __syncthreads();
         PROF(200 + l, 1);   // (development timeline: scores + max done)
 #pragma unroll
         for (int cc = 0; cc < CPW; ++cc) {
@@ -526,7 +540,7 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                     lsum += pr[q][h];
                 }
                 lsum = rows_sum(lsum);
-                if (lane == 0) S.wred[wave][cc][h] = lsum;
+                if (lane == 0) S.wsum[wave][cc][h] = lsum;
             }
             float acc[R][8];
 #pragma unroll
@@ -566,7 +580,7 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
         if (nch == 1) {   // one chunk: k_attn's single-split output
             if (t < R * D / 2) {
                 const int h = t / (D / 2), d = 2 * (t % (D / 2));
-                const float lsum = (S.wred[0][0][h] + S.wred[1][0][h]) + (S.wred[2][0][h] + S.wred[3][0][h]);
+                const float lsum = (S.wsum[0][0][h] + S.wsum[1][0][h]) + (S.wsum[2][0][h] + S.wsum[3][0][h]);
                 const float a0 = (S.ared[0][0][h][d] + S.ared[1][0][h][d]) + (S.ared[2][0][h][d] + S.ared[3][0][h][d]);
                 const float a1 = (S.ared[0][0][h][d + 1] + S.ared[1][0][h][d + 1]) + (S.ared[2][0][h][d + 1] + S.ared[3][0][h][d + 1]);
                 g_put(gout + t, (uint32_t)f2h(a0 / lsum) | ((uint32_t)f2h(a1 / lsum) << 16), X.tag(ph));
@@ -581,7 +595,7 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                     g_put(mine + t, __float_as_uint(av), X.tag(ph));
                     if (t < PSLOT - R * D) {
                         const int hh = t % R;
-                        const float lsum = (S.wred[0][cc][hh] + S.wred[1][cc][hh]) + (S.wred[2][cc][hh] + S.wred[3][cc][hh]);
+                        const float lsum = (S.wsum[0][cc][hh] + S.wsum[1][cc][hh]) + (S.wsum[2][cc][hh] + S.wsum[3][cc][hh]);
                         const float v = t < R ? S.mch[cc][hh] : t < 2 * R ? lsum : 0.0f;
                         g_put(mine + R * D + t, __float_as_uint(v), X.tag(ph));
                     }
@@ -593,48 +607,60 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                     pl[cc * PSLOT + t] = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
                     if (t < R) {
                         pl[cc * PSLOT + R * D + t] = S.mch[cc][t];
-                        pl[cc * PSLOT + R * D + R + t] = (S.wred[0][cc][t] + S.wred[1][cc][t]) + (S.wred[2][cc][t] + S.wred[3][cc][t]);
+                        pl[cc * PSLOT + R * D + R + t] = (S.wsum[0][cc][t] + S.wsum[1][cc][t]) + (S.wsum[2][cc][t] + S.wsum[3][cc][t]);
                     }
                 }
                 const int n = (nch - CPW) * PSLOT;
                 PROF(200 + l, 3);   // (development timeline: own partials staged, remote ones polled next)
-                for (int i0 = 4 * t; i0 < n; i0 += 1024) {
-                    uint32_t u4[4];
-                    g_wait<4>(gp + CPW * PSLOT + i0, X.tag(ph), u4, X.c);
+                // every remote partial in one sweep per 3,072 granules (granule t + 256 k of each thread, all loads
+                // issued before any tag is checked)
+                for (int r0 = 0; r0 < n; r0 += 256 * 12) {
+                    uint64_t v[12];
+                    unsigned it = 0;
+                    const uint64_t *gb = gp + CPW * PSLOT;
+                    while (true) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) pl[CPW * PSLOT + i0 + q] = __uint_as_float(u4[q]);
-                }
-                __syncthreads();
-                if (t < R) {
-                    float mx = -INFINITY;
-                    for (int s2 = 0; s2 < nch; ++s2) mx = fmaxf(mx, pl[s2 * PSLOT + R * D + t]);
-                    float lt = 0.0f;
-                    for (int s2 = 0; s2 < nch; ++s2)
-                        lt = __fmaf_rn(pl[s2 * PSLOT + R * D + R + t], expf(pl[s2 * PSLOT + R * D + t] - mx), lt);
-                    S.cm[t] = mx;
-                    S.cl[t] = lt;
-                }
-                __syncthreads();
-                for (int i = t; i < nch * R; i += 256) {
-                    const int s2 = i / R, h = i % R;
-                    S.sw[s2][h] = expf(pl[s2 * PSLOT + R * D + h] - S.cm[h]);
-                }
-                __syncthreads();
-                if (t < R * D / 2) {
-                    const int h = t / (D / 2), d = 2 * (t % (D / 2));
-                    float a2[2];
+                        for (int k = 0; k < 12; ++k) v[k] = g_ld(gb + min(r0 + 256 * k + t, n - 1));
+                        bool ok = true;
 #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        float av = 0.0f;
-                        for (int s2 = 0; s2 < nch; ++s2) av = __fmaf_rn(pl[s2 * PSLOT + h * D + d + q], S.sw[s2][h], av);
-                        a2[q] = av;
+                        for (int k = 0; k < 12; ++k) ok &= r0 + 256 * k + t >= n || (uint32_t)(v[k] >> 32) == X.tag(ph);
+                        if (ok || X.c.abort) break;
+                        if ((++it & 255u) == 0 && (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                                                   it >= SPIN_LIMIT)) {
+                            X.c.abort = true;
+                            __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
                     }
-                    g_put(gout + t, (uint32_t)f2h(a2[0] / S.cl[h]) | ((uint32_t)f2h(a2[1] / S.cl[h]) << 16), X.tag(ph));
+#pragma unroll
+                    for (int k = 0; k < 12; ++k)
+                        if (r0 + 256 * k + t < n) pl[CPW * PSLOT + r0 + 256 * k + t] = __uint_as_float((uint32_t)v[k]);
+                }
+                __syncthreads();
+                // k_attn's combine, one output per thread (head t / 128, dimension t % 128), each thread deriving its
+                // head's max / sum / weights itself (the same expressions in the same order: no further barriers)
+                {
+                    const int h = t / D, d = t % D;
+                    float mx = -INFINITY;
+#pragma unroll 8
+                    for (int s2 = 0; s2 < nch; ++s2) mx = fmaxf(mx, pl[s2 * PSLOT + R * D + h]);
+                    float lt = 0.0f, av = 0.0f;
+#pragma unroll 8
+                    for (int s2 = 0; s2 < nch; ++s2) {
+                        const float sw = expf(pl[s2 * PSLOT + R * D + h] - mx);
+                        lt = __fmaf_rn(pl[s2 * PSLOT + R * D + R + h], sw, lt);
+                        av = __fmaf_rn(pl[s2 * PSLOT + h * D + d], sw, av);
+                    }
+                    const uint32_t o = f2h(av / lt);
+                    const uint32_t o1 = dpp_u<DPP_XOR1>(o);   // dimension d + 1 (lane ^ 1)
+                    if ((t & 1) == 0) g_put(gout + t / 2, o | (o1 << 16), X.tag(ph));
                 }
             }
         }
         PROF(ph, 2);
-        // the next layer's K/V rows, a layer ahead of their use (after the combine: its polls would wait behind them)
+        // the next layer's K/V rows, a layer ahead of their use (after the combine: its polls would wait behind them;
+        // issued once the O projection is done instead, the stream landed late: 0.484 vs 0.464 ms at position 500)
         if (l + 1 < nl) issue(l + 1);
     }
 }
@@ -691,9 +717,9 @@ __global__ void __launch_bounds__(256, 2) k_tk_roles(const PersistParams p) {
     if (t < p.n_layers) S.layers[t] = p.L[t];
     __syncthreads();
     const int sel_w = AW + 8 * p.roles_split;
-    if (w < OW) tk_dn(X);
-    else if (w < UW) tk_o(X);
-    else if (w < QW) tk_gu(X);
+    if (w >= OW && w < OW + NO) tk_o(X);
+    else if (w >= UW && w < UW + NU) tk_gu(X);
+    else if (w >= DW && w < DW + ND) tk_dn(X);
     else if (w < AW) tk_qkv(X);
     else if (w < sel_w) tk_att(X);
     else tk_sel(X);

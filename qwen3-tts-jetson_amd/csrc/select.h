@@ -15,6 +15,10 @@ namespace q3t {
 
 constexpr int SEL_VPT_MAX = 16;   // V <= 4096
 
+#ifndef SEL_STAMP
+#define SEL_STAMP(k) ((void)0)   // development hook (tools/dev/selbench.hip): stage timestamps of one selection
+#endif
+
 constexpr int SEL_CAND = 256;     // boundary-bin candidate list of the top-k threshold search
 
 struct alignas(16) SelLds {
@@ -26,6 +30,8 @@ struct alignas(16) SelLds {
     unsigned ures[4];
     unsigned sres[2];
     float wsum[4];
+    float rmax[4], rmin[4];   // sel_kth_largest_range's wave max / min (apart from fred: CB0's block max reads fred
+                              // right before it, so its first barrier is not needed)
     unsigned last;
 };
 
@@ -215,14 +221,16 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
             mx = fmaxf(mx, v[e]);
             if (v[e] > -INFINITY) mn = fminf(mn, v[e]);
         }
+    // (no barrier ahead of these writes: rmax / rmin / hist are read only inside this call, and every caller runs a
+    // workgroup barrier between two selections)
     S.hist[t] = 0u;   // 256 bins, one per thread
     mx = wave_max(mx);
     mn = -wave_max(-mn);
+    if (lane == 0) { S.rmax[wave] = mx; S.rmin[wave] = mn; }
     __syncthreads();
-    if (lane == 0) { S.fred[wave] = mx; S.wsum[wave] = mn; }
-    __syncthreads();
-    mx = fmaxf(fmaxf(S.fred[0], S.fred[1]), fmaxf(S.fred[2], S.fred[3]));
-    mn = fminf(fminf(S.wsum[0], S.wsum[1]), fminf(S.wsum[2], S.wsum[3]));
+    mx = fmaxf(fmaxf(S.rmax[0], S.rmax[1]), fmaxf(S.rmax[2], S.rmax[3]));
+    mn = fminf(fminf(S.rmin[0], S.rmin[1]), fminf(S.rmin[2], S.rmin[3]));
+    SEL_STAMP(1);
     *vmax = mx;
     const float range = mx - mn;
     if (!(range > 0.0f) || !(range < INFINITY)) return sel_kth_largest(v, n, vpt, k, S);   // uniform
@@ -237,6 +245,7 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
         }
     }
     __syncthreads();
+    SEL_STAMP(2);
     if (wave == 0) {
         // lane l owns bins 255-4l .. 252-4l (descending), so the inclusive lane scan counts keys from the top
         const uint4 h4 = *reinterpret_cast<const uint4 *>(&S.hist[252 - 4 * lane]);
@@ -255,6 +264,7 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
         }
     }
     __syncthreads();
+    SEL_STAMP(3);
     const unsigned bstar = S.sres[0];
     if (bstar == 0xFFFFFFFFu) return -INFINITY;   // fewer than k finite values: the k-th largest is -inf
     const int kk = k - (int)S.sres[1];
@@ -265,6 +275,7 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
             if (i < SEL_CAND) S.cand[i] = sel_fkey(v[e]);
         }
     __syncthreads();
+    SEL_STAMP(4);
     const unsigned nc = S.ncand;
     if (nc > SEL_CAND) return sel_kth_largest(v, n, vpt, k, S);   // uniform
     if (nc <= 64) {
@@ -286,9 +297,8 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
         if (gt < (unsigned)kk && (unsigned)kk <= gt + eq) S.sres[0] = me;
     }
     __syncthreads();
-    const uint32_t r = S.sres[0];
-    __syncthreads();
-    return sel_keyf(r);
+    SEL_STAMP(5);
+    return sel_keyf(S.sres[0]);   // (sres is written again only by the next selection, behind the caller's barrier)
 }
 
 // temperature -> top-k -> keep_id restored -> exp -> inverse CDF with u (v is modified)
@@ -329,13 +339,15 @@ __device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vp
         v[e] = in ? expf(v[e] - m) : 0.0f;
         loc += v[e];
     }
+    SEL_STAMP(6);
     // block exclusive scan of the per-thread sums (index order)
     const int lane = t & 63, wave = t >> 6;
     const float incl = wave_scan_incl_f(loc);
-    __syncthreads();
+    // (wsum / ures[0] are last read behind a barrier of this selection's threshold search, or of the previous selection)
     if (lane == 63) S.wsum[wave] = incl;
     if (t == 0) S.ures[0] = 0x7fffffffu;
     __syncthreads();
+    SEL_STAMP(7);
     float wpre = 0.0f, total = 0.0f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) { if (w < wave) wpre += S.wsum[w]; total += S.wsum[w]; }
@@ -350,6 +362,7 @@ __device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vp
     }
     if (found != 0x7fffffff) atomicMin(reinterpret_cast<int *>(&S.ures[0]), found);
     __syncthreads();
+    SEL_STAMP(8);
     const int r = (int)S.ures[0];
     return r == 0x7fffffff ? n - 1 : r;
 }

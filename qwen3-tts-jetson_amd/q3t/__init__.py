@@ -67,6 +67,7 @@ _lib.q3t_synchronize.argtypes = [_P]
 _lib.q3t_last_timing.argtypes = [_P, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.q3t_time_stage.argtypes = [_P, _I, _I, _I, _I, C.POINTER(C.c_double)]
 _lib.q3t_persist_status.argtypes = [_P]
+_lib.q3t_persist_kernels.argtypes = [_P]
 if hasattr(_lib, "q3t_debug_read"):   # development builds only (make -C csrc DEV=1)
     _lib.q3t_debug_read.argtypes = [_P, _I, _P, C.c_size_t]
 _lib.q3t_vocoder_num_samples.restype = C.c_int64
@@ -98,7 +99,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_generate_queue", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
+           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_persist_kernels", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_vocoder_decode_batch", "q3t_vocoder_set_batch_frames", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
            "q3t_tokenizer_decode", "q3t_talker_forward", "q3t_talker_prefill",
@@ -325,6 +326,11 @@ class Engine:
         """-1: single-slot path runs launch-per-phase; 0: persistent launches in use; 1: one flagged a hand-off
         fault; 2: persistent launches disabled after a fault (bit-identical launch-per-op graphs in use)."""
         return _lib.q3t_persist_status(self.h)
+
+    def persist_kernels(self):
+        """bit mask of the single-slot persistent kernels in use: 1 talker roles (persist_tk.hip), 2 talker all-role
+        (persist.hip), 4 code-predictor roles (persist_cp.hip), 8 code-predictor all-role (persist.hip)"""
+        return _lib.q3t_persist_kernels(self.h)
 
     def debug_read(self, which, nbytes):
         """development builds only: raw bytes of a device state buffer (0 K, 1 V cache, 2 QKV, 3 attention, 5 timeline)"""

@@ -33,7 +33,7 @@ pytestmark = pytest.mark.gpu
 NF = 512            # bench.py --frames default
 MAX_CTX = 544       # bench.py: max(frames, roofline_pos) + 32
 TAIL = 64           # frames checked at the end of each run
-MM_MAX_OFF = 0.06
+MM_MAX_OFF = 0.035   # observed 0.2-2.9 % at the bench depths (round 3); the gate follows the observation
 
 
 @pytest.fixture(scope="module")
@@ -48,7 +48,7 @@ def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max
     nf = out.shape[0]
     kw = dict(force_frames=nf, temperature=temperature, top_k=50, seed=seed, utt=utt)
     if max_off is None:
-        max_off = 0.03 if temperature <= 0 else 0.05
+        max_off = 0.03 if temperature <= 0 else 0.035
     res = []
     if head:   # frames [0, TAIL): the oracle replays the prefix only (max_len = TAIL: no early-stop semantics)
         res.append(check_decisions(orc, toks, spk, out[:TAIL], max_len=TAIL, max_off_frac=max_off, **kw))

@@ -27,7 +27,7 @@ from q3t_testutil import REPO, check_decisions, prompt, rel_err, synth_dir
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
 TOL = 5e-3          # talker hidden / logits, relative max-abs (test_gpu_parity.py, full model)
-MM_MAX_OFF = 0.06   # near-tie decision fraction on the matrix-core path (test_gpu_mfma.py header)
+MM_MAX_OFF = 0.035  # near-tie decision fraction on the matrix-core path (observed <= 2.9 %)
 
 
 def _env_engine(env, *a, **kw):
@@ -70,7 +70,7 @@ def test_b1_generate_at_bench_lengths(full, nf, temperature):
         # the mass (320 frames: 85 / 5120), so a 32-frame sample needs a 5 % bound; the 5e-2 per-decision bound holds
         n_off, n_dec, worst = check_decisions(orc, toks, spk, out, max_len=nf, force_frames=nf,
                                               temperature=temperature, top_k=50, seed=77, utt=0,
-                                              max_off_frac=0.03 if temperature <= 0 else 0.05)
+                                              max_off_frac=0.03 if temperature <= 0 else 0.035)
         print(f"B=1 {nf} frames T={temperature}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g} "
               f"(oracle {time.time() - t0:.1f} s)")
         assert eng.persist_status() == 0
@@ -163,6 +163,6 @@ def test_vocoder_full_512_frames(full):
         rms = float(np.sqrt(np.mean((g - o) ** 2)))
         print(f"FULL 512 frames: {g.shape[0]} samples, max|d|={err:.3e} rms={rms:.3e} (oracle {time.time() - t0:.1f} s)")
         assert g.shape == o.shape
-        assert err < 1e-2 and rms < 2e-3
+        assert err < 6e-3 and rms < 2e-3   # observed max 3.8e-3
     finally:
         eng.close()

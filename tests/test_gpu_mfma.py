@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
 TOL = {"tiny": 3e-3, "full": 5e-3}
 LOGIT_TOL = {"tiny": 5e-2, "full": 8e-2}
-MAX_OFF = 0.06   # near-tie decision fraction (see the header)
+MAX_OFF = 0.035  # near-tie decision fraction (see the header; observed <= 2.9 % at the bench depths)
 
 
 @pytest.fixture(scope="module", params=["tiny", "full"])

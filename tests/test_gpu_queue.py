@@ -25,7 +25,7 @@ from q3t_testutil import REPO, check_decisions, prompt, synth_dir
 
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
-MM_MAX_OFF = 0.06   # near-tie decision fraction on the matrix-core path (test_gpu_mfma.py header)
+MM_MAX_OFF = 0.035  # near-tie decision fraction on the matrix-core path (observed <= 2.9 %)
 
 
 @pytest.fixture(scope="module")

@@ -14,7 +14,7 @@ from q3t_testutil import REPO, synth_dir
 
 sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
-PCM_TOL = {"tiny": 1e-2, "full": 1e-2}   # measured max |dPCM| 3.7e-3 / 3.6e-3, rms <= 7e-4
+PCM_TOL = {"tiny": 6e-3, "full": 6e-3}   # measured max |dPCM| 3.7e-3 / 3.6e-3 (3.8e-3 at 512 frames), rms <= 7e-4
 
 
 @pytest.fixture(scope="module", params=["tiny", "full"])

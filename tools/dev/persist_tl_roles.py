@@ -53,3 +53,12 @@ for lab, r in rows.items():
     print(f"{lab:8s} " + " ".join(f"{v:8.2f}" for v in m) + f"  {len(a)}")
 ends = [stamps(ps * PPH + 25, "ATT", 2).max() for ps in range(1, 16)]
 print(f"per-pass span (selection to selection) {np.mean(np.diff(ends)):.2f} us; total steps {tot:.1f} us; last selection {ends[-1]:.1f} us")
+# selection split (ATT workgroups: [1] logits arrived, [3] token selected, [2] committed / published)
+a, b, c = [], [], []
+for ps in range(1, 16):
+    h = ps * PPH + 25
+    for w in ROLES["ATT"]:
+        if T[w, h, 1] >= 0 and T[w, h, 3] >= 0 and T[w, h, 2] >= 0:
+            a.append(T[w, h, 3] - T[w, h, 1]); b.append(T[w, h, 2] - T[w, h, 3])
+if a:
+    print(f"selection: select_token_pre {np.median(a):.2f} us, commit + publish {np.median(b):.2f} us (median over passes x 8)")

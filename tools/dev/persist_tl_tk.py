@@ -9,7 +9,7 @@ S = int(sys.argv[2])
 t0 = T[T > 0].min()
 T = np.where(T > 0, T - t0, -1) * 10e-3
 AW = 248
-ROLES = {"DN": range(0, 56), "O": range(56, 88), "GU": range(88, 184), "QKV": range(184, 248),
+ROLES = {"O": range(0, 32), "GU": range(32, 128), "DN": range(128, 184), "QKV": range(184, 248),
          "ATT": range(AW, AW + 8 * S), "ATT0": range(AW, AW + 8), "SEL": range(AW + 8 * S, AW + 8 * S + 1)}
 NL = 28
 role_of_k = {0: "QKV", 1: "ATT", 2: "O", 3: "GU", 4: "DN"}
