@@ -98,7 +98,9 @@ def cpu_baseline(tts, tok, prompt, frames, vocoder_mode, gpu):
                       "gpu_rtf": round(gpu["cfg0_rtf"], 5), "rtf_ratio": round(rtf0 / gpu["cfg0_rtf"], 1)},
             sample=f"prefill + {r['n']} frames + vocoder of {r['n']} frames, then one {cfg0}-frame utterance end to "
                    f"end ({r['wall']:.1f} s of CPU work): t_prefill {r['t_prefill']:.2f}s, {r['t_frame'] * 1e3:.1f} "
-                   f"ms/frame, vocoder {r['t_voc'] * 1e3:.1f} ms/frame, extrapolated to {frames} frames")
+                   f"ms/frame, vocoder {r['t_voc'] * 1e3:.1f} ms/frame, extrapolated to {frames} frames (the CPU's "
+                   f"per-frame attention grows with the KV position: a {r['n']}-frame sample undercounts it at positions "
+                   f"up to {frames + len(prompt)}, so the extrapolated CPU time, and the GPU/CPU ratio, are conservative)")
     r4 = res[4]
     return {"value": r4["value"], "unit": "frames/s", "cores": 4, "kind": "port", "rtf": r4["rtf"],
             "decode_only": r4["decode_only"], "vocoder_only": r4["vocoder_only"], "configs0": r4["configs0"],
