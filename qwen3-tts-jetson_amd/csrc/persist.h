@@ -46,6 +46,7 @@ struct PersistParams {
     // hand-off state (persist_alloc)
     uint64_t *gx = nullptr, *gx2 = nullptr, *gqkv = nullptr, *gattn = nullptr, *gh = nullptr;
     uint64_t *gpart = nullptr;     // [8][32][264] attention split partials (granules)
+    uint64_t *gop = nullptr;       // [4][1024] O-projection K-slice partial rows (granules, persist_tk.hip)
     uint64_t *gtok = nullptr;      // [16] code-predictor tokens of the launch (granules)
     uint64_t *glog = nullptr;      // [3072] head logits (granules): the selecting workgroup gathers them
     const uint16_t *const *heads = nullptr;   // code-predictor frame: device array of the 15 lm_heads

@@ -676,7 +676,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
 }
 
 struct StateLayout {
-    size_t gx, gx2, gqkv, gattn, gh, part, gpart, gtok, glog, ctr, total;
+    size_t gx, gx2, gqkv, gattn, gh, part, gpart, gop, gtok, glog, ctr, total;
     StateLayout() {
         size_t o = 0;
         auto take = [&](size_t b) { const size_t r = o; o += (b + 255) & ~(size_t)255; return r; };
@@ -687,6 +687,7 @@ struct StateLayout {
         gh = take(INTER / 2 * 8);
         part = take((size_t)NKV * MAXSPLIT * R * (D + 2) * 4);
         gpart = take((size_t)NKV * MAXSPLIT * PSLOT * 8);
+        gop = take((size_t)4 * H * 8);
         gtok = take(16 * 8);
         glog = take(VOC * 8);
         ctr = take(64 * 4);
@@ -758,6 +759,7 @@ void persist_carve(uint8_t *base, PersistParams &p) {
     p.gh = reinterpret_cast<uint64_t *>(base + L.gh);
     p.part = reinterpret_cast<float *>(base + L.part);
     p.gpart = reinterpret_cast<uint64_t *>(base + L.gpart);
+    p.gop = reinterpret_cast<uint64_t *>(base + L.gop);
     p.gtok = reinterpret_cast<uint64_t *>(base + L.gtok);
     p.glog = reinterpret_cast<uint64_t *>(base + L.glog);
     unsigned *ctr = reinterpret_cast<unsigned *>(base + L.ctr);

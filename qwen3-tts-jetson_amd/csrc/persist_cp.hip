@@ -31,6 +31,10 @@
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_WAIT
+#define Q3T_CP_WAIT g_wait   // development: g_wait_gated
+#endif
+
 namespace q3t {
 
 namespace {
@@ -117,7 +121,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             } else {
                 uint32_t u[4];
                 PROF(ph, 0);
-                g_wait<4>(p.gx + 4 * t, X.tag(ph_of(pass, l - 1, 4)), u, X.c);
+                Q3T_CP_WAIT<4>(p.gx + 4 * t, X.tag(ph_of(pass, l - 1, 4)), u, X.c);
                 PROF(ph, 1);
                 x = f4_of(u);
             }
@@ -149,7 +153,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
         const int hph = ph_of(pass, NLC, 0);
         uint32_t u[4];
         PROF(hph, 0);
-        g_wait<4>(p.gx + 4 * t, X.tag(ph_of(pass, NLC - 1, 4)), u, X.c);
+        Q3T_CP_WAIT<4>(p.gx + 4 * t, X.tag(ph_of(pass, NLC - 1, 4)), u, X.c);
         PROF(hph, 1);
         rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
         __syncthreads();
@@ -210,7 +214,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             } else {
                 uint32_t u[2];
                 PROF(ph, 0);
-                g_wait<2, 64>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
+                Q3T_CP_WAIT<2, 64>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
                 PROF(ph, 1);
                 xr[0] = __uint_as_float(u[0]);
                 xr[1] = __uint_as_float(u[1]);
@@ -371,7 +375,7 @@ __device__ __forceinline__ void role_o(Ctx &X) {
             }
             uint32_t u[4];
             PROF(ph, 0);
-            g_wait<4>(p.gattn + 4 * t, X.tag(ph_of(pass, l, 1)), u, X.c);
+            Q3T_CP_WAIT<4>(p.gattn + 4 * t, X.tag(ph_of(pass, l, 1)), u, X.c);
             PROF(ph, 1);
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
             __syncthreads();
@@ -427,7 +431,7 @@ __device__ __forceinline__ void role_gu(Ctx &X) {
             const int ph = ph_of(pass, l, 3);
             uint32_t u[4];
             PROF(ph, 0);
-            g_wait<4>(p.gx2 + 4 * t, X.tag(ph_of(pass, l, 2)), u, X.c);
+            Q3T_CP_WAIT<4>(p.gx2 + 4 * t, X.tag(ph_of(pass, l, 2)), u, X.c);
             PROF(ph, 1);
             rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
             __syncthreads();
@@ -491,7 +495,7 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
             }
             uint32_t u[6];
             PROF(ph, 0);
-            g_wait<6>(p.gh + 6 * t, X.tag(ph_of(pass, l, 3)), u, X.c);
+            Q3T_CP_WAIT<6>(p.gh + 6 * t, X.tag(ph_of(pass, l, 3)), u, X.c);
             PROF(ph, 1);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);

@@ -49,15 +49,16 @@ struct Ctl {
     bool abort;
 };
 
-// spin until granules base[0..N) all carry `tag`; payloads to out.  Bounded: after SPIN_LIMIT polls (or once any
-// workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch drain.
-template <int N, int STRIDE = 1>
+// spin until granules base[(i / RUN) * STRIDE + i % RUN], i in [0, N), all carry `tag`; payloads to out.  Bounded:
+// after SPIN_LIMIT polls (or once any workgroup has flagged a timeout) the wait gives up, sets *err and lets the launch
+// drain.
+template <int N, int STRIDE = 1, int RUN = 1>
 __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
     uint64_t v[N];
     unsigned it = 0;
     while (true) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) v[i] = g_ld(base + i * STRIDE);
+        for (int i = 0; i < N; ++i) v[i] = g_ld(base + (i / RUN) * STRIDE + i % RUN);
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < N; ++i) ok &= (uint32_t)(v[i] >> 32) == tag;
@@ -77,6 +78,29 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];
+}
+
+// g_gate: lane 0 of each wave polls one granule alone (one 8-B load per poll) until it carries `tag`.  g_wait_gated:
+// g_wait behind the gate on the wave's first granule: lane 0 first polls it alone, then the wave sweeps all N.  For long waits of many granules per thread, whose sweeps would otherwise flood
+// the CU's memory path for the whole wait (a co-resident workgroup's stores then stalled for ~230 us).
+__device__ __forceinline__ void g_gate(const uint64_t *g, uint32_t tag, Ctl &c) {
+    if ((threadIdx.x & 63) == 0) {
+        unsigned it = 0;
+        while (!c.abort && (uint32_t)(g_ld(g) >> 32) != tag) {
+            if ((++it & 255u) == 0 && (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                                       it >= SPIN_LIMIT)) {
+                c.abort = true;
+                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    c.abort = __shfl(c.abort ? 1 : 0, 0) != 0;
+}
+template <int N, int STRIDE = 1, int RUN = 1>
+__device__ __forceinline__ void g_wait_gated(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
+    g_gate(base, tag, c);
+    g_wait<N, STRIDE, RUN>(base, tag, out, c);
 }
 
 __device__ __forceinline__ float4 f4_of(const uint32_t (&u)[4]) {

@@ -4,15 +4,23 @@
 // step, whose attention reads a growing HBM-resident KV cache.
 //
 //   role (workgroups)        per layer                                           input edge
-//   O    [0, 32)             32 O-projection rows + residual                      attn   8 -> 32
-//   GU   [32, 128)           RMSNorm(ffn_norm) + 32 gate/up SwiGLU units          x'     32 -> 96
-//   DN   [128, 184)          18-19 down rows + residual                           h      96 -> 56
+//   O    [0, 32)             K slice w = i >> 3 (kv groups 2w, 2w + 1): the      partials 2S -> 32
+//                            combine of their split partials in split order,
+//                            then 128 O-projection rows (row block i & 7) over
+//                            the slice's 512 columns (k_gemv's wave w sum)
+//   GU   [32, 128)           x' = x + (((o0 + o1) + o2) + o3); RMSNorm(ffn_norm)  o      32 -> 96
+//                            + 32 gate/up SwiGLU units
+//   DN   [128, 184)          18-19 down rows + residual x'                        h      96 -> 56
 //   QKV  [184, 248)          RMSNorm(attn_norm) + 64 QKV rows (4 x 16); codec     x      DN 56 -> 64
 //                            head 48 rows (3 x 16) after the last layer
 //   ATT  [248, 248 + 8S)     kv group g, split s: positions [64 s, 64 s + 64)     QKV    ~8 -> S per group
-//                            (S = ceil(n_ctx / 64)); split 0 combines every
-//                            split's partial in split order
+//                            (S = ceil(n_ctx / 64)): the chunk's partial
 //   SEL  248 + 8S            CB0 selection of the next frame                      logits QKV 64 -> 1
+//
+// No workgroup combines the splits on its own: each O workgroup combines the two kv groups its K slice reads (k_attn's
+// combine, one output per thread and group), so the attention reaches the O projection in one hand-off, not two.  The
+// O projection's four per-wave K-slice sums (k_gemv<1,1,4,PRO_F16,4>: wave w reduces columns [512 w, 512 w + 512))
+// are computed by four workgroups and summed by their consumers in k_gemv's order, so the step stays bit-identical.
 //
 // Two workgroups per CU (LDS <= 80 KB, <= 256 registers per wave): the grid of up to 505 workgroups is co-resident,
 // so the attention keeps k_attn's split of 64 positions per workgroup (one chunk's body; a workgroup that ran 2-3
@@ -45,6 +53,9 @@ constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of pos
 #ifndef Q3T_TK_PAIR
 #define Q3T_TK_PAIR 0   // development: 0 = O, gate/up, down, QKV (the splits beside O); 1 = down, O, gate/up, QKV
 #endif
+#ifndef Q3T_TK_WAIT_ATT
+#define Q3T_TK_WAIT_ATT g_wait   // development: g_wait_gated
+#endif
 #if Q3T_TK_PAIR == 0
 constexpr int OW = 0, NO = 32;       // O rows 32 (8 x 4)
 constexpr int UW = 32, NU = 96;      // gate/up units 32 (2 x 16)
@@ -68,7 +79,7 @@ struct TLds {
     uint16_t xs[INTER];
     float xr[32];
     float red[4][32];
-    float outv[64];              // QKV / head rows staged for one whole-line publish
+    float outv[128];             // QKV / head / O rows staged for one whole-line publish
     double dscr[8];
     float hs[32];
     // attention
@@ -76,8 +87,6 @@ struct TLds {
     float wred[4][CPW][R], wsum[4][CPW][R];   // per-wave softmax max / sum per chunk
     float mch[CPW][R], lch[CPW][R];   // per-chunk max / sum (split partials)
     float ared[4][CPW][R][D];
-    float pl[MAXCH * PSLOT];     // split 0: every chunk's partial, chunk order
-    float cm[R], cl[R], sw[MAXCH][R];
     SelLds sel;
     PLayerW layers[MAXL];
 };
@@ -157,7 +166,7 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
         } else {
             uint32_t u[4];
             PROF(ph, 0);
-            g_wait<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u, X.c);
+            g_wait_gated<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u, X.c);
             PROF(ph, 1);
             x = f4_of(u);
         }
@@ -196,7 +205,7 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
     const int hph = 5 * nl;
     uint32_t u[4];
     PROF(hph, 0);
-    g_wait<4>(p.gx + 4 * t, X.tag(5 * (nl - 1) + 4), u, X.c);
+    Q3T_TK_WAIT_ATT<4>(p.gx + 4 * t, X.tag(5 * (nl - 1) + 4), u, X.c);
     PROF(hph, 1);
     rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, i == 0 ? p.hidden : nullptr);
     __syncthreads();
@@ -223,63 +232,115 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
     PROF(hph, 2);
 }
 
-// ------------------------------------------------------------------ O-projection + residual (39-40 rows)
+// ------------------------------------------------------------------ split combine + O-projection K slice (128 rows)
 template <int CPW>
 __device__ __forceinline__ void tk_o(Ctx<CPW> &X) {
+    constexpr int CB = 8;   // chunks per poll sweep
     const PersistParams &p = X.p;
     TLds<CPW> &S = X.S;
-    const int i = blockIdx.x - OW, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15, grp4 = lane >> 4, nl = X.nl;
-    const int lo = i * H / NO, n = (i + 1) * H / NO - lo;
+    const int i = blockIdx.x - OW, w = i >> 3, rb = i & 7, t = threadIdx.x, lane = t & 63, wave = t >> 6, l16 = t & 15,
+              grp4 = lane >> 4, nl = X.nl, nch = X.pos / CHK + 1;
     uint4 wo[8][4];
-    auto issue = [&](int l) {   // row lo + 4j + grp4, K slice = wave (k_gemv<1,1,4,PRO_F16,4>)
+    auto issue = [&](int l) {   // row 128 rb + 32 wave + 4j + grp4, columns of K slice w (k_gemv<1,1,4,PRO_F16,4>)
         const uint16_t *W = S.layers[l].o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint16_t *r = W + (size_t)(lo + min(4 * j + grp4, n - 1)) * (NH * D) + wave * 512 + l16 * 8;
+            const uint16_t *r = W + (size_t)(128 * rb + 32 * wave + 4 * j + grp4) * (NH * D) + w * 512 + l16 * 8;
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt) wo[j][tt] = ld16(r + tt * 128);
         }
     };
+    // split partials of kv groups 2w (sel 0) and 2w + 1 (sel 1): this thread's output is element t of each group
+    // (head r = t >> 7, uniform over a wave; dimension t & 127: granule t of every chunk slot).  Lane j also fetches the
+    // max / sum of head r (granules 256 + r, 258 + r) of chunk j & 31 of group j >> 5, so the chunk weights
+    // expf(m - max), uniform over the wave, are computed once per chunk (one lane each) and read back with readlane
+    const uint64_t *gp0 = p.gpart + (size_t)(2 * w) * MAXCH * PSLOT;
+    const int r = t >> 7, jsel = lane >> 5, jc = lane & 31;
+    const uint64_t *mlp = gp0 + (size_t)jsel * MAXCH * PSLOT + (size_t)min(jc, nch - 1) * PSLOT + R * D + r;
     issue(0);
     for (int l = 0; l < nl; ++l) {
         const int ph = 5 * l + 2;
-        if (t < n) {
-            float xr;
-            if (l == 0) {
-                xr = layer0_x1(p, lo + t);
-            } else {
-                uint32_t u1[1];
-                g_wait<1>(p.gx + lo + t, X.tag(5 * (l - 1) + 4), u1, X.c);
-                xr = __uint_as_float(u1[0]);
-            }
-            S.xr[t] = xr;
-        }
-        uint32_t u[4];
+        const uint32_t want = X.tag(5 * l + 1);
         PROF(ph, 0);
-        g_wait<4>(p.gattn + 4 * t, X.tag(5 * l + 1), u, X.c);
-        PROF(ph, 1);
-        *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
+        if (nch == 1) {   // k_attn's single-split output of the two groups (granule 128 g + t: elements 2t, 2t + 1)
+            uint32_t u[1];
+            Q3T_TK_WAIT_ATT<1>(p.gattn + (size_t)w * 256 + t, want, u, X.c);
+            PROF(ph, 1);
+            *reinterpret_cast<uint32_t *>(S.xs + 2 * t) = u[0];
+        } else {          // k_attn's combine in chunk order (the same expressions as its split combine)
+            float lt[2] = {0.0f, 0.0f}, av[2] = {0.0f, 0.0f}, swl = 0.0f, ll = 0.0f;
+            // the sweeps below behind a one-lane gate on the last chunk's partial: sweeping 18 granules per thread for
+            // the whole wait stalled the co-resident attention workgroup's partial stores by up to 1.7 us
+            g_gate(gp0 + (size_t)(nch - 1) * PSLOT + t, want, X.c);
+            for (int c0 = 0; c0 < nch; c0 += CB) {
+                const int nb = min(CB, nch - c0);
+                uint64_t va[2][CB], vm = 0, vl = 0;
+                unsigned it = 0;
+                while (true) {   // every granule of the sweep issued before any tag is checked
+                    if (c0 == 0) {
+                        vm = g_ld(mlp);
+                        vl = g_ld(mlp + R);
+                    }
+#pragma unroll
+                    for (int sel = 0; sel < 2; ++sel)
+#pragma unroll
+                        for (int k = 0; k < CB; ++k)
+                            va[sel][k] = g_ld(gp0 + (size_t)sel * MAXCH * PSLOT + (size_t)(c0 + min(k, nb - 1)) * PSLOT + t);
+                    bool ok = c0 > 0 || jc >= nch || ((uint32_t)(vm >> 32) == want && (uint32_t)(vl >> 32) == want);
+#pragma unroll
+                    for (int sel = 0; sel < 2; ++sel)
+#pragma unroll
+                        for (int k = 0; k < CB; ++k) ok &= k >= nb || (uint32_t)(va[sel][k] >> 32) == want;
+                    if (ok || X.c.abort) break;
+                    if ((++it & 255u) == 0 && (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                                               it >= SPIN_LIMIT)) {
+                        X.c.abort = true;
+                        __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (c0 == 0) {   // lane j: chunk j & 31 of group j >> 5.  max over the chunks: order-free (expf(m - max)
+                                 // is the same for either zero sign of max), then one expf per chunk
+                    PROF(ph, 1);
+                    const float m = jc < nch ? __uint_as_float((uint32_t)vm) : -INFINITY;
+                    ll = __uint_as_float((uint32_t)vl);
+                    const float mx = group_max<32>(m);
+                    swl = jc < nch ? expf(m - mx) : 0.0f;
+                    PROF(200 + l, 0);   // (development timeline: chunk weights)
+                }
+#pragma unroll
+                for (int k = 0; k < CB; ++k)
+                    if (k < nb)
+#pragma unroll
+                        for (int sel = 0; sel < 2; ++sel) {
+                            const int src = sel * 32 + c0 + k;
+                            const float sw = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(swl), src));
+                            lt[sel] = __fmaf_rn(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(ll), src)), sw, lt[sel]);
+                            av[sel] = __fmaf_rn(__uint_as_float((uint32_t)va[sel][k]), sw, av[sel]);
+                        }
+            }
+            PROF(200 + l, 1);   // (development timeline: wave 0's combine done)
+            S.xs[t] = f2h(av[0] / lt[0]);
+            S.xs[256 + t] = f2h(av[1] / lt[1]);
+        }
         __syncthreads();
+        PROF(ph, 3);   // (development timeline: attention combined)
         float acc[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             acc[j] = 0.0f;
 #pragma unroll
-            for (int tt = 0; tt < 4; ++tt)
-                acc[j] = dot8(wo[j][tt], *reinterpret_cast<const uint4 *>(S.xs + wave * 512 + l16 * 8 + tt * 128), acc[j]);
+            for (int tt = 0; tt < 4; ++tt) acc[j] = dot8(wo[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), acc[j]);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             acc[j] = group_sum<16>(acc[j]);
-            if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+            if (l16 == 0) S.outv[32 * wave + 4 * j + grp4] = acc[j];
         }
         __syncthreads();
-        // one store instruction publishes the workgroup's rows (whole lines from one wave: scattered single-lane
-        // stores from four waves into the same lines made the next edge 2-5 us slower)
-        if (t < n) {
-            const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
-            g_put(p.gx2 + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
-        }
+        // two store instructions (waves 0, 1: whole lines each) publish the slice sums of the 128 rows
+        if (t < 128) g_put(p.gop + (size_t)w * H + 128 * rb + t, __float_as_uint(S.outv[t]), X.tag(ph));
         PROF(ph, 2);
         if (l + 1 < nl) issue(l + 1);
     }
@@ -309,11 +370,25 @@ __device__ __forceinline__ void tk_gu(Ctx<CPW> &X) {
     issue(0);
     for (int l = 0; l < nl; ++l) {
         const int ph = 5 * l + 3;
-        uint32_t u[4];
+        float4 xr;   // the residual stream entering the layer
+        if (l == 0) {
+            xr = layer0_x4(p);
+        } else {
+            uint32_t u4[4];
+            g_wait<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u4, X.c);
+            xr = f4_of(u4);
+        }
+        uint32_t u[16];   // K-slice sums o_w of rows 4t..4t+3 (w = 0..3)
         PROF(ph, 0);
-        g_wait<4>(p.gx2 + 4 * t, X.tag(5 * l + 2), u, X.c);
+        g_wait_gated<16, H, 4>(p.gop + 4 * t, X.tag(5 * l + 2), u, X.c);
         PROF(ph, 1);
-        rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {   // k_gemv's ((w0 + w1) + w2) + w3, then the residual add
+            const float s = ((__uint_as_float(u[e]) + __uint_as_float(u[4 + e])) + __uint_as_float(u[8 + e])) + __uint_as_float(u[12 + e]);
+            x[e] = (e == 0 ? xr.x : e == 1 ? xr.y : e == 2 ? xr.z : xr.w) + s;
+        }
+        rms_to_f16(make_float4(x[0], x[1], x[2], x[3]), nw, p.eps, S.xs, S.dscr, nullptr);
         __syncthreads();
         float a0[2], a1[2], b0[2], b1[2];
 #pragma unroll
@@ -365,14 +440,23 @@ __device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
     issue(0);
     for (int l = 0; l < nl; ++l) {
         const int ph = 5 * l + 4;
-        if (t < n) {
-            uint32_t u1[1];
-            g_wait<1>(p.gx2 + lo + t, X.tag(5 * l + 2), u1, X.c);
-            S.xr[t] = __uint_as_float(u1[0]);
+        if (t < n) {   // x' = x + (((o0 + o1) + o2) + o3) of row lo + t (as the gate/up workgroups)
+            float xr;
+            if (l == 0) {
+                xr = layer0_x1(p, lo + t);
+            } else {
+                uint32_t u1[1];
+                g_wait<1>(p.gx + lo + t, X.tag(5 * (l - 1) + 4), u1, X.c);
+                xr = __uint_as_float(u1[0]);
+            }
+            uint32_t uo[4];
+            g_wait<4, H>(p.gop + lo + t, X.tag(5 * l + 2), uo, X.c);
+            const float s = ((__uint_as_float(uo[0]) + __uint_as_float(uo[1])) + __uint_as_float(uo[2])) + __uint_as_float(uo[3]);
+            S.xr[t] = xr + s;
         }
         uint32_t u[6];
         PROF(ph, 0);
-        g_wait<6>(p.gh + 6 * t, X.tag(5 * l + 3), u, X.c);
+        g_wait_gated<6>(p.gh + 6 * t, X.tag(5 * l + 3), u, X.c);
         PROF(ph, 1);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
@@ -441,7 +525,7 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
         {
             uint32_t u[2];
             PROF(ph, 0);
-            g_wait<2, 64>(p.gqkv + gi, X.tag(5 * l), u, X.c);
+            Q3T_TK_WAIT_ATT<2, 64>(p.gqkv + gi, X.tag(5 * l), u, X.c);
             PROF(ph, 1);
             xr[0] = __uint_as_float(u[0]);
             xr[1] = __uint_as_float(u[1]);
@@ -528,19 +612,21 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
         PROF(200 + l, 1);   // (development timeline: scores + max done)
 #pragma unroll
         for (int cc = 0; cc < CPW; ++cc) {
-            float pr[4][R];
+            float pr[4][R], ls[R];
 #pragma unroll
             for (int h = 0; h < R; ++h) {
-                float lsum = 0.0f;
+                ls[h] = 0.0f;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int pi = 4 * cc + q;
                     const bool ok = j0 + pi * 16 + pg <= pos;
                     pr[q][h] = ok ? expf(__fsub_rn(sc[pi][h], M[cc][h])) : 0.0f;
-                    lsum += pr[q][h];
+                    ls[h] += pr[q][h];
                 }
-                lsum = rows_sum(lsum);
-                if (lane == 0) S.wsum[wave][cc][h] = lsum;
+            }
+            {   // rows_sum of both heads at once: row 0 ends with head 0's (r0 + r1) + (r2 + r3), row 1 with head 1's
+                const float lsum = rows_sum_pair(ls[0], ls[1]);
+                if ((lane & 47) == 0) S.wsum[wave][cc][lane >> 4] = lsum;   // lanes 0, 16
             }
             float acc[R][8];
 #pragma unroll
@@ -566,13 +652,23 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr[q][h], ok ? v8[e] : 0.0f, acc[h][e]);
             }
+            // rows_sum of the 16 accumulators as a reduce-scatter (12 row swaps in place of 32): row k ends with values
+            // k, 4 + k, 8 + k, 12 + k (value n = 8 h + e), each (r0 + r1) + (r2 + r3) as rows_sum
+            float v16[16], c8[8];
 #pragma unroll
-            for (int h = 0; h < R; ++h)
+            for (int n = 0; n < 16; ++n) v16[n] = acc[n >> 3][n & 7];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float av = rows_sum(acc[h][e]);
-                    if (lane < 16) S.ared[wave][cc][h][li * 8 + e] = av;
-                }
+            for (int m = 0; m < 8; ++m) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v16[2 * m]), __float_as_uint(v16[2 * m + 1]), false, false);
+                c8[m] = __uint_as_float((uint32_t)sw[0]) + __uint_as_float((uint32_t)sw[1]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(c8[2 * q]), __float_as_uint(c8[2 * q + 1]), false, false);
+                const float av = __uint_as_float((uint32_t)sw[0]) + __uint_as_float((uint32_t)sw[1]);
+                const int n = 4 * q + (lane >> 4);
+                S.ared[wave][cc][n >> 3][li * 8 + (n & 7)] = av;
+            }
         }
         __syncthreads();
         PROF(200 + l, 2);   // (development timeline: P.V reduced)
@@ -585,82 +681,24 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                 const float a1 = (S.ared[0][0][h][d + 1] + S.ared[1][0][h][d + 1]) + (S.ared[2][0][h][d + 1] + S.ared[3][0][h][d + 1]);
                 g_put(gout + t, (uint32_t)f2h(a0 / lsum) | ((uint32_t)f2h(a1 / lsum) << 16), X.tag(ph));
             }
-        } else {
+        } else {   // this split's chunk partials (acc [2][128], m [2], l [2]) in their chunk slots: the O workgroups combine
             uint64_t *gp = p.gpart + (size_t)g * MAXCH * PSLOT;
-            if (s > 0) {   // publish this split's chunk partials (acc [2][128], m [2], l [2]) in their chunk slots
-                for (int cc = 0; cc < myc; ++cc) {
-                    uint64_t *mine = gp + (size_t)(c0 + cc) * PSLOT;
-                    const int h = t / D, d = t % D;
-                    const float av = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
-                    g_put(mine + t, __float_as_uint(av), X.tag(ph));
-                    if (t < PSLOT - R * D) {
-                        const int hh = t % R;
-                        const float lsum = (S.wsum[0][cc][hh] + S.wsum[1][cc][hh]) + (S.wsum[2][cc][hh] + S.wsum[3][cc][hh]);
-                        const float v = t < R ? S.mch[cc][hh] : t < 2 * R ? lsum : 0.0f;
-                        g_put(mine + R * D + t, __float_as_uint(v), X.tag(ph));
-                    }
-                }
-            } else {       // split 0: its own chunks from LDS, the others' from their granules, combined in chunk order
-                float *pl = S.pl;
-                for (int cc = 0; cc < myc; ++cc) {
-                    const int h = t / D, d = t % D;
-                    pl[cc * PSLOT + t] = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
-                    if (t < R) {
-                        pl[cc * PSLOT + R * D + t] = S.mch[cc][t];
-                        pl[cc * PSLOT + R * D + R + t] = (S.wsum[0][cc][t] + S.wsum[1][cc][t]) + (S.wsum[2][cc][t] + S.wsum[3][cc][t]);
-                    }
-                }
-                const int n = (nch - CPW) * PSLOT;
-                PROF(200 + l, 3);   // (development timeline: own partials staged, remote ones polled next)
-                // every remote partial in one sweep per 3,072 granules (granule t + 256 k of each thread, all loads
-                // issued before any tag is checked)
-                for (int r0 = 0; r0 < n; r0 += 256 * 12) {
-                    uint64_t v[12];
-                    unsigned it = 0;
-                    const uint64_t *gb = gp + CPW * PSLOT;
-                    while (true) {
-#pragma unroll
-                        for (int k = 0; k < 12; ++k) v[k] = g_ld(gb + min(r0 + 256 * k + t, n - 1));
-                        bool ok = true;
-#pragma unroll
-                        for (int k = 0; k < 12; ++k) ok &= r0 + 256 * k + t >= n || (uint32_t)(v[k] >> 32) == X.tag(ph);
-                        if (ok || X.c.abort) break;
-                        if ((++it & 255u) == 0 && (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                                                   it >= SPIN_LIMIT)) {
-                            X.c.abort = true;
-                            __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 12; ++k)
-                        if (r0 + 256 * k + t < n) pl[CPW * PSLOT + r0 + 256 * k + t] = __uint_as_float((uint32_t)v[k]);
-                }
-                __syncthreads();
-                // k_attn's combine, one output per thread (head t / 128, dimension t % 128), each thread deriving its
-                // head's max / sum / weights itself (the same expressions in the same order: no further barriers)
-                {
-                    const int h = t / D, d = t % D;
-                    float mx = -INFINITY;
-#pragma unroll 8
-                    for (int s2 = 0; s2 < nch; ++s2) mx = fmaxf(mx, pl[s2 * PSLOT + R * D + h]);
-                    float lt = 0.0f, av = 0.0f;
-#pragma unroll 8
-                    for (int s2 = 0; s2 < nch; ++s2) {
-                        const float sw = expf(pl[s2 * PSLOT + R * D + h] - mx);
-                        lt = __fmaf_rn(pl[s2 * PSLOT + R * D + R + h], sw, lt);
-                        av = __fmaf_rn(pl[s2 * PSLOT + h * D + d], sw, av);
-                    }
-                    const uint32_t o = f2h(av / lt);
-                    const uint32_t o1 = dpp_u<DPP_XOR1>(o);   // dimension d + 1 (lane ^ 1)
-                    if ((t & 1) == 0) g_put(gout + t / 2, o | (o1 << 16), X.tag(ph));
+            for (int cc = 0; cc < myc; ++cc) {
+                uint64_t *mine = gp + (size_t)(c0 + cc) * PSLOT;
+                const int h = t / D, d = t % D;
+                const float av = (S.ared[0][cc][h][d] + S.ared[1][cc][h][d]) + (S.ared[2][cc][h][d] + S.ared[3][cc][h][d]);
+                g_put(mine + t, __float_as_uint(av), X.tag(ph));
+                if (t < PSLOT - R * D) {
+                    const int hh = t % R;
+                    const float lsum = (S.wsum[0][cc][hh] + S.wsum[1][cc][hh]) + (S.wsum[2][cc][hh] + S.wsum[3][cc][hh]);
+                    const float v = t < R ? S.mch[cc][hh] : t < 2 * R ? lsum : 0.0f;
+                    g_put(mine + R * D + t, __float_as_uint(v), X.tag(ph));
                 }
             }
         }
         PROF(ph, 2);
-        // the next layer's K/V rows, a layer ahead of their use (after the combine: its polls would wait behind them;
-        // issued once the O projection is done instead, the stream landed late: 0.484 vs 0.464 ms at position 500)
+        // the next layer's K/V rows, a layer ahead of their use (issued once the O projection was done instead, the
+        // stream landed late: 0.484 vs 0.464 ms at position 500)
         if (l + 1 < nl) issue(l + 1);
     }
 }

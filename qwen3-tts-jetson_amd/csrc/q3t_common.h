@@ -133,6 +133,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // sum / max over the lanes {l, l^16, l^32, l^48} (same position in the 4 rows), result in every lane
 __device__ __forceinline__ float rows_sum(float v) { v += xrow16(v); return v + xrow32(v); }
 __device__ __forceinline__ float rows_max(float v) { v = fmaxf(v, xrow16(v)); return fmaxf(v, xrow32(v)); }
+// rows_sum of two values in one pass: row 0 (and 2) ends with a's (r0 + r1) + (r2 + r3), row 1 (and 3) with b's
+__device__ __forceinline__ float rows_sum_pair(float a, float b) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b), false, false);
+    const float c = __builtin_bit_cast(float, (unsigned)s[0]) + __builtin_bit_cast(float, (unsigned)s[1]);
+    return c + xrow32(c);
+}
 __device__ __forceinline__ double rows_sum_d(double v) { v += xrow16_d(v); return v + xrow32_d(v); }
 
 // wave inclusive scan (row_shr DPP within rows, row_bcast15/31 across rows: the GCN scan idiom)

@@ -10,7 +10,7 @@ T="timeout -k 10"
 $T 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_persist.py tests/test_gpu_select.py 2>&1 | tail -3 || exit 1
 for v in "" "$@"; do
     echo "== lib ${v:-release}"
-    for a in "0 1 266 50 544" "0 1 500 50 544" "0 1 40 50 544" "1 1 266 50"; do
+    for a in "0 1 266 50 544" "0 1 500 50 544" "0 1 40 50 544" "0 1 1500 30 2048" "1 1 266 50"; do
         Q3T_DEV_LIB=$v $T 60 python3 tools/dev/stage_only.py $a || exit 1
     done
 done

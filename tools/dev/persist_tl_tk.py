@@ -10,7 +10,7 @@ t0 = T[T > 0].min()
 T = np.where(T > 0, T - t0, -1) * 10e-3
 AW = 248
 ROLES = {"O": range(0, 32), "GU": range(32, 128), "DN": range(128, 184), "QKV": range(184, 248),
-         "ATT": range(AW, AW + 8 * S), "ATT0": range(AW, AW + 8), "SEL": range(AW + 8 * S, AW + 8 * S + 1)}
+         "ATT": range(AW, AW + 8 * S), "SEL": range(AW + 8 * S, AW + 8 * S + 1)}
 NL = 28
 role_of_k = {0: "QKV", 1: "ATT", 2: "O", 3: "GU", 4: "DN"}
 
@@ -44,30 +44,35 @@ print(f"{'phase':6s} {'edge_med':>8s} {'edge_max':>8s} {'body_med':>8s} {'step':
 for lab, r in rows.items():
     m = np.nanmean(np.array(r), axis=0)
     print(f"{lab:6s} " + " ".join(f"{v:8.2f}" for v in m) + f"  n={len(r)}")
-# attention split detail: split 0 (combiner) vs others
+# attention split spread and the O workgroups' combine
 for l in [5, 15]:
     ph = 5 * l + 1
-    a0 = T[AW:AW + 8, ph]
-    ao = T[AW + 8:AW + 8 * S, ph]
-    print(f"layer {l} B: split0 arrive {np.median(a0[:,1]):.2f} pub {np.median(a0[:,2]):.2f} max {a0[:,2].max():.2f};"
-          f" others arrive {np.median(ao[ao[:,1]>=0,1]) if (ao[:,1]>=0).any() else -1:.2f} pub {np.median(ao[ao[:,2]>=0,2]) if (ao[:,2]>=0).any() else -1:.2f}"
-          f"; QKV last pub {T[184:248, 5*l, 2].max():.2f}")
+    a = T[AW:AW + 8 * S, ph]
+    o = T[0:32, ph + 1]
+    print(f"layer {l} B: splits arrive {np.median(a[:,1]):.2f} pub med {np.median(a[:,2]):.2f} max {a[:,2].max():.2f}; "
+          f"QKV last pub {T[184:248, 5*l, 2].max():.2f}; O arrive med {np.median(o[:,1]):.2f} combined {np.median(o[:,3]):.2f} pub {np.median(o[:,2]):.2f}")
 print(f"span {T[:, 140, 2].max():.1f} us")
-# attention body split (stamps 200 + l: 0 normed, 1 scores + max, 2 P.V reduced, 3 combine start (split 0))
-segs = {"arrive->norm": [], "norm->scores": [], "scores->pv": [], "pv->pub(others)": [], "pv->combine(s0)": [], "combine->pub(s0)": []}
+# attention body split (stamps 200 + l: 0 normed, 1 scores + max, 2 P.V reduced)
+segs = {"arrive->norm": [], "norm->scores": [], "scores->pv": [], "pv->pub": [], "O arrive->combined": [], "O combined->pub": [],
+        "O arrive->weights": [], "O weights->w0 combine": [], "O w0 combine->barrier": []}
 for l in range(1, NL):
     ph = 5 * l + 1
     for w in ROLES["ATT"]:
-        a, n0, n1, n2, n3, pb = T[w, ph, 1], T[w, 200 + l, 0], T[w, 200 + l, 1], T[w, 200 + l, 2], T[w, 200 + l, 3], T[w, ph, 2]
+        a, n0, n1, n2, pb = T[w, ph, 1], T[w, 200 + l, 0], T[w, 200 + l, 1], T[w, 200 + l, 2], T[w, ph, 2]
         if min(a, n0, n1, n2, pb) < 0:
             continue
         segs["arrive->norm"].append(n0 - a)
         segs["norm->scores"].append(n1 - n0)
         segs["scores->pv"].append(n2 - n1)
-        if w < AW + 8:
-            if n3 >= 0:
-                segs["pv->combine(s0)"].append(n3 - n2)
-                segs["combine->pub(s0)"].append(pb - n3)
-        else:
-            segs["pv->pub(others)"].append(pb - n2)
+        segs["pv->pub"].append(pb - n2)
+    for w in ROLES["O"]:
+        a, c, pb = T[w, ph + 1, 1], T[w, ph + 1, 3], T[w, ph + 1, 2]
+        if min(a, c, pb) >= 0:
+            segs["O arrive->combined"].append(c - a)
+            segs["O combined->pub"].append(pb - c)
+            b0, b1 = T[w, 200 + l, 0], T[w, 200 + l, 1]
+            if min(b0, b1) >= 0:
+                segs["O arrive->weights"].append(b0 - a)
+                segs["O weights->w0 combine"].append(b1 - b0)
+                segs["O w0 combine->barrier"].append(c - b1)
 print("attention body: " + ", ".join(f"{k} {np.median(v):.2f}" for k, v in segs.items() if v))
