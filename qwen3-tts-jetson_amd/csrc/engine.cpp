@@ -126,12 +126,6 @@ T *Engine::dalloc(size_t n) {
     return static_cast<T *>(p);
 }
 
-void Engine::dfree(void *p) {
-    if (!p) return;
-    auto it = std::find(allocs_.begin(), allocs_.end(), p);
-    if (it != allocs_.end()) allocs_.erase(it);
-    hipFree(p);
-}
 
 // the pinned / device scratch of generate() and generate_queue(), kept across calls: a per-call hipFree or
 // hipHostFree would synchronise the whole device (every other context on it included)
@@ -378,7 +372,8 @@ bool Engine::upload_weights(const Gguf &g) {
     tabs16[0] = codec_embd_;
     for (int i = 0; i < 15; ++i) tabs16[1 + i] = cp_embd_[i];
     tabs16_dev_ = dalloc<uint16_t *>(16);
-    Q3T_HIP(hipMemcpy(tabs16_dev_, tabs16.data(), 16 * sizeof(uint16_t *), hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemcpyAsync(tabs16_dev_, tabs16.data(), 16 * sizeof(uint16_t *), hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     // RoPE cos/sin table with ggml_rope_cache_init's f32 recurrence (theta *= theta_scale), NEOX pairs
     rope_len_ = std::max(max_ctx_, 16);
     std::vector<float> rope((size_t)rope_len_ * D);
@@ -392,7 +387,8 @@ bool Engine::upload_weights(const Gguf &g) {
         }
     }
     rope_ = dalloc<float>(rope.size());
-    Q3T_HIP(hipMemcpy(rope_, rope.data(), rope.size() * 4, hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemcpyAsync(rope_, rope.data(), rope.size() * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     return true;
 }
 
@@ -449,13 +445,16 @@ bool Engine::alloc_state() {
     if (!x_ || !kc_ || !vc_ || !recipe_ || !proj_out_) { set_error("device allocation failed"); return false; }
     std::vector<int> cpp((size_t)16 * S);
     for (int p = 0; p < 16; ++p) for (int s = 0; s < S; ++s) cpp[(size_t)p * S + s] = p;
-    Q3T_HIP(hipMemcpy(cp_pos_, cpp.data(), cpp.size() * 4, hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemcpyAsync(cp_pos_, cpp.data(), cpp.size() * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     std::vector<uint64_t> utt(S);
     for (int s = 0; s < S; ++s) utt[s] = (uint64_t)s;
-    Q3T_HIP(hipMemcpy(utt_, utt.data(), S * 8, hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemcpyAsync(utt_, utt.data(), S * 8, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     std::vector<int> iota(S);
     for (int s = 0; s < S; ++s) iota[s] = s;
-    Q3T_HIP(hipMemcpy(slot_iota_, iota.data(), S * 4, hipMemcpyHostToDevice));
+    Q3T_HIP(hipMemcpyAsync(slot_iota_, iota.data(), S * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     return true;
 }
 
@@ -486,7 +485,8 @@ bool Engine::setup_persist() {
             pl[i] = PLayerW{L_[i].qkv, L_[i].o, L_[i].gu, L_[i].down, L_[i].attn_norm, L_[i].ffn_norm, L_[i].qn, L_[i].kn};
         pl_dev_ = dalloc<PLayerW>(pl.size());
         if (!pl_dev_) { set_error("device allocation failed"); return false; }
-        Q3T_HIP(hipMemcpy(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+        Q3T_HIP(hipMemcpyAsync(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
     }
     // the code-predictor frame (persist_cp_frame): its 5 layers and 15 lm_heads
     if (persist_cp_) {
@@ -496,9 +496,11 @@ bool Engine::setup_persist() {
         pl_cp_dev_ = dalloc<PLayerW>(cpl.size());
         heads_dev_ = dalloc<const uint16_t *>(16);
         if (!pl_cp_dev_ || !heads_dev_) { set_error("device allocation failed"); return false; }
-        Q3T_HIP(hipMemcpy(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice));
+        Q3T_HIP(hipMemcpyAsync(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
         std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
-        Q3T_HIP(hipMemcpy(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice));
+        Q3T_HIP(hipMemcpyAsync(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
         // the per-token tables are computed from the weights: a receiving context (replica, non-root rank) builds
         // them once its arena has been filled (finish_weights, after copy_weights_from / the RCCL broadcast)
         if (!wa_.recv && !build_persist_tables()) return false;
@@ -511,11 +513,27 @@ bool Engine::setup_persist() {
 }
 
 // the persistent code-predictor frame's per-token tables
+// No build buffer is freed: hipFree synchronises the whole device, and a replica or shared rank builds its tables while
+// other contexts on the device may be capturing graphs on other threads (the free invalidated those captures).  The
+// token iota (12 KB) is kept; the 1.7B projected rows' scratch (codec_vocab x H f32) is carved from the QKV table,
+// which is written only after the projected table is complete.
 bool Engine::build_persist_tables() {
     if (!persist_cp_ || tables_built_) return true;
-    if (c_.has_mtp && !build_cp_proj_table()) return false;
+    table_iota_ = dalloc<int>(c_.codec_vocab);
+    if (!table_iota_) { set_error("device allocation failed (table token iota)"); return false; }
+    std::vector<int> ih(c_.codec_vocab);
+    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
+    Q3T_HIP(hipMemcpyAsync(table_iota_, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+    Q3T_HIP(hipStreamSynchronize(stream_));
     // (520 MB of f32 for any slot count: a serving context's rare 1-slot calls run the frame with it too)
-    if (opt_.cp_qkv_table && !build_cp_qkv_table()) return false;
+    const int QKV = (cpc_.n_heads + 2 * cpc_.n_kv) * cpc_.head_dim;
+    const bool qkv_ok = opt_.cp_qkv_table && c_.codec_vocab == 3072 && c_.cp_vocab == 2048 && (int)cp_embd_.size() >= 14;
+    if (qkv_ok) {
+        cp_qkvtab_ = dalloc<float>(persist_qkv_table_rows() * QKV);
+        if (!cp_qkvtab_) { set_error("device allocation failed (code-predictor QKV table)"); return false; }
+    }
+    if (c_.has_mtp && !build_cp_proj_table()) return false;
+    if (qkv_ok && !build_cp_qkv_table()) return false;
     tables_built_ = true;
     return true;
 }
@@ -534,14 +552,7 @@ bool Engine::finish_weights() {
 // phase and its all-to-all edge (persist.hip).  520 MB of f32.
 bool Engine::build_cp_qkv_table() {
     const int H = cpc_.hidden, QKV = (cpc_.n_heads + 2 * cpc_.n_kv) * cpc_.head_dim;
-    if (c_.codec_vocab != 3072 || c_.cp_vocab != 2048 || (int)cp_embd_.size() < 14) return true;   // shapes persist.hip supports
-    const size_t rows = persist_qkv_table_rows();
-    cp_qkvtab_ = dalloc<float>(rows * QKV);
-    int *iota = dalloc<int>(c_.codec_vocab);
-    if (!cp_qkvtab_ || !iota) { set_error("device allocation failed (code-predictor QKV table)"); return false; }
-    std::vector<int> ih(c_.codec_vocab);
-    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
-    Q3T_HIP(hipMemcpyAsync(iota, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+    const int *iota = table_iota_;
     size_t row0 = 0;
     for (int t = 0; t < 15; ++t) {
         const int V = t == 0 ? c_.codec_vocab : c_.cp_vocab;
@@ -559,7 +570,6 @@ bool Engine::build_cp_qkv_table() {
         row0 += V;
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
-    dfree(iota);
     return true;
 }
 
@@ -571,12 +581,10 @@ bool Engine::build_cp_proj_table() {
     const int H = c_.hidden, CH = c_.cp_hidden;
     const size_t rows = persist_qkv_table_rows();
     cp_projtab_ = dalloc<float>(rows * CH);
-    int *iota = dalloc<int>(c_.codec_vocab);
-    float *rowbuf = dalloc<float>((size_t)c_.codec_vocab * H);
-    if (!cp_projtab_ || !iota || !rowbuf) { set_error("device allocation failed (code-predictor projected table)"); return false; }
-    std::vector<int> ih(c_.codec_vocab);
-    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
-    Q3T_HIP(hipMemcpyAsync(iota, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+    const int *iota = table_iota_;
+    // scratch rows: the QKV table's first codec_vocab x H floats when it exists (written after this build), else kept
+    float *rowbuf = cp_qkvtab_ ? cp_qkvtab_ : dalloc<float>((size_t)c_.codec_vocab * H);
+    if (!cp_projtab_ || !rowbuf) { set_error("device allocation failed (code-predictor projected table)"); return false; }
     size_t row0 = 0;
     for (int t = 0; t < 15; ++t) {
         const int V = t == 0 ? c_.codec_vocab : c_.cp_vocab;
@@ -593,8 +601,6 @@ bool Engine::build_cp_proj_table() {
         row0 += V;
     }
     Q3T_HIP(hipStreamSynchronize(stream_));
-    dfree(rowbuf);
-    dfree(iota);
     return true;
 }
 
@@ -609,9 +615,8 @@ bool Engine::persist_recover() {
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
     persist_ = persist_cp_ = cp_roles_ = tk_roles_ = false;
-    dfree(cp_qkvtab_);   // the tables serve only the persistent frame
-    dfree(cp_projtab_);
-    cp_qkvtab_ = cp_projtab_ = nullptr;
+    // the tables (serving only the persistent frame) stay allocated until the context is destroyed: a hipFree here
+    // would synchronise the device and invalidate graph captures other contexts' threads have in progress
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
     // (as does the per-op talker step for n_ctx <= 2048), so a re-run regenerates the frames already delivered exactly
     cp_fused_attn_ = false;
@@ -668,8 +673,11 @@ bool Engine::persist_error() {
     if (!persist_enabled() || !pstate_) return false;
     PersistParams p;
     persist_carve(pstate_, p);
+    // on the context's own (non-blocking) stream: a null-stream copy would order against, and break, graph captures
+    // in progress on other threads' streams
     unsigned e = 0;
-    if (hipMemcpy(&e, p.err, 4, hipMemcpyDeviceToHost) != hipSuccess) return true;
+    if (hipMemcpyAsync(&e, p.err, 4, hipMemcpyDeviceToHost, stream_) != hipSuccess || hipStreamSynchronize(stream_) != hipSuccess)
+        return true;
     return e != 0;
 }
 

@@ -220,7 +220,6 @@ private:
     std::vector<void *> allocs_;
     WeightArena wa_;
     template <class T> T *dalloc(size_t n);
-    void dfree(void *p);   // free a dalloc allocation early (one-off build buffers)
 
     // weights
     std::vector<DevLayer> L_, CP_;
@@ -277,6 +276,7 @@ private:
     bool cp_roles_ = false;    // the 1-slot code-predictor frame runs persist_cp.hip
     bool tk_roles_ = false;    // the 1-slot talker step runs persist_tk.hip
     uint8_t *pstate_ = nullptr;
+    int *table_iota_ = nullptr;   // 0..codec_vocab-1: the table builds' token ids
     uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline
 
     bool enqueue_cp_only(int S, hipStream_t s) { return enqueue_cp_frame(S, s); }
