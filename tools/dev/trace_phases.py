@@ -6,13 +6,15 @@ import csv
 import re
 import sys
 
-TALKER_KERNELS = int(sys.argv[2]) if len(sys.argv) > 2 else 141
 rows = []
 with open(sys.argv[1]) as f:
     for r in csv.DictReader(f):
         n = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void q3t::", "").replace("q3t::", "")
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), n, r["Grid_Size_X"], r["Grid_Size_Y"]))
 rows.sort()
+# the 1-slot talker step is ONE persistent launch when the persistent kernels run (k_tk_roles / k_persist<0, *>)
+persistent = any(n.startswith(("k_tk_roles", "k_persist<0")) for _, _, n, _, _ in rows)
+TALKER_KERNELS = int(sys.argv[2]) if len(sys.argv) > 2 else (1 if persistent else 141)
 frames, cur = [], []
 for row in rows:
     if row[2] == "k_advance":
@@ -20,7 +22,9 @@ for row in rows:
         cur = []
     else:
         cur.append(row)
-frames = [f for f in frames[1:] if len(f) > TALKER_KERNELS]   # first chunk holds prefill/setup kernels
+frames = [f for f in frames[1:] if len(f) > TALKER_KERNELS]
+if persistent:   # the frame loop's first chunk ends in the prefill; every later chunk is [cp frame, talker step]
+    frames = [f for f in frames if len(f) >= 2]   # first chunk holds prefill/setup kernels
 agg = {"cp": collections.defaultdict(list), "talker": collections.defaultdict(list)}
 spans = {"cp": [], "talker": [], "frame": []}
 for f in frames:
