@@ -595,6 +595,8 @@ __global__ void __launch_bounds__(64) k_attn_small(const AttnParams p) {
 // q / k head RMSNorm + NEOX RoPE at the row's position, the F16 K/V rows appended to the cache, explicit KQ, scale,
 // diag_mask_inf, soft_max and KQV per row.  One workgroup per (utterance, kv head) holds the utterance's <= 16 rows of
 // that head group in LDS; the head-norm / RoPE prologue is k_attn's (one wave per vector, the same roundings).
+// 512 threads: the 64 prologue vectors and 32 (row, head) tasks of a 16-row prompt spread over 8 waves (at one
+// workgroup per kv head, 4 waves ran them as a serial chain: 16 us per layer).
 __device__ __forceinline__ float tree16(const float (&v)[16]) {
     float a[8], b[4];
 #pragma unroll
@@ -603,9 +605,10 @@ __device__ __forceinline__ float tree16(const float (&v)[16]) {
     for (int k = 0; k < 4; ++k) b[k] = a[2 * k] + a[2 * k + 1];
     return (b[0] + b[1]) + (b[2] + b[3]);
 }
+constexpr int PF_THREADS = 512;
 template <int D, int R>
-__global__ void __launch_bounds__(256) k_prefill_attn(const PrefillAttnParams p) {
-    constexpr int PMAX = PREFILL_MAX_ROWS, E = D / 64, LPP = D / 8, GROUPS = 256 / LPP;
+__global__ void __launch_bounds__(PF_THREADS) k_prefill_attn(const PrefillAttnParams p) {
+    constexpr int PMAX = PREFILL_MAX_ROWS, E = D / 64, LPP = D / 8, GROUPS = PF_THREADS / LPP, NW = PF_THREADS / 64;
     static_assert(PMAX == 16, "tree16: the decode kernel's first 16 positions");
     __shared__ float q_s[PMAX][R][D];
     __shared__ float k_s[PMAX][D], v_s[PMAX][D];
@@ -613,16 +616,16 @@ __global__ void __launch_bounds__(256) k_prefill_attn(const PrefillAttnParams p)
     const int plen = p.plen, QKV = (p.nH + 2 * p.nKV) * D;
     const size_t head_off = ((size_t)p.slot[u] * p.nKV + g) * p.n_ctx * D;
     // ---- prologue: vectors (row i, v) with v < R the q heads, v == R the k row, v == R + 1 the v row; task
-    // wave + 4k.  Every operand of the wave's tasks is loaded first (one memory round trip instead of one per task:
+    // wave + NW k.  Every operand of the wave's tasks is loaded first (one memory round trip instead of one per task:
     // with one workgroup per kv head the serial loads were ~17 us of an 18 us launch)
-    constexpr int MAXT = (PMAX * (R + 2) + 3) / 4;
+    constexpr int MAXT = (PMAX * (R + 2) + NW - 1) / NW;
     const int ntask = plen * (R + 2);
     float xv[MAXT][E], rc[MAXT], rs[MAXT], qw[E], kw[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) { qw[e] = p.qn[lane + 64 * e]; kw[e] = p.kn[lane + 64 * e]; }
 #pragma unroll
     for (int k = 0; k < MAXT; ++k) {
-        const int task = wave + 4 * k;
+        const int task = wave + NW * k;
         rc[k] = rs[k] = 0.0f;
 #pragma unroll
         for (int e = 0; e < E; ++e) xv[k][e] = 0.0f;
@@ -640,7 +643,7 @@ __global__ void __launch_bounds__(256) k_prefill_attn(const PrefillAttnParams p)
     }
 #pragma unroll
     for (int k = 0; k < MAXT; ++k) {
-        const int task = wave + 4 * k;
+        const int task = wave + NW * k;
         if (task >= ntask) break;
         const int i = task / (R + 2), v = task % (R + 2);
         if (v == R + 1) {
@@ -730,7 +733,7 @@ bool prefill_attn(const PrefillAttnParams &p, hipStream_t s) {
     }
     const dim3 grid(p.n_utt, p.nKV);
     const int R = p.nH / p.nKV;
-#define Q3T_PF_LAUNCH(DD, RR) hipLaunchKernelGGL((k_prefill_attn<DD, RR>), grid, dim3(256), 0, s, p)
+#define Q3T_PF_LAUNCH(DD, RR) hipLaunchKernelGGL((k_prefill_attn<DD, RR>), grid, dim3(PF_THREADS), 0, s, p)
     if (p.D == 128 && R == 2) Q3T_PF_LAUNCH(128, 2);
     else if (p.D == 128 && R == 1) Q3T_PF_LAUNCH(128, 1);
     else if (p.D == 128 && R == 4) Q3T_PF_LAUNCH(128, 4);
