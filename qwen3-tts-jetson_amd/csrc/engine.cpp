@@ -775,6 +775,7 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;
         dn.pro = PRO_F16; dn.x = hmlp; dn.ldx = c.inter;
         dn.parts = parts; dn.ksplit = splitk_for(H, S_main, dn.K); dn.force_mm = force;
+        dn.xcd_slices = true;   // each XCD fetches 1 / ksplit of hmlp (FETCH 1.42x -> 1.06x of the algorithmic bytes)
         if (!gemv(dn, s)) return false;
         const bool last = il + 1 == layers.size();
         if (last && !final_norm) break;   // code-predictor pass 0: only its K/V caches are read afterwards

@@ -109,6 +109,7 @@ struct GemvParams {
     // to parts[z][b][n] (no epilogue); resid_norm() folds them into the residual stream
     float *parts = nullptr;
     int ksplit = 1;
+    bool xcd_slices = false;   // split-K tiles in XCD-aware order (gemm_mfma.hip splitk_tile)
     bool force_mm = false;   // matrix-core path even below gemm_mfma_min_batch() (a single slot reproducing the
                              // per-token arithmetic of a batch that runs there)
     int family_b = 0;        // > 0: kernel family (vector / matrix core) and K split chosen as for a batch of
