@@ -280,18 +280,29 @@ __device__ __forceinline__ void role_att(Ctx &X) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) M[h] = fmaxf(fmaxf(S.wred[0][h], S.wred[1][h]), fmaxf(S.wred[2][h], S.wred[3][h]));
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                pr[h] = ok ? expf(__fsub_rn(sc[h], M[h])) : 0.0f;
-                const float lsum = rows_sum(pr[h]);
-                if (lane == 0) S.wsum[wave][h] = lsum;
+            for (int h = 0; h < 2; ++h) pr[h] = ok ? expf(__fsub_rn(sc[h], M[h])) : 0.0f;
+            {   // rows_sum of both heads at once: row 0 ends with head 0's (r0 + r1) + (r2 + r3), row 1 with head 1's
+                const float lsum = rows_sum_pair(pr[0], pr[1]);
+                if ((lane & 47) == 0) S.wsum[wave][lane >> 4] = lsum;   // lanes 0, 16
             }
+            {   // rows_sum of the 16 products as a reduce-scatter (persist_tk.hip): row k ends with values k, 4 + k,
+                // 8 + k, 12 + k (value n = 8 h + e), each (r0 + r1) + (r2 + r3) as rows_sum
+                float v16[16], c8[8];
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+                for (int n = 0; n < 16; ++n) v16[n] = __fmaf_rn(pr[n >> 3], ok ? v8[n & 7] : 0.0f, 0.0f);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const float a = rows_sum(__fmaf_rn(pr[h], ok ? v8[e] : 0.0f, 0.0f));
-                    if (lane < 16) S.ared[wave][h][li * 8 + e] = a;
+                for (int m = 0; m < 8; ++m) {
+                    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v16[2 * m]), __float_as_uint(v16[2 * m + 1]), false, false);
+                    c8[m] = __uint_as_float((uint32_t)sw[0]) + __uint_as_float((uint32_t)sw[1]);
                 }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(c8[2 * q]), __float_as_uint(c8[2 * q + 1]), false, false);
+                    const float av = __uint_as_float((uint32_t)sw[0]) + __uint_as_float((uint32_t)sw[1]);
+                    const int n = 4 * q + (lane >> 4);
+                    S.ared[wave][n >> 3][li * 8 + (n & 7)] = av;
+                }
+            }
             __syncthreads();
             if (t < 128) {
                 const int h = t / (D / 2), d = 2 * (t % (D / 2));
