@@ -962,7 +962,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         p.qkvtab = cp_qkvtab_;
         p.sel = select_spec(SEL_CP, gp_, 0, 0);
         p.prof = pprof_;
-        if (cp_roles_ && p.qkvtab && !p.xtab) return persist_cp_roles(p, s);
+        if (cp_roles_ && p.qkvtab) return persist_cp_roles(p, s);   // (1.7B: layer 0's residual rows from xtab)
         return persist_cp_frame(p, s);
     }
     const bool fsel_all = fused_select_ && !use_mm(S);

@@ -138,7 +138,7 @@ public:
     bool persist_error();
     bool persist_enabled() const { return persist_ || persist_cp_; }
     int persist_kernels() const {   // q3t_persist_kernels
-        return (persist_ ? (tk_roles_ ? 1 : 2) : 0) | (persist_cp_ ? (cp_roles_ && cp_qkvtab_ && !cp_projtab_ ? 4 : 8) : 0);
+        return (persist_ ? (tk_roles_ ? 1 : 2) : 0) | (persist_cp_ ? (cp_roles_ && cp_qkvtab_ ? 4 : 8) : 0);
     }
     bool persist_fell_back() const { return persist_fallback_; }
 #ifdef Q3T_DEV

@@ -376,7 +376,9 @@ __device__ __forceinline__ void role_o(Ctx &X) {
                         g_wait<1>(p.gtok + pass - 1, X.tag(ph_of(pass - 1, NLC, 0)), u1, X.c);
                         tok = min((int)u1[0], p.sel.V - 1);   // an aborted wait returns a stale payload: keep it in the table
                     }
-                    xr = h2f(S.tabs[pass - 1][(size_t)tok * H + row]);
+                    // 1.7B: the projected f32 row (xtab, the QKV table's row order) instead of the f16 table row
+                    xr = p.xtab ? p.xtab[((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * CPV) + tok) * H + row]
+                                : h2f(S.tabs[pass - 1][(size_t)tok * H + row]);
                 } else {
                     uint32_t u1[1];
                     g_wait<1>(p.gx + row, X.tag(ph_of(pass, l - 1, 4)), u1, X.c);
@@ -569,7 +571,7 @@ bool persist_cp_roles_resident(int device) {
 
 bool persist_cp_roles(const PersistParams &p, hipStream_t s) {
     if (!p.L || p.n_layers != NLC || !p.heads || !p.logits || !p.rope || !p.x_in || !p.gs.tok || !p.gs.tabs || !p.qkvtab ||
-        p.xtab || !p.gx || p.sel.mode != SEL_CP || p.sel.V != CPV) {
+        !p.gx || p.sel.mode != SEL_CP || p.sel.V != CPV) {
         set_error("persist_cp_roles: bad parameters");
         return false;
     }

@@ -138,6 +138,7 @@ def test_full17_persistent_code_predictor_bit_exact():
     eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=64)
     try:
         assert eng.persist_status() == 0 and ref.persist_status() == -1
+        assert eng.persist_kernels() & 4, eng.persist_kernels()   # the role-specialised frame (persist_cp.hip)
         H = eng.cfg["hidden"]
         rng = np.random.default_rng(9)
         for frame in range(6):
