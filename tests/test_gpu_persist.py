@@ -63,6 +63,31 @@ def test_talker_step_bit_exact(engines):
     assert ep.persist_status() == 0
 
 
+def test_talker_step_bit_exact_role_kernel_long_context():
+    """the role-specialised step (persist_tk.hip) at max_ctx 2048: up to 32 attention chunks, so the O workgroups'
+    combine runs several poll sweeps (8 chunks each) -- positions on both sides of every sweep boundary, bit-exact
+    against the launch-per-op graph (unwritten cache positions are zero in both contexts)"""
+    tts, tok = synth_dir("full")
+    ep = _engine(tts, None, True, max_slots=1, max_ctx=2048)
+    eg = _engine(tts, None, False, max_slots=1, max_ctx=2048)
+    try:
+        assert ep.persist_kernels() & 1, ep.persist_kernels()   # k_tk_roles
+        H = ep.cfg["hidden"]
+        rng = np.random.default_rng(23)
+        bad = []
+        for pos in (0, 1, 63, 64, 65, 300, 511, 512, 513, 575, 1023, 1024, 1500, 1535, 1536, 2000, 2046, 2047):
+            e = (rng.standard_normal(H) * 0.5).astype(np.float32)
+            hp, lp = ep.talker_forward(e[None], [pos])
+            hg, lg = eg.talker_forward(e[None], [pos])
+            if not (np.array_equal(hp, hg) and np.array_equal(lp, lg)):
+                bad.append((pos, float(np.abs(hp - hg).max()), float(np.abs(lp - lg).max())))
+        assert not bad, (len(bad), bad[:8])
+        assert ep.persist_status() == 0
+    finally:
+        ep.close()
+        eg.close()
+
+
 @pytest.mark.parametrize("temperature", [0.0, 0.9])
 def test_cp_frame_bit_exact(engines, temperature):
     """the 16-pass code-predictor frame as one persistent launch vs 16 x (5 layers + head + selection) launches"""
