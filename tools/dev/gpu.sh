@@ -56,6 +56,7 @@ phases)
     S=$(find "$P" -name '*kernel_stats.csv' | head -1)
     python3 "$R/tools/dev/prof_stats.py" "$T" > "$R/gpurun_out/prof_${TAG}_summary.txt"
     python3 "$R/tools/dev/trace_phases.py" "$T" > "$R/gpurun_out/phases_${TAG}.txt"
+    cp "$T" "$R/gpurun_out/trace_${TAG}.csv"
     cp "$S" "$R/gpurun_out/prof_${TAG}_kernel_stats.csv"
     rm -rf "$P"
     head -30 "$R/gpurun_out/prof_${TAG}_summary.txt" ;;

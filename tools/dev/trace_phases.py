@@ -22,6 +22,8 @@ for row in rows:
         cur = []
     else:
         cur.append(row)
+print(f"({len(rows)} kernels, {sum(1 for r in rows if r[2] == 'k_advance')} k_advance, {len(frames)} chunks, "
+      f"persistent={persistent}, chunk sizes {[len(f) for f in frames[:6]]})")
 frames = [f for f in frames[1:] if len(f) > TALKER_KERNELS]
 if persistent:   # the frame loop's first chunk ends in the prefill; every later chunk is [cp frame, talker step]
     frames = [f for f in frames if len(f) >= 2]   # first chunk holds prefill/setup kernels
