@@ -27,6 +27,15 @@
 // K/V append (no head consumes its output).
 #include "persist.h"
 #include "persist_dev.h"
+#ifdef Q3T_DEV
+// development timeline: the selection's stage stamps (select.h SEL_STAMP) in phase slots 440.. of the profile rows
+namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
+#define SEL_STAMP(k)                                                                                              \
+    do {                                                                                                          \
+        if (threadIdx.x == 0 && q3t::g_selprof)                                                                   \
+            q3t::g_selprof[((size_t)blockIdx.x * PROF_PH + 440 + ((k) >> 2)) * 4 + ((k) & 3)] = wall_clock64();   \
+    } while (0)
+#endif
 #include "select.h"
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
@@ -544,6 +553,9 @@ __global__ void __launch_bounds__(256) k_cp_roles(const PersistParams p) {
     CLds &S = *reinterpret_cast<CLds *>(smem);
     const int t = threadIdx.x, w = blockIdx.x;
     Ctx X{p, S, Ctl{p.err, false}, __hip_atomic_load(p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)};
+#ifdef Q3T_DEV
+    if (w == 0 && t == 0) g_selprof = p.prof;
+#endif
     // pointer tables in LDS: a pointer fetched from global memory inside the chain would make the next wait cover every
     // weight stream in flight (vmcnt order)
     if (t < NLC) S.layers[t] = p.L[t];

@@ -62,3 +62,9 @@ for ps in range(1, 16):
             a.append(T[w, h, 3] - T[w, h, 1]); b.append(T[w, h, 2] - T[w, h, 3])
 if a:
     print(f"selection: select_token_pre {np.median(a):.2f} us, commit + publish {np.median(b):.2f} us (median over passes x 8)")
+# selection stage stamps of the last pass (development builds: select.h SEL_STAMP -> phase slots 440..442)
+st = T[64:72, 440:443].reshape(8, -1)
+if (st[:, 1:9] >= 0).all():
+    names = ["minmax", "hist", "bin", "cand", "rank", "exp", "scan", "pick"]
+    rel = np.median(st[:, 1:9] - st[:, 1:2], axis=0)
+    print("selection stages (us after minmax): " + ", ".join(f"{n} {v:.2f}" for n, v in zip(names[1:], rel[1:])))
