@@ -46,12 +46,14 @@ using namespace pdev;
 constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, VOC = 3072;
 constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of positions; partial granules; gpart slots
 // Workgroups b and b + 256 share a CU (observed dispatch, tools/dev/cuprobe.hip; speed only, never correctness): the
-// attention splits >= 1 (workgroups 256..) sit beside the O-projection workgroups (then gate/up), whose weight stream
-// (issued right after their phase) has landed long before the next attention, and the splits issue their own next-layer
-// K/V rows only once the O projection is done.  Beside the QKV workgroups, which issue the next layer's rows right at
-// the QKV -> attention edge, a split's poll arrived 2.3 us late; beside the down workgroups 0.7 us.
+// attention splits >= 1 (workgroups 256..) sit beside the down workgroups, then (splits >= 8) the O workgroups.  The
+// down workgroups' weight stream (issued right after their phase) has landed long before the next attention, and
+// their wait during the attention is a one-lane gate.  With the O workgroups beside the splits instead, the O
+// workgroups' combine sweeps shared the CU with the partials' producers: 0.385 vs 0.376 ms at position 266, 0.392 vs
+// 0.382 at 500, 0.480 vs 0.476 at 1500.  Beside the QKV workgroups, which issue the next layer's rows right at the
+// QKV -> attention edge, a split's poll arrived 2.3 us late (round 4, before the gated polls).
 #ifndef Q3T_TK_PAIR
-#define Q3T_TK_PAIR 0   // development: 0 = O, gate/up, down, QKV (the splits beside O); 1 = down, O, gate/up, QKV
+#define Q3T_TK_PAIR 1   // development: 0 = O, gate/up, down, QKV; 1 = down, O, gate/up, QKV (the splits beside down)
 #endif
 #ifndef Q3T_TK_WAIT_ATT
 #define Q3T_TK_WAIT_ATT g_wait   // development: g_wait_gated

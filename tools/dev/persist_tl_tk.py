@@ -1,5 +1,5 @@
 """dev: offline report of the role-specialised talker step's timeline (persist_tk.hip; raw dump of
-tools/dev/persist_dump.py 0 TAG POS CTX).  usage: persist_tl_tk.py FILE.npy NSPLIT"""
+tools/dev/persist_dump.py 0 TAG POS CTX).  usage: persist_tl_tk.py FILE.npy NSPLIT [PAIR]"""
 import sys
 
 import numpy as np
@@ -9,7 +9,10 @@ S = int(sys.argv[2])
 t0 = T[T > 0].min()
 T = np.where(T > 0, T - t0, -1) * 10e-3
 AW = 248
-ROLES = {"O": range(0, 32), "GU": range(32, 128), "DN": range(128, 184), "QKV": range(184, 248),
+# role layout of persist_tk.hip (Q3T_TK_PAIR = 1: down, O, gate/up, QKV; a third argument 0 = the other layout)
+PAIR = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+OR, GR, DR = (range(56, 88), range(88, 184), range(0, 56)) if PAIR else (range(0, 32), range(32, 128), range(128, 184))
+ROLES = {"O": OR, "GU": GR, "DN": DR, "QKV": range(184, 248),
          "ATT": range(AW, AW + 8 * S), "SEL": range(AW + 8 * S, AW + 8 * S + 1)}
 NL = 28
 role_of_k = {0: "QKV", 1: "ATT", 2: "O", 3: "GU", 4: "DN"}
@@ -48,7 +51,7 @@ for lab, r in rows.items():
 for l in [5, 15]:
     ph = 5 * l + 1
     a = T[AW:AW + 8 * S, ph]
-    o = T[0:32, ph + 1]
+    o = T[list(OR), ph + 1]
     print(f"layer {l} B: splits arrive {np.median(a[:,1]):.2f} pub med {np.median(a[:,2]):.2f} max {a[:,2].max():.2f}; "
           f"QKV last pub {T[184:248, 5*l, 2].max():.2f}; O arrive med {np.median(o[:,1]):.2f} combined {np.median(o[:,3]):.2f} pub {np.median(o[:,2]):.2f}")
 print(f"span {T[:, 140, 2].max():.1f} us")
