@@ -514,7 +514,8 @@ __global__ void __launch_bounds__(64) k_attn_small(const AttnParams p) {
     }
     // head RMSNorm + NEOX RoPE of the 2 q heads and the new k, the new v f16-rounded (k_attn arithmetic)
     const int QKV = (p.nH + 2 * p.nKV) * D;
-    const float *qkv = p.qkv + (size_t)slot * QKV;
+    const float *qkv = p.qkv_tab ? p.qkv_tab + (p.tab_row0 + (size_t)p.tab_tok[(size_t)slot * p.tab_ld + p.tab_col]) * QKV
+                                 : p.qkv + (size_t)slot * QKV;
     const float *rope = p.rope + (size_t)pos * D;
     float xs[4][2];
 #pragma unroll

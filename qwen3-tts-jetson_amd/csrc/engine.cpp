@@ -83,6 +83,7 @@ Options Options::from_env() {
     o.cp_fused_attn = env_flag("Q3T_CP_FUSED_ATTN", true);
     o.cp_qkv_table = env_flag("Q3T_CP_QKV_TABLE", true);
     o.cp_roles = env_flag("Q3T_CP_ROLES", true);
+    o.mm_cp_table = env_flag("Q3T_MM_CP_TABLE", true);
     o.tk_roles = env_flag("Q3T_TK_ROLES", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
@@ -721,7 +722,8 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
                              unsigned *ticket, hipStream_t s, const StackInput *in0, const float *final_norm,
-                             float *final_side, int S_main = 0, bool cp_attn = false, const PrefillAttnParams *pf = nullptr) {
+                             float *final_side, int S_main = 0, bool cp_attn = false, const PrefillAttnParams *pf = nullptr,
+                             const AttnParams *l0tab = nullptr) {
     // S_main: the batch whose kernel choices this stack reproduces (a continuous-batching admission runs ONE slot
     // with the S_main-slot kernels, so its per-token arithmetic is the batch's)
     if (S_main <= 0) S_main = S;
@@ -739,13 +741,21 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
     rn.nw = layers[0].attn_norm;
     if (!(in0 && in0->prenormed) && !resid_norm(rn, s)) return false;
     rn.xin = nullptr;
+    // the code predictor's <= 16 positions run on k_attn_small, which can read layer 0's raw QKV rows from the per-token
+    // table (l0tab: passes 1..15) instead of a QKV GEMM over xn
+    const bool small = cp_attn && n_ctx <= 16 && D == 128 && c.n_heads == 2 * c.n_kv;
+#ifdef Q3T_NO_SMALL_ATTN
+    const bool use_tab = false;
+#else
+    const bool use_tab = small && l0tab && l0tab->qkv_tab && !pf;
+#endif
     for (size_t il = 0; il < layers.size(); ++il) {
         const DevLayer &l = layers[il];
         GemvParams g;
         g.W = l.qkv; g.N = QKV; g.K = H; g.B = S;
         g.pro = PRO_F16; g.x = xn; g.ldx = H;
         g.out_f32 = qkv; g.ldo = QKV; g.force_mm = force;
-        if (!gemv(g, s)) return false;
+        if (!(il == 0 && use_tab) && !gemv(g, s)) return false;
         AttnParams a;
         a.qkv = qkv; a.qn = l.qn; a.kn = l.kn; a.eps = c.eps; a.rope = rope; a.pos = pos;
         a.kc = kc + il * kv_layer; a.vc = vc + il * kv_layer;
@@ -753,7 +763,11 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         a.max_splits = max_splits;   // chunk 128 measured no faster at 64 slots (1.79 vs 1.77 ms per step)
         a.seqk = S_main >= 16 && !attn_split;   // enough (slot, kv head) pairs to fill the chip
         // the code predictor's <= 16 positions: one wave per (slot, kv head) (the 0.6B head layout)
-        a.small = cp_attn && n_ctx <= 16 && D == 128 && c.n_heads == 2 * c.n_kv;
+        a.small = small;
+        if (il == 0 && use_tab) {
+            a.qkv_tab = l0tab->qkv_tab; a.tab_tok = l0tab->tab_tok; a.tab_ld = l0tab->tab_ld; a.tab_col = l0tab->tab_col;
+            a.tab_row0 = l0tab->tab_row0;
+        }
 #ifdef Q3T_NO_SMALL_ATTN
         a.small = 0;   // experiment builds: the code predictor on k_attn_seq / k_attn as before
 #endif
@@ -1000,9 +1014,17 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         }
         const bool mm = use_mm(S);
         if (mm) {
+            // passes 1..15: layer 0's raw QKV rows from the per-token table (the 0.6B layout; the table's rows are the
+            // 1-slot GEMV's, within the batched family's f32 tolerance of its MFMA GEMM)
+            AttnParams l0;
+            if (p >= 1 && cp_qkvtab_ && !c_.has_mtp) {
+                l0.qkv_tab = cp_qkvtab_; l0.tab_tok = tokens_; l0.tab_ld = 16; l0.tab_col = p - 1;
+                l0.tab_row0 = p == 1 ? 0 : (size_t)c_.codec_vocab + (size_t)(p - 2) * c_.cp_vocab;
+            }
             if (!decoder_stack_mm(cpc_, opt_.attn_split, CP_, S, cpx_, xn_, parts_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, &in0,
-                                  p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_, true))
+                                  p == 0 ? nullptr : cp_out_norm_, nullptr, policy_slots_, true, nullptr,
+                                  opt_.mm_cp_table ? &l0 : nullptr))
                 return false;
         } else if (!decoder_stack(cpc_, CP_, S, cpx_, qkv_, attn_, hmlp_, cpkc_, cpvc_, kv_layer, 16, 1,
                                   cp_pos_ + (size_t)p * max_slots_, rope_, part_, ticket_, s, c_.has_mtp ? nullptr : &in0,

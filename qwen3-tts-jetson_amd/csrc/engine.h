@@ -62,6 +62,7 @@ struct Options {
     bool persist = true, persist_cp = true, cp_fused_attn = true, fused_select = true, defer_cp_select = true;
     bool cp_qkv_table = true;   // Q3T_CP_QKV_TABLE: the persistent code-predictor frame reads layer 0's QKV rows from a table
     bool cp_roles = true;       // Q3T_CP_ROLES: that frame on role-specialised workgroups (persist_cp.hip)
+    bool mm_cp_table = true;    // Q3T_MM_CP_TABLE: batched code predictor, layer 0 of passes 1..15 from the QKV table
     bool tk_roles = true;       // Q3T_TK_ROLES: the 1-slot talker step on role-specialised workgroups (persist_tk.hip)
     bool attn_split = false;
     unsigned persist_fault_at = 0;

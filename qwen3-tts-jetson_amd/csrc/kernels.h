@@ -143,6 +143,12 @@ struct AttnParams {
     unsigned *ticket = nullptr;   // [S][nKV] arrival counters, zero between launches
     uint16_t *out = nullptr;      // [S][nH*D] f16 (rounded attention output, the O-proj input)
     float *dbg = nullptr;         // development dump (slot 0, kv group 5, split 0)
+    // k_attn_small only: slot s's raw QKV row is the per-token table row qkv_tab[tab_row0 + tab_tok[s * tab_ld +
+    // tab_col]] (the code predictor's layer 0 of passes 1..15, Engine::build_cp_qkv_table) instead of qkv[s]
+    const float *qkv_tab = nullptr;
+    const int *tab_tok = nullptr;
+    int tab_ld = 0, tab_col = 0;
+    size_t tab_row0 = 0;
 };
 bool attn_decode(const AttnParams &p, hipStream_t s);
 constexpr int ATTN_CHUNK = 64;
