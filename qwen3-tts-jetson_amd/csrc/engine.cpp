@@ -773,6 +773,8 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
 #endif
         a.part = part; a.ticket = ticket; a.out = attn;
         if (pf ? !prefill_layer_attn(*pf, c, l, qkv, rope, a.kc, a.vc, n_ctx, attn, s) : !attn_decode(a, s)) return false;
+        // code-predictor pass 0 (no head): its last layer's K/V rows, appended above, are all that is ever read
+        if (il + 1 == layers.size() && !final_norm) break;
         GemvParams o;
         o.W = l.o; o.N = H; o.K = c.n_heads * D; o.B = S;
         o.pro = PRO_F16; o.x = attn; o.ldx = c.n_heads * D;
