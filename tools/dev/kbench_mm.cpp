@@ -59,25 +59,31 @@ int main(int argc, char **argv) {
     float *x = dev<float>((size_t)B * 4096, 1.0f), *nw = dev<float>(4096, 1.0f);
     float *out = dev<float>((size_t)B * 8192, 0.0f), *resid = dev<float>((size_t)B * 4096, 1.0f);
     uint16_t *xh = dev<uint16_t>((size_t)B * 4096, 1.0f), *oh = dev<uint16_t>((size_t)B * 8192, 0.0f);
-    struct Shape { const char *name; int N, K, pro, act; };
+    float *parts = dev<float>((size_t)4 * B * 8192, 0.0f);
+    struct Shape { const char *name; int N, K, pro, act, ks = 0; };
     const Shape shapes[] = {{"qkv  N4096 K1024 RMS", 4096, 1024, PRO_RMS, ACT_NONE},
                             {"gu   N6144 K1024 RMS+SwiGLU", 6144, 1024, PRO_RMS, ACT_SWIGLU},
                             {"o    N1024 K2048 F16+res", 1024, 2048, PRO_F16, ACT_NONE},
                             {"down N1024 K3072 F16+res", 1024, 3072, PRO_F16, ACT_NONE},
                             {"head N2048 K1024 RMS", 2048, 1024, PRO_RMS, ACT_NONE},
                             {"qkv  N4096 K1024 F16", 4096, 1024, PRO_F16, ACT_NONE},
-                            {"gu   N6144 K1024 F16+SwiGLU", 6144, 1024, PRO_F16, ACT_SWIGLU}};
+                            {"gu   N6144 K1024 F16+SwiGLU", 6144, 1024, PRO_F16, ACT_SWIGLU},
+                            {"qkv  N4096 K1024 F16 split-K 2", 4096, 1024, PRO_F16, ACT_NONE, 2},
+                            {"qkv  N4096 K1024 F16 split-K 4", 4096, 1024, PRO_F16, ACT_NONE, 4},
+                            {"o    N1024 K2048 F16 split-K 4", 1024, 2048, PRO_F16, ACT_NONE, 4},
+                            {"down N1024 K3072 F16 split-K 4", 1024, 3072, PRO_F16, ACT_NONE, 4}};
     for (const Shape &sh : shapes) {
         std::vector<uint16_t *> W(NC);
         for (int c = 0; c < NC; ++c) W[c] = dev<uint16_t>((size_t)sh.N * sh.K, 0.05f);
-        for (int dbg : {0, 1, 2, 3}) {
+        for (int dbg : {0, 3}) {
             const double us = time_graph(NC, [&](int i) {
                 GemvParams p;
                 p.W = W[i % NC]; p.N = sh.N; p.K = sh.K; p.B = B; p.pro = sh.pro; p.act = sh.act; p.dbg = dbg;
                 p.nw = nw; p.eps = 1e-6f;
                 if (sh.pro == PRO_F16) {
                     p.x = xh; p.ldx = sh.K;
-                    if (sh.N == 1024) { p.resid = resid; p.ldr = sh.N; p.out_f32 = resid; }
+                    if (sh.N == 1024 && !sh.ks) { p.resid = resid; p.ldr = sh.N; p.out_f32 = resid; }
+                    if (sh.ks) { p.parts = parts; p.ksplit = sh.ks; }
                 }
                 else { p.x = x; p.ldx = sh.K; }
                 if (sh.act == ACT_SWIGLU) { p.out_f16 = oh; p.ldo = sh.N / 2; }
