@@ -718,6 +718,7 @@ static bool prefill_layer_attn(const PrefillAttnParams &pf, const Config &c, con
     return prefill_attn(q, s);
 }
 
+static const bool g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return !e || std::atoi(e) != 0; }();
 static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
@@ -781,6 +782,10 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         o.parts = parts; o.ksplit = splitk_for(H, S_main, o.K); o.force_mm = force;
         if (!gemv(o, s)) return false;
         rn.parts = parts; rn.ksplit = o.ksplit; rn.nw = l.ffn_norm; rn.side = nullptr;
+        // the talker's weights stream from HBM each step: the norm before a projection touches that projection's lines
+        // (the code predictor's 157 MB stay in the Infinity Cache across its 16 passes anyway)
+        const bool pf_w = !cp_attn && g_mm_prefetch;
+        rn.prefetch = pf_w ? l.gu : nullptr; rn.prefetch_bytes = (size_t)2 * c.inter * H * 2;
         if (!resid_norm(rn, s)) return false;
         GemvParams gu;
         gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
@@ -798,7 +803,9 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         rn.parts = parts; rn.ksplit = dn.ksplit;
         rn.nw = last ? (final_norm ? final_norm : l.ffn_norm) : layers[il + 1].attn_norm;
         rn.side = last ? final_side : nullptr;
+        rn.prefetch = pf_w && !last ? layers[il + 1].qkv : nullptr; rn.prefetch_bytes = (size_t)QKV * H * 2;
         if (!resid_norm(rn, s)) return false;
+        rn.prefetch = nullptr;
     }
     return true;
 }

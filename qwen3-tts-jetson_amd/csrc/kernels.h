@@ -194,6 +194,10 @@ struct ResidNorm {
     uint16_t *xn = nullptr;
     float *side = nullptr;
     int S = 0, H = 0;
+    // optional: extra workgroups touch one dword of every 128-B line of the NEXT projection's weights (up to 256 MB)
+    // while the token rows normalise, so the lines are in the Infinity Cache when that GEMM streams them
+    const void *prefetch = nullptr;
+    size_t prefetch_bytes = 0;
 };
 bool resid_norm(const ResidNorm &r, hipStream_t s);
 

@@ -165,23 +165,38 @@ void launch_sample_topk_f32(const float *logits, const float *rand_val, int32_t 
 
 // ------------------------------------------------------------------------------------------ batched residual + norm
 // one workgroup per token; thread t owns elements 4t .. 4t+3 (H <= 1024).  Partial slabs are added in slice order;
-// the RMS sum runs in double over the block (gemv.hip / gemm_mfma.hip prologue numerics).
+// the RMS sum runs in double over the block (gemv.hip / gemm_mfma.hip prologue numerics).  KS (the slab count) is a
+// template argument so the x and slab loads issue back to back: with a runtime count each sat in its own branch and
+// waited for its own round trip.
+// Workgroups past the S token rows only prefetch (ResidNorm::prefetch): global->LDS dword loads, one per 128-B line
+// of the next projection's weights, which leave no register to wait on; the lines land in the Infinity Cache.
+constexpr int RN_PF_LINES = 2;   // prefetched lines per thread
+template <int KS>
 __global__ void __launch_bounds__(256) k_resid_norm(const ResidNorm r) {
     __shared__ double scr[4];
     const int b = blockIdx.x, t = threadIdx.x, k = 4 * t;
+    if (b >= r.S) {
+        __shared__ uint32_t sink[256];
+        const size_t lines = r.prefetch_bytes / 128, nthr = (size_t)(gridDim.x - r.S) * 256;
+#pragma unroll
+        for (int q = 0; q < RN_PF_LINES; ++q) {
+            const size_t line = (size_t)q * nthr + (size_t)(b - r.S) * 256 + t;
+            if (line < lines)
+                __builtin_amdgcn_global_load_lds(static_cast<const uint8_t *>(r.prefetch) + line * 128,
+                                                 (__attribute__((address_space(3))) void *)sink, 4, 0, 0);
+        }
+        return;
+    }
     const bool ok = k < r.H;
     const size_t o = (size_t)b * r.H + (ok ? k : 0);
     float4 x = *reinterpret_cast<const float4 *>((r.xin ? r.xin : r.x) + o);
-    float4 pz[8];
-    const int ks = r.parts ? r.ksplit : 0;
+    float4 pz[KS > 0 ? KS : 1];
 #pragma unroll
-    for (int z = 0; z < 8; ++z)
-        if (z < ks) pz[z] = *reinterpret_cast<const float4 *>(r.parts + (size_t)z * r.S * r.H + o);
+    for (int z = 0; z < KS; ++z) pz[z] = *reinterpret_cast<const float4 *>(r.parts + (size_t)z * r.S * r.H + o);
 #pragma unroll
-    for (int z = 0; z < 8; ++z)
-        if (z < ks) x = make_float4(x.x + pz[z].x, x.y + pz[z].y, x.z + pz[z].z, x.w + pz[z].w);
+    for (int z = 0; z < KS; ++z) x = make_float4(x.x + pz[z].x, x.y + pz[z].y, x.z + pz[z].z, x.w + pz[z].w);
     if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok && (ks > 0 || (r.xin && r.xin != r.x))) *reinterpret_cast<float4 *>(r.x + o) = x;
+    if (ok && (KS > 0 || (r.xin && r.xin != r.x))) *reinterpret_cast<float4 *>(r.x + o) = x;
     double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);
     ss = wave_sum_d(ss);
     if ((t & 63) == 0) scr[t >> 6] = ss;
@@ -211,7 +226,8 @@ __global__ void __launch_bounds__(256) k_select_embed_norm(const SelectSpec sp, 
     const int sel_col = sp.mode == SEL_CB0 ? 0 : sp.step + 1;   // the column this launch selected
     const GatherSum &gs = en.gs;
     auto token = [&](int col) {   // finished slots (no selection) keep the token already in the table
-        return col == sel_col && stok >= 0 ? stok : gs.tok[(size_t)b * gs.tok_ld + col];
+        const int tt = gs.tok[(size_t)b * gs.tok_ld + col];   // loaded unconditionally: no branch around the load
+        return col == sel_col && stok >= 0 ? stok : tt;
     };
     const bool ok = k < en.H;
     const int kk = ok ? k : 0;
@@ -222,6 +238,7 @@ __global__ void __launch_bounds__(256) k_select_embed_norm(const SelectSpec sp, 
         a[0] = h2f(u.x & 0xffff); a[1] = h2f(u.x >> 16); a[2] = h2f(u.y & 0xffff); a[3] = h2f(u.y >> 16);
     }
     if (en.nt == 16) {
+#pragma unroll   // the 15 token loads, then the 15 row loads, each group in flight together
         for (int j = 1; j < 16; ++j) {
             const uint2 u = *reinterpret_cast<const uint2 *>(gs.tabs[j] + (size_t)token(j) * en.H + kk);
             a[0] += h2f(u.x & 0xffff); a[1] += h2f(u.x >> 16); a[2] += h2f(u.y & 0xffff); a[3] += h2f(u.y >> 16);
@@ -264,11 +281,20 @@ bool select_embed_norm(const SelectSpec &sp, const float *logits, const EmbedNor
 
 bool resid_norm(const ResidNorm &r, hipStream_t s) {
     if (r.S <= 0) return true;
-    if (r.H > 1024 || r.H % 4 != 0 || !r.x || !r.nw || !r.xn || (r.parts && (r.ksplit < 1 || r.ksplit > 8))) {
+    if (r.H > 1024 || r.H % 4 != 0 || !r.x || !r.nw || !r.xn || (r.parts && (r.ksplit < 1 || r.ksplit > 4))) {
         set_error("resid_norm: unsupported shape");
         return false;
     }
-    hipLaunchKernelGGL(k_resid_norm, dim3(r.S), dim3(256), 0, s, r);
+    const size_t pf_lines = r.prefetch ? r.prefetch_bytes / 128 : 0;
+    const unsigned pf_wgs = (unsigned)std::min<size_t>((pf_lines + 256 * RN_PF_LINES - 1) / (256 * RN_PF_LINES), 1024);
+    const dim3 grid((unsigned)r.S + pf_wgs);
+    switch (r.parts ? r.ksplit : 0) {
+        case 0: hipLaunchKernelGGL(k_resid_norm<0>, grid, dim3(256), 0, s, r); break;
+        case 1: hipLaunchKernelGGL(k_resid_norm<1>, grid, dim3(256), 0, s, r); break;
+        case 2: hipLaunchKernelGGL(k_resid_norm<2>, grid, dim3(256), 0, s, r); break;
+        case 3: hipLaunchKernelGGL(k_resid_norm<3>, grid, dim3(256), 0, s, r); break;
+        default: hipLaunchKernelGGL(k_resid_norm<4>, grid, dim3(256), 0, s, r); break;
+    }
     Q3T_HIP(hipGetLastError());
     return true;
 }
