@@ -110,6 +110,34 @@ int main(int argc, char **argv) {
     CK(hipSetDevice(0));
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const int H = 1024, QKV = 4096, I = 3072, NC = 28;
+    if (argc > 1 && std::string(argv[1]) == "attn_seq") {
+        // ---- batched decode attention (k_attn_seq: one workgroup per (slot, kv head)), 8 rotating cache copies:
+        // fixed cost (prologue, wave merge) vs per-chunk cost from a sweep over positions and slot counts
+        const int n_ctx = 1024, NCA = 8;
+        for (int S : {16, 32, 64}) {
+            float *qkv = dev<float>((size_t)S * QKV, 1.0f), *qn = dev<float>(128, 1.0f), *kn = dev<float>(128, 1.0f);
+            float *rope = dev<float>((size_t)n_ctx * 128, 1.0f);
+            int *pos = dev<int>(S);
+            const size_t kvl = (size_t)S * 8 * n_ctx * 128;
+            uint16_t *kc = dev<uint16_t>(kvl * NCA, 0.5f), *vc = dev<uint16_t>(kvl * NCA, 0.5f);
+            uint16_t *ao = dev<uint16_t>((size_t)S * 2048, 0.0f);
+            for (int P : {0, 63, 127, 266, 511, 1000}) {
+                std::vector<int> pv(S, P);
+                CK(hipMemcpy(pos, pv.data(), S * 4, hipMemcpyHostToDevice));
+                const double us = time_graph(NCA, [&](int i) {
+                    AttnParams a;
+                    a.qkv = qkv; a.qn = qn; a.kn = kn; a.eps = 1e-6f; a.rope = rope; a.pos = pos;
+                    a.kc = kc + (i % NCA) * kvl; a.vc = vc + (i % NCA) * kvl;
+                    a.n_ctx = n_ctx; a.S = S; a.nH = 16; a.nKV = 8; a.D = 128; a.max_splits = 1; a.seqk = true; a.out = ao;
+                    return attn_decode(a, st);
+                });
+                const double mb = (double)S * (P + 1) * 8 * 128 * 2 * 2 / 1e6;
+                printf("attn_seq S %2d pos %4d: %7.2f us  KV %6.2f MB  %6.0f GB/s\n", S, P, us, mb, mb / us * 1e3);
+            }
+            hipFree(qkv); hipFree(qn); hipFree(kn); hipFree(rope); hipFree(pos); hipFree(kc); hipFree(vc); hipFree(ao);
+        }
+        return 0;
+    }
     // ---- launch floor
     for (int blocks : {256, 512, 1024}) {
         const double us = time_graph(100, [&](int) { hipLaunchKernelGGL(k_empty, dim3(blocks), dim3(256), 0, st, nullptr); return true; });
