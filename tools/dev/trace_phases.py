@@ -9,7 +9,8 @@ import sys
 rows = []
 with open(sys.argv[1]) as f:
     for r in csv.DictReader(f):
-        n = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void q3t::", "").replace("q3t::", "")
+        n = r["Kernel_Name"].replace("(anonymous namespace)::", "")   # the role kernels sit in an anonymous namespace
+        n = re.sub(r"\(.*", "", n).replace("void q3t::", "").replace("q3t::", "")
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), n, r["Grid_Size_X"], r["Grid_Size_Y"]))
 rows.sort()
 # the 1-slot talker step is ONE persistent launch when the persistent kernels run (k_tk_roles / k_persist<0, *>)
