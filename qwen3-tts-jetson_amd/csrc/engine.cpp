@@ -719,6 +719,10 @@ static bool prefill_layer_attn(const PrefillAttnParams &pf, const Config &c, con
 }
 
 static const bool g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return !e || std::atoi(e) != 0; }();
+// gate/up on 64-token tiles: 192 workgroups of one per CU instead of 384 (two on half the CUs, which set the tail);
+// the other projections keep 32-token tiles.  64-slot talker step 1.574 -> 1.549 ms (two A/B pairs,
+// tools/dev/exp_gutt.sh); the tile never changes a row's arithmetic.  Q3T_MM_GU_TT=1 restores 32-token tiles.
+static const int g_mm_gu_tt = [] { const char *e = std::getenv("Q3T_MM_GU_TT"); return e ? std::atoi(e) : 2; }();
 static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector<DevLayer> &layers, int S, float *x, uint16_t *xn,
                              float *parts, float *qkv, uint16_t *attn, uint16_t *hmlp, uint16_t *kc, uint16_t *vc,
                              size_t kv_layer, int n_ctx, int max_splits, const int *pos, const float *rope, float *part,
@@ -790,7 +794,7 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         GemvParams gu;
         gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
         gu.pro = PRO_F16; gu.x = xn; gu.ldx = H;
-        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter; gu.force_mm = force;
+        gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter; gu.force_mm = force; gu.mm_tt = g_mm_gu_tt;
         if (!gemv(gu, s)) return false;
         GemvParams dn;
         dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;

@@ -689,7 +689,7 @@ static bool launch_norm_nch(const GemvParams &p, hipStream_t s) {
 }
 template <int NCH>
 static bool launch_f16_tt(const GemvParams &p, hipStream_t s) {
-    return g_tt == 2 && p.B > 32 ? launch_f16<NCH, 2>(p, s) : launch_f16<NCH, 1>(p, s);
+    return (p.mm_tt ? p.mm_tt : g_tt) == 2 && p.B > 32 ? launch_f16<NCH, 2>(p, s) : launch_f16<NCH, 1>(p, s);
 }
 
 bool gemm_mfma(const GemvParams &p, hipStream_t s) {

@@ -110,6 +110,7 @@ struct GemvParams {
     float *parts = nullptr;
     int ksplit = 1;
     bool xcd_slices = false;   // split-K tiles in XCD-aware order (gemm_mfma.hip splitk_tile)
+    int mm_tt = 0;              // MFMA token tile in 32-token units for this call (0: the library default)
     bool force_mm = false;   // matrix-core path even below gemm_mfma_min_batch() (a single slot reproducing the
                              // per-token arithmetic of a batch that runs there)
     int family_b = 0;        // > 0: kernel family (vector / matrix core) and K split chosen as for a batch of
