@@ -718,7 +718,9 @@ static bool prefill_layer_attn(const PrefillAttnParams &pf, const Config &c, con
     return prefill_attn(q, s);
 }
 
-static const bool g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return !e || std::atoi(e) != 0; }();
+// weight prefetch of the batched talker stack: 0 off, 1 the norms before QKV and gate/up, 2 also the gate/up GEMM for
+// the down projection (its 64-token tiles leave a quarter of the CUs free)
+static const int g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return e ? std::atoi(e) : 2; }();
 // gate/up on 64-token tiles: 192 workgroups of one per CU instead of 384 (two on half the CUs, which set the tail);
 // the other projections keep 32-token tiles.  64-slot talker step 1.574 -> 1.549 ms (two A/B pairs,
 // tools/dev/exp_gutt.sh); the tile never changes a row's arithmetic.  Q3T_MM_GU_TT=1 restores 32-token tiles.
@@ -788,13 +790,14 @@ static bool decoder_stack_mm(const Config &c, bool attn_split, const std::vector
         rn.parts = parts; rn.ksplit = o.ksplit; rn.nw = l.ffn_norm; rn.side = nullptr;
         // the talker's weights stream from HBM each step: the norm before a projection touches that projection's lines
         // (the code predictor's 157 MB stay in the Infinity Cache across its 16 passes anyway)
-        const bool pf_w = !cp_attn && g_mm_prefetch;
+        const bool pf_w = !cp_attn && g_mm_prefetch > 0;
         rn.prefetch = pf_w ? l.gu : nullptr; rn.prefetch_bytes = (size_t)2 * c.inter * H * 2;
         if (!resid_norm(rn, s)) return false;
         GemvParams gu;
         gu.W = l.gu; gu.N = 2 * c.inter; gu.K = H; gu.B = S;
         gu.pro = PRO_F16; gu.x = xn; gu.ldx = H;
         gu.act = ACT_SWIGLU; gu.out_f16 = hmlp; gu.ldo = c.inter; gu.force_mm = force; gu.mm_tt = g_mm_gu_tt;
+        if (pf_w && g_mm_prefetch > 1) { gu.prefetch = l.down; gu.prefetch_bytes = (size_t)c.inter * H * 2; }
         if (!gemv(gu, s)) return false;
         GemvParams dn;
         dn.W = l.down; dn.N = H; dn.K = c.inter; dn.B = S;

@@ -20,6 +20,8 @@
 //     tile (bias, activation, scale, residual, aux, SwiGLU pairs, f16/f32 stores of 4 consecutive rows).
 #include "kernels.h"
 
+#include <algorithm>
+
 #include <cstdlib>
 
 namespace q3t {
@@ -173,6 +175,19 @@ __global__ void __launch_bounds__(256, 1) k_gemm_mfma(const GemvParams p) {
     constexpr bool kLds = PRO != PRO_F16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
     const int K = NCH * 256;
+    if (PRO == PRO_F16 && (int)blockIdx.x >= p.N / MM_ROWS) {
+        // prefetch workgroup (GemvParams::prefetch): global->LDS dword loads, nothing to wait on
+        const int ntx = p.N / MM_ROWS;
+        const size_t lines = p.prefetch_bytes / 128, nthr = (size_t)(gridDim.x - ntx) * 256;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const size_t line = (size_t)q * nthr + (size_t)(blockIdx.x - ntx) * 256 + tid;
+            if (line < lines)
+                __builtin_amdgcn_global_load_lds(static_cast<const uint8_t *>(p.prefetch) + line * 128,
+                                                 (__attribute__((address_space(3))) void *)smem, 4, 0, 0);
+        }
+        return;
+    }
     const TileIdx ti = PRO == PRO_F16 && p.parts && p.xcd_slices ? splitk_tile() : TileIdx{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
     const int row0 = ti.x * MM_ROWS;
     const int t0 = ti.y * (TT * 32);
@@ -638,7 +653,11 @@ static bool launch_f16_sw(const GemvParams &p, hipStream_t s) {
     const size_t lds = (size_t)4 * TT * 16 * 64 * 4;
     static bool attr = false;
     if (!set_lds(reinterpret_cast<const void *>(&k_gemm_mfma<PRO_F16, NCH, TT, SW>), lds, attr)) return false;
-    const dim3 grid((unsigned)(p.N / MM_ROWS), (unsigned)((p.B + TT * 32 - 1) / (TT * 32)), (unsigned)(p.parts ? p.ksplit : 1));
+    const unsigned gy = (unsigned)((p.B + TT * 32 - 1) / (TT * 32));
+    // prefetch workgroups only on a one-row, unsplit grid (their index is blockIdx.x past the row tiles)
+    const size_t pf_lines = p.prefetch && !p.parts && gy == 1 ? p.prefetch_bytes / 128 : 0;
+    const unsigned pf_wgs = (unsigned)std::min<size_t>((pf_lines + 511) / 512, 1024);
+    const dim3 grid((unsigned)(p.N / MM_ROWS) + pf_wgs, gy, (unsigned)(p.parts ? p.ksplit : 1));
     hipLaunchKernelGGL((k_gemm_mfma<PRO_F16, NCH, TT, SW>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;

@@ -111,6 +111,10 @@ struct GemvParams {
     int ksplit = 1;
     bool xcd_slices = false;   // split-K tiles in XCD-aware order (gemm_mfma.hip splitk_tile)
     int mm_tt = 0;              // MFMA token tile in 32-token units for this call (0: the library default)
+    // matrix-core f16 path, one token-tile row, no split-K: extra workgroups past the row tiles touch one dword per
+    // 128-B line of these bytes (the NEXT projection's weights) so they are in the Infinity Cache when it runs
+    const void *prefetch = nullptr;
+    size_t prefetch_bytes = 0;
     bool force_mm = false;   // matrix-core path even below gemm_mfma_min_batch() (a single slot reproducing the
                              // per-token arithmetic of a batch that runs there)
     int family_b = 0;        // > 0: kernel family (vector / matrix core) and K split chosen as for a batch of
