@@ -94,7 +94,10 @@ int q3t_generate(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const in
 /* streaming: on_frames(user, u, codes [n][16], n, 16) is called on the caller's thread every `interval` frames of
  * utterance u with its newest `interval` frames, and once more after the loop with the remainder (< interval
  * frames, or the frames before EOS); returning 0 stops utterance u after the frames delivered so far.  The callback
- * may call q3t_vocoder_decode on the same context (it runs behind the frames already queued). */
+ * may call q3t_vocoder_decode on the same context (it runs behind the frames already queued).  The callback runs
+ * while the generate holds its device lock (shared for batches, exclusive for one utterance): it must not start a
+ * one-utterance generate on another context of the same device, and a wait in it for another thread's work on the
+ * same device can be delayed up to 20 ms by a one-utterance generate queued meanwhile (devlock.h). */
 typedef int (*q3t_frame_cb)(void *user, int32_t utterance, const int32_t *codes, int32_t n_frames, int32_t n_codebooks);
 int q3t_generate_stream(q3t_ctx *ctx, int n_utt, const int32_t *const *tokens, const int32_t *n_tokens,
                         const float *const *speaker, const q3t_gen_params *p, int32_t *codes, int32_t *n_frames,

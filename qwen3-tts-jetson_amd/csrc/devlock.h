@@ -8,6 +8,10 @@
 // persistent grid.  Every holder keeps it until its GPU work has drained (the entry points all return synchronised).
 // Re-entrant per thread: a retry, or a frame callback calling back into the library on the same thread, keeps the
 // hold it has (a callback must not start a single-slot generation on another context of the same device).
+// Frame callbacks (q3t_generate_stream, q3t_generate_queue) run while their generate holds the lock.  Waiting writers
+// are preferred over new readers for at most 20 ms (engine.cpp WPLock): a callback that waits for another thread's
+// shared-hold work on the same device (a vocoder worker) is therefore delayed, never deadlocked, by a single-slot
+// generate queued meanwhile.
 #pragma once
 #include <mutex>
 #include <shared_mutex>

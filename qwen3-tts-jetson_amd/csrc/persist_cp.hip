@@ -40,6 +40,12 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_MMS
+#define Q3T_CP_MMS 16   // granule stride of the head workgroups' max / min pairs (16: a line each; 2: packed)
+#endif
+#ifndef Q3T_CP_PREDIV
+#define Q3T_CP_PREDIV 1   // the head workgroups publish the rows divided by T (0: the selecting workgroups divide)
+#endif
 #ifndef Q3T_CP_WAIT
 #define Q3T_CP_WAIT g_wait   // development: g_wait_gated
 #endif
@@ -50,7 +56,7 @@ namespace {
 using namespace pdev;
 
 constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, VOC = 3072, CPV = 2048;
-constexpr int G = 256, NLC = 5, NPASS = 16, PPH = 5 * NLC + 1;
+constexpr int G = 256, NLC = 5, NPASS = 16, PPH = 5 * NLC + 1, MMS = Q3T_CP_MMS;
 constexpr int QW = 0, NQ = 64;      // QKV rows 64 (4 x 16) of 4096; lm_head rows 32 (2 x 16) of 2048
 constexpr int AW = 64, NA = 8;      // attention of kv group w - AW, token selection
 constexpr int OW = 72, NO = 32;     // O-projection rows 32 (8 x 4) of 1024
@@ -98,6 +104,8 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
     const PersistParams &p = X.p;
     CLds &S = X.S;
     const int i = blockIdx.x - QW, t = threadIdx.x, l16 = t & 15, grp = t >> 4;
+    const float temp = p.sel.temperature;
+    const bool samp = temp > 0.0f;
     uint4 wq[4][8];
     float4 nw;
     auto issue_qkv = [&](int l) {
@@ -182,9 +190,17 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             if (l16 == 0) S.outv[16 * j + grp] = lg;
         }
         __syncthreads();
-        if (t < 32) {
-            g_put(p.glog + 32 * i + t, __float_as_uint(S.outv[t]), X.tag(hph));
-            p.logits[32 * i + t] = S.outv[t];   // read after the launch only (host, tests)
+        if (t < 64) {   // wave 0, ONE store instruction: lanes 0..31 publish the rows, lanes 32 / 33 (sampling) their max
+                        // and finite min
+            // sampling: the rows divided by T (the selection's first step, the same IEEE division) and the 32 rows'
+            // max / finite min, so the selecting workgroups skip that step and its block reduction
+            const float lg = S.outv[t & 31];   // lanes 32..63 hold the same rows
+            const float sv = samp && Q3T_CP_PREDIV ? lg / temp : lg;
+            const float mx = group_max<32>(sv), mn = -group_max<32>(sv > -INFINITY ? -sv : -INFINITY);
+            if (t < 32 || (samp && t < 34))
+                g_put(t < 32 ? p.glog + 32 * i + t : p.glog + CPV + MMS * i + (t - 32),
+                      __float_as_uint(t < 32 ? sv : t == 32 ? mx : mn), X.tag(hph));
+            if (t < 32) p.logits[32 * i + t] = lg;   // read after the launch only (host, tests)
         }
         PROF(hph, 2);
         if (pass + 1 < NPASS) issue_qkv(1);
@@ -206,6 +222,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         S.kn[e / D][e % D] = S.layers[e / D].kn[e % D];
     }
     for (int e = t; e < 16 * D; e += 256) S.rope[e / D][e % D] = p.rope[e];
+    S.sel.hist[t] = 0u;   // sel_sample_range's precondition (zeroed again after every selection)
     SelPre spre;
     sel_prefetch<SEL_CP>(p.sel, 0, spre);
     int tok = p.gs.tok[0];   // CB0: the input of pass 1
@@ -327,16 +344,35 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         // same token in all 8), so the next pass's attention starts without a token hand-off; workgroup AW commits it
         // and hands it to the O workgroups (the residual row of layer 0)
         const int hph = ph_of(pass, NLC, 0);
-        uint32_t u8[8];
+        const bool samp = p.sel.temperature > 0.0f;
+        const float u = uniform24(spre.seed, spre.utt, (uint64_t)spre.frame, (uint64_t)pass);   // select_token_pre's u
+        uint32_t u8[8], mm[2];
         PROF(hph, 0);
-        g_wait<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
+        if (samp) g_wait_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
+        else g_wait<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
         PROF(hph, 1);
         float v[SEL_VPT_MAX];
 #pragma unroll
         for (int e = 0; e < SEL_VPT_MAX; ++e) v[e] = e < 8 ? __uint_as_float(u8[e]) : -INFINITY;
         SelectSpec sp = p.sel;
         sp.step = pass - 1;
-        const int sel = select_token_pre<SEL_CP>(sp, spre, v, S.sel);
+        int sel;
+        if (spre.done >= 0) {
+            sel = -1;
+        } else if (!samp) {
+            sel = sel_argmax(v, CPV, 8, S.sel);
+        } else {   // the row arrives divided by T with the 64 producers' max / min (lane l: producer l)
+            float mx = wave_max(__uint_as_float(mm[0])), mn = -wave_max(-__uint_as_float(mm[1]));
+            if constexpr (!Q3T_CP_PREDIV) {   // the raw row: divide here (x -> x / T is monotonic, so the max / min of
+                                              // the quotients are the quotients of the max / min)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = v[e] / p.sel.temperature;
+                mx = mx / p.sel.temperature;
+                mn = mn / p.sel.temperature;
+            }
+            sel = sel_sample_range(v, CPV, 8, p.sel.top_k, u, mx, mn, S.sel);
+        }
+        S.sel.hist[t] = 0u;   // the next selection's range histogram (this one's bins were read before its last barrier)
         PROF(hph, 3);   // (development timeline: token selected)
         if (g == 0 && t == 0) {
             if (pass + 1 < NPASS) g_put(p.gtok + pass, (uint32_t)max(sel, 0), X.tag(hph));

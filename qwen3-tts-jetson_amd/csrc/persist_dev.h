@@ -80,6 +80,37 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
     for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];
 }
 
+// g_wait over two granule runs a[0..N) and b[0..M) in one poll loop (one round trip per poll for both)
+template <int N, int M>
+__device__ __forceinline__ void g_wait_pair(const uint64_t *a, const uint64_t *b, uint32_t tag, uint32_t (&oa)[N], uint32_t (&ob)[M],
+                                            Ctl &c) {
+    uint64_t v[N + M];
+    unsigned it = 0;
+    while (true) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = g_ld(a + i);
+#pragma unroll
+        for (int i = 0; i < M; ++i) v[N + i] = g_ld(b + i);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < N + M; ++i) ok &= (uint32_t)(v[i] >> 32) == tag;
+        if (ok || c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                c.abort = true;
+                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) oa[i] = (uint32_t)v[i];
+#pragma unroll
+    for (int i = 0; i < M; ++i) ob[i] = (uint32_t)v[N + i];
+}
+
 // g_gate: lane 0 of each wave polls one granule alone (one 8-B load per poll) until it carries `tag`.  g_wait_gated:
 // g_wait behind the gate on the wave's first granule: lane 0 first polls it alone, then the wave sweeps all N.  For long waits of many granules per thread, whose sweeps would otherwise flood
 // the CU's memory path for the whole wait (a co-resident workgroup's stores then stalled for ~230 us).

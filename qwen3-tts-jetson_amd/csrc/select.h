@@ -32,6 +32,7 @@ struct alignas(16) SelLds {
     float wsum[4];
     float rmax[4], rmin[4];   // sel_kth_largest_range's wave max / min (apart from fred: CB0's block max reads fred
                               // right before it, so its first barrier is not needed)
+    unsigned fcnt[4];         // sel_topk_fast: entries per wave (the entries overlay hist[1024..2047])
     unsigned last;
 };
 
@@ -301,6 +302,152 @@ __device__ __forceinline__ float sel_kth_largest_range(const float (&v)[SEL_VPT_
     return sel_keyf(S.sres[0]);   // (sres is written again only by the next selection, behind the caller's barrier)
 }
 
+// Top-k sampling in three workgroup barriers (v already divided by T; returns the token, or -2 when the row needs the
+// general path below: a degenerate value range, fewer than k finite values, or more than SEL_FAST_CAP entries at or above
+// the boundary bin; the condition is uniform over the workgroup).
+//   B1  row max / min of the finite values (the range histogram's bounds, and the softmax max)
+//   B2  256-bin range histogram (sel_kth_largest_range's bins); every wave then scans it itself: boundary bin b*, count
+//       above it
+//   B3  each wave writes its entries with bin >= b* (and the kept id) in index order into its own LDS region
+// then EVERY wave, redundantly (so no barrier hands the token over): loads the <= 128 entries two per lane in index order,
+// ranks the boundary-bin entries among themselves (an entry survives iff fewer than k - above of them are larger: the
+// same set as `v >= k-th largest`), exp(v - max), a wave scan of the survivors' exps in index order (two per lane), total
+// = the last lane's sum, and the first index whose cumulative sum reaches u * total.
+// RANGE: the caller passes the row max and finite min (mx, mn; computed by the logits' producers) and has zeroed
+// S.hist[0..255] behind a workgroup barrier that follows the previous selection: B1 is skipped.
+constexpr int SEL_FAST_CAP = 128;
+template <bool RANGE = false>
+__device__ __forceinline__ int sel_topk_fast(const float (&v)[SEL_VPT_MAX], int n, int vpt, int k, float u, int keep_id, SelLds &S,
+                                             float mx = -INFINITY, float mn = INFINITY) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if constexpr (!RANGE) {
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e)
+            if (e < vpt && t * vpt + e < n) {
+                mx = fmaxf(mx, v[e]);
+                if (v[e] > -INFINITY) mn = fminf(mn, v[e]);
+            }
+        S.hist[t] = 0u;
+        mx = wave_max(mx);
+        mn = -wave_max(-mn);
+        if (lane == 0) { S.rmax[wave] = mx; S.rmin[wave] = mn; }
+        __syncthreads();   // B1
+        SEL_STAMP(10);
+        mx = fmaxf(fmaxf(S.rmax[0], S.rmax[1]), fmaxf(S.rmax[2], S.rmax[3]));
+        mn = fminf(fminf(S.rmin[0], S.rmin[1]), fminf(S.rmin[2], S.rmin[3]));
+    }
+    const float range = mx - mn;
+    if (!(range > 0.0f) || !(range < INFINITY)) return -2;
+    const float scale = 256.0f / range;
+    int dig[SEL_VPT_MAX];
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        dig[e] = -1;
+        if (e < vpt && t * vpt + e < n && v[e] > -INFINITY) {
+            dig[e] = min(255, (int)((v[e] - mn) * scale));
+            atomicAdd(&S.hist[dig[e]], 1u);
+        }
+    }
+    __syncthreads();   // B2
+    SEL_STAMP(11);
+    unsigned bstar, above;
+    {   // lane l owns bins 255-4l .. 252-4l (descending): the inclusive lane scan counts keys from the top
+        const uint4 h4 = *reinterpret_cast<const uint4 *>(&S.hist[252 - 4 * lane]);
+        const unsigned c[4] = {h4.w, h4.z, h4.y, h4.x};
+        const unsigned loc = c[0] + c[1] + c[2] + c[3];
+        const unsigned incl = wave_scan_incl_u(loc);
+        if ((unsigned)__builtin_amdgcn_readlane((int)incl, 63) < (unsigned)k) return -2;   // < k finite values
+        unsigned cum = incl - loc, mb = 0, ma = 0;
+        bool hit = false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (cum < (unsigned)k && (unsigned)k <= cum + c[q]) { hit = true; mb = 255 - 4 * lane - q; ma = cum; }
+            cum += c[q];
+        }
+        const int src = __builtin_ctzll(__ballot(hit));
+        bstar = (unsigned)__builtin_amdgcn_readlane((int)mb, src);
+        above = (unsigned)__builtin_amdgcn_readlane((int)ma, src);
+    }
+    SEL_STAMP(12);
+    // entries: bin >= b*, or the kept id (its value competes for the threshold like any other and survives anyway)
+    uint2 *ent = reinterpret_cast<uint2 *>(&S.hist[1024]) + SEL_FAST_CAP * wave;
+    unsigned cnt = 0;
+#pragma unroll
+    for (int e = 0; e < SEL_VPT_MAX; ++e) {
+        const int i = t * vpt + e;
+        if (e < vpt && i < n && (dig[e] >= (int)bstar || i == keep_id)) ++cnt;
+    }
+    const unsigned cincl = wave_scan_incl_u(cnt);
+    const unsigned wtot = (unsigned)__builtin_amdgcn_readlane((int)cincl, 63);
+    if (wtot <= (unsigned)SEL_FAST_CAP) {
+        unsigned pos = cincl - cnt;
+#pragma unroll
+        for (int e = 0; e < SEL_VPT_MAX; ++e) {
+            const int i = t * vpt + e;
+            if (e < vpt && i < n && (dig[e] >= (int)bstar || i == keep_id))
+                ent[pos++] = make_uint2(__float_as_uint(v[e]), (uint32_t)i | (dig[e] == (int)bstar ? 0x80000000u : 0u));
+        }
+    }
+    if (lane == 0) S.fcnt[wave] = wtot;
+    __syncthreads();   // B3
+    SEL_STAMP(13);
+    const unsigned c0 = S.fcnt[0], c1 = S.fcnt[1], c2 = S.fcnt[2], c3 = S.fcnt[3];
+    const unsigned ns = c0 + c1 + c2 + c3;
+    if (ns > (unsigned)SEL_FAST_CAP) return -2;   // (also covers one wave over its region: ns >= that wave's count)
+    float ev[2];
+    uint32_t ei[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const unsigned j = 2 * lane + s;
+        ev[s] = -INFINITY;
+        ei[s] = 0x7fffffffu;
+        if (j < ns) {
+            const unsigned r = j < c0 ? 0u : j < c0 + c1 ? 1u : j < c0 + c1 + c2 ? 2u : 3u;
+            const unsigned off = j - (r >= 1 ? c0 : 0u) - (r >= 2 ? c1 : 0u) - (r >= 3 ? c2 : 0u);
+            const uint2 q = reinterpret_cast<const uint2 *>(&S.hist[1024])[SEL_FAST_CAP * r + off];
+            ev[s] = __uint_as_float(q.x);
+            ei[s] = q.y;
+        }
+    }
+    SEL_STAMP(14);
+    // boundary-bin entries: rank among themselves
+    const unsigned kk = (unsigned)k - above;
+    unsigned gt[2] = {0u, 0u};
+#pragma unroll
+    for (int so = 0; so < 2; ++so) {
+        uint64_t m = __ballot((ei[so] & 0x80000000u) && ei[so] != 0x7fffffffu);
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const float o = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ev[so]), j));
+            gt[0] += o > ev[0];
+            gt[1] += o > ev[1];
+        }
+    }
+    SEL_STAMP(15);
+    float p[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const bool valid = ei[s] != 0x7fffffffu;
+        const bool cand = valid && (ei[s] & 0x80000000u);
+        const bool keep = valid && (int)(ei[s] & 0x7fffffffu) == keep_id;
+        const bool surv = valid && (keep || !cand || gt[s] < kk);
+        p[s] = surv ? expf(ev[s] - mx) : 0.0f;
+    }
+    const float loc = p[0] + p[1];
+    const float incl = wave_scan_incl_f(loc);
+    const float total = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 63));
+    const float target = u * total;
+    const float cum0 = (incl - loc) + p[0], cum1 = cum0 + p[1];
+    const bool f0 = cum0 >= target && p[0] > 0.0f, f1 = cum1 >= target && p[1] > 0.0f;
+    const uint64_t fm = __ballot(f0 || f1);
+    SEL_STAMP(16);
+    if (fm == 0) return n - 1;
+    const int src = __builtin_ctzll(fm);
+    const uint32_t pick = f0 ? ei[0] : ei[1];
+    return (int)((uint32_t)__builtin_amdgcn_readlane((int)pick, src) & 0x7fffffffu);
+}
+
 // temperature -> top-k -> keep_id restored -> exp -> inverse CDF with u (v is modified)
 __device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vpt, float temperature, int top_k, float u, int keep_id,
                           SelLds &S) {
@@ -316,6 +463,13 @@ __device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vp
         if (t == keep_owner && t * vpt + e == keep_id) keep_v = v[e];
     float m = -INFINITY;
     const bool topk = top_k > 0 && top_k < n;
+#ifndef Q3T_SEL_GENERAL
+    if (topk) {
+        const int r = sel_topk_fast(v, n, vpt, top_k, u, keep_id, S);
+        if (r != -2) return r;
+        __syncthreads();   // (uniform) the waves may still read this selection's histogram
+    }
+#endif
     if (topk) {
         // the row max survives the threshold and bounds the restored kept logit: it is the softmax max as well
         const float thr = sel_kth_largest_range(v, n, vpt, top_k, &m, S);
@@ -365,6 +519,19 @@ __device__ __forceinline__ int sel_sample(float (&v)[SEL_VPT_MAX], int n, int vp
     SEL_STAMP(8);
     const int r = (int)S.ures[0];
     return r == 0x7fffffff ? n - 1 : r;
+}
+
+// top-k sampling of a row already divided by T whose max / finite min the producers computed (the code-predictor role
+// kernel's heads): sel_topk_fast<true>, or sel_sample at T = 1 (x / 1 = x exactly) for the rows it does not take.
+// Precondition as sel_topk_fast<true>: S.hist[0..255] zeroed behind a barrier after the previous selection.
+__device__ __forceinline__ int sel_sample_range(float (&v)[SEL_VPT_MAX], int n, int vpt, int top_k, float u, float mx, float mn,
+                                                SelLds &S) {
+    if (top_k > 0 && top_k < n) {
+        const int r = sel_topk_fast<true>(v, n, vpt, top_k, u, -1, S, mx, mn);
+        if (r != -2) return r;
+        __syncthreads();   // (uniform) the waves may still read this selection's histogram
+    }
+    return sel_sample(v, n, vpt, 1.0f, top_k, u, -1, S);
 }
 
 // load one slot's logits row into the owner registers (SC1: agent-scope loads of a row published in this launch)

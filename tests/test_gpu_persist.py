@@ -19,11 +19,14 @@ sys.path.insert(0, os.path.join(REPO, "qwen3-tts-jetson_amd"))
 pytestmark = pytest.mark.gpu
 
 
-def _engine(tts, tok, persist, **kw):
+def _engine(tts, tok, persist, roles=True, **kw):
     """persist=False: the launch-per-op graphs, with the code predictor's attention as its own k_attn launch
-    (Q3T_CP_FUSED_ATTN=0), whose arithmetic the persistent frame reproduces bit for bit"""
+    (Q3T_CP_FUSED_ATTN=0), whose arithmetic the persistent frame reproduces bit for bit; roles=False: the all-role
+    persistent kernels (k_persist<0,CH>, k_persist<1,16>), the production fallback where the role kernels are not
+    resident"""
     import q3t
-    env = {"Q3T_PERSIST": "1" if persist else "0", "Q3T_CP_FUSED_ATTN": "1" if persist else "0"}
+    env = {"Q3T_PERSIST": "1" if persist else "0", "Q3T_CP_FUSED_ATTN": "1" if persist else "0",
+           "Q3T_TK_ROLES": "1" if roles else "0", "Q3T_CP_ROLES": "1" if roles else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -42,6 +45,7 @@ def engines():
     ep = _engine(tts, tok, True, max_slots=1, max_ctx=320)
     eg = _engine(tts, tok, False, max_slots=1, max_ctx=320)
     assert ep.persist_status() == 0, "persistent talker step not in use on this device"
+    assert ep.persist_kernels() == 1 | 4, ep.persist_kernels()   # k_tk_roles + k_cp_roles
     assert eg.persist_status() == -1
     yield ep, eg
     ep.close()
@@ -101,6 +105,33 @@ def test_cp_frame_bit_exact(engines, temperature):
         cg = eg.codepred_frame(hid[None], [cb0], temperature=temperature, top_k=50, seed=3, frame=frame)
         assert np.array_equal(cp, cg), (frame, cp, cg)
     assert ep.persist_status() == 0
+
+
+def test_all_role_kernels_bit_exact():
+    """the all-role persistent kernels (Q3T_TK_ROLES=0, Q3T_CP_ROLES=0: k_persist<0,64>, k_persist<1,16>) against the
+    launch-per-op graph: talker step positions across the split combine, code-predictor frames greedy and sampled"""
+    tts, tok = synth_dir("full")
+    ea = _engine(tts, tok, True, roles=False, max_slots=1, max_ctx=320)
+    eg = _engine(tts, tok, False, max_slots=1, max_ctx=320)   # fresh caches on both sides
+    try:
+        assert ea.persist_status() == 0 and ea.persist_kernels() == 2 | 8, ea.persist_kernels()
+        H = ea.cfg["hidden"]
+        rng = np.random.default_rng(31)
+        for pos in range(0, 140):
+            e = (rng.standard_normal(H) * 0.5).astype(np.float32)
+            ha, la = ea.talker_forward(e[None], [pos])
+            hg, lg = eg.talker_forward(e[None], [pos])
+            assert np.array_equal(ha, hg) and np.array_equal(la, lg), pos
+        for frame, temperature in ((0, 0.0), (1, 0.9), (2, 0.9)):
+            hid = (rng.standard_normal(H) * 1.5).astype(np.float32)
+            cb0 = int(rng.integers(0, 2048))
+            ca = ea.codepred_frame(hid[None], [cb0], temperature=temperature, top_k=50, seed=3, frame=frame)
+            cg = eg.codepred_frame(hid[None], [cb0], temperature=temperature, top_k=50, seed=3, frame=frame)
+            assert np.array_equal(ca, cg), (frame, ca, cg)
+        assert ea.persist_status() == 0
+    finally:
+        ea.close()
+        eg.close()
 
 
 @pytest.mark.parametrize("temperature", [0.0, 0.9])
