@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <sys/stat.h>
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
@@ -484,7 +485,7 @@ bool Engine::setup_persist() {
     cp_roles_ = persist_cp_ && opt_.cp_roles && c_.cp_layers == 5 && persist_cp_roles_resident(device_);
     tk_roles_ = persist_ && opt_.tk_roles && persist_chunk(max_ctx_) == 64 && persist_tk_roles_supported(max_ctx_) &&
                 persist_tk_roles_resident(device_, max_ctx_);
-    if (!persist_ && !persist_cp_) return true;
+    if (!persist_ && !persist_cp_) return wa_.recv || build_persist_tables();   // (the batched path's table)
     pstate_ = dalloc<uint8_t>(persist_state_bytes());
     if (!pstate_) { set_error("device allocation failed"); return false; }
     if (persist_) {
@@ -520,28 +521,104 @@ bool Engine::setup_persist() {
     return true;
 }
 
-// the persistent code-predictor frame's per-token tables
-// No build buffer is freed: hipFree synchronises the whole device, and a replica or shared rank builds its tables while
-// other contexts on the device may be capturing graphs on other threads (the free invalidated those captures).  The
-// token iota (12 KB) is kept; the 1.7B projected rows' scratch (codec_vocab x H f32) is carved from the QKV table,
-// which is written only after the projected table is complete.
-bool Engine::build_persist_tables() {
-    if (!persist_cp_ || tables_built_) return true;
-    table_iota_ = dalloc<int>(c_.codec_vocab);
-    if (!table_iota_) { set_error("device allocation failed (table token iota)"); return false; }
-    std::vector<int> ih(c_.codec_vocab);
-    for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
-    Q3T_HIP(hipMemcpyAsync(table_iota_, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
-    Q3T_HIP(hipStreamSynchronize(stream_));
-    // (520 MB of f32 for any slot count: a serving context's rare 1-slot calls run the frame with it too)
-    const int QKV = (cpc_.n_heads + 2 * cpc_.n_kv) * cpc_.head_dim;
-    const bool qkv_ok = opt_.cp_qkv_table && c_.codec_vocab == 3072 && c_.cp_vocab == 2048 && (int)cp_embd_.size() >= 14;
-    if (qkv_ok) {
-        cp_qkvtab_ = dalloc<float>(persist_qkv_table_rows() * QKV);
-        if (!cp_qkvtab_) { set_error("device allocation failed (code-predictor QKV table)"); return false; }
+// The code predictor's per-token tables (the layer-0 QKV rows, 520 MB of f32; 1.7B: the projected pass inputs, 130 MB)
+// are functions of the weights alone.  One copy per device serves every context that loaded the same weight file
+// (path, size and modification time: replicas and test contexts of one model), built by the first of them on its own
+// stream and freed with the last one's destruction -- no per-context copy, and no free outside context destruction:
+// hipFree synchronises the whole device, and a free while other contexts' threads capture graphs invalidated those
+// captures (round 4).
+struct CpTables {
+    int device = -1;
+    std::string key;
+    float *qkv = nullptr, *proj = nullptr;
+    size_t bytes = 0;
+    bool built = false;
+    std::mutex build;   // held by the building context; later users wait for the finished tables
+    ~CpTables() {
+        if (device >= 0) hipSetDevice(device);
+        if (qkv) hipFree(qkv);
+        if (proj) hipFree(proj);
     }
-    if (c_.has_mtp && !build_cp_proj_table()) return false;
-    if (qkv_ok && !build_cp_qkv_table()) return false;
+};
+namespace {
+std::mutex g_cp_tables_m;
+std::vector<std::weak_ptr<CpTables>> g_cp_tables;
+std::shared_ptr<CpTables> cp_tables_for(int device, const std::string &key) {
+    std::lock_guard<std::mutex> g(g_cp_tables_m);
+    for (auto it = g_cp_tables.begin(); it != g_cp_tables.end();) {
+        if (auto t = it->lock()) {
+            if (t->device == device && t->key == key) return t;
+            ++it;
+        } else {
+            it = g_cp_tables.erase(it);
+        }
+    }
+    auto t = std::make_shared<CpTables>();
+    t->device = device;
+    t->key = key;
+    g_cp_tables.push_back(t);
+    return t;
+}
+}  // namespace
+
+size_t cp_tables_live_bytes(int device) {   // development / test accounting
+    std::lock_guard<std::mutex> g(g_cp_tables_m);
+    size_t b = 0;
+    for (auto &w : g_cp_tables)
+        if (auto t = w.lock())
+            if (t->device == device) b += t->bytes;
+    return b;
+}
+
+// Built whenever a path reads them: the persistent frame (persist_cp_), or the batched code predictor
+// (Q3T_MM_CP_TABLE, 0.6B shapes), so the batched arithmetic depends on the shapes and options, not on whether this
+// device runs persistent kernels.
+bool Engine::build_persist_tables() {
+    if (tables_built_) return true;
+    const bool qkv_shapes = opt_.cp_qkv_table && c_.codec_vocab == 3072 && c_.cp_vocab == 2048 && (int)cp_embd_.size() >= 14 &&
+                            cpc_.hidden == 1024 && (int)CP_.size() >= 1;
+    const bool want_proj = persist_cp_ && c_.has_mtp;
+    const bool want_qkv = qkv_shapes && (persist_cp_ || (opt_.mm_cp_table && mm_ok_ && max_slots_ > 1));
+    if (!want_proj && !want_qkv) { tables_built_ = true; return true; }
+    struct stat st{};
+    if (stat(tts_path_.c_str(), &st) != 0) { set_error("stat failed: " + tts_path_); return false; }
+    const std::string key = tts_path_ + "|" + std::to_string((long long)st.st_size) + "|" + std::to_string((long long)st.st_mtime) +
+                            (want_proj ? "|proj" : "") + (want_qkv ? "|qkv" : "");
+    cp_tables_ = cp_tables_for(device_, key);
+    std::lock_guard<std::mutex> g(cp_tables_->build);
+    if (!cp_tables_->built) {
+        table_iota_ = dalloc<int>(c_.codec_vocab);
+        if (!table_iota_) { set_error("device allocation failed (table token iota)"); return false; }
+        std::vector<int> ih(c_.codec_vocab);
+        for (int i = 0; i < c_.codec_vocab; ++i) ih[i] = i;
+        Q3T_HIP(hipMemcpyAsync(table_iota_, ih.data(), ih.size() * 4, hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        const int QKV = (cpc_.n_heads + 2 * cpc_.n_kv) * cpc_.head_dim;
+        const size_t rows = persist_qkv_table_rows();
+        if (want_qkv) {
+            if (hipMalloc(&cp_tables_->qkv, rows * QKV * sizeof(float)) != hipSuccess) {
+                cp_tables_->qkv = nullptr;
+                set_error("device allocation failed (code-predictor QKV table)");
+                return false;
+            }
+            cp_tables_->bytes += rows * QKV * sizeof(float);
+        }
+        if (want_proj) {
+            if (hipMalloc(&cp_tables_->proj, rows * c_.cp_hidden * sizeof(float)) != hipSuccess) {
+                cp_tables_->proj = nullptr;
+                set_error("device allocation failed (code-predictor projected table)");
+                return false;
+            }
+            cp_tables_->bytes += rows * c_.cp_hidden * sizeof(float);
+        }
+        cp_qkvtab_ = cp_tables_->qkv;
+        cp_projtab_ = cp_tables_->proj;
+        if (want_proj && !build_cp_proj_table()) return false;
+        if (want_qkv && !build_cp_qkv_table()) return false;
+        cp_tables_->built = true;
+    }
+    cp_qkvtab_ = cp_tables_->qkv;
+    cp_projtab_ = cp_tables_->proj;
     tables_built_ = true;
     return true;
 }
@@ -587,8 +664,6 @@ bool Engine::build_cp_qkv_table() {
 // (130 MB of f32).
 bool Engine::build_cp_proj_table() {
     const int H = c_.hidden, CH = c_.cp_hidden;
-    const size_t rows = persist_qkv_table_rows();
-    cp_projtab_ = dalloc<float>(rows * CH);
     const int *iota = table_iota_;
     // scratch rows: the QKV table's first codec_vocab x H floats when it exists (written after this build), else kept
     float *rowbuf = cp_qkvtab_ ? cp_qkvtab_ : dalloc<float>((size_t)c_.codec_vocab * H);

@@ -269,6 +269,8 @@ private:
     const uint16_t **heads_dev_ = nullptr;
     float *cp_qkvtab_ = nullptr;         // persistent code-predictor frame: layer 0's QKV row per table token
     float *cp_projtab_ = nullptr;        // 1.7B: mtp_proj . f16(table row) + b per table token (f32, code-predictor space)
+    std::shared_ptr<struct CpTables> cp_tables_;   // the two tables above, shared by every context of this device
+                                                   // that loaded the same weight file (engine.cpp, table registry)
     bool build_cp_proj_table();
     bool build_cp_qkv_table();
     bool build_persist_tables();

@@ -43,6 +43,9 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 #ifndef Q3T_CP_MMS
 #define Q3T_CP_MMS 16   // granule stride of the head workgroups' max / min pairs (16: a line each; 2: packed)
 #endif
+#ifndef Q3T_CP_RANGE
+#define Q3T_CP_RANGE 1    // the head workgroups publish each 32-row block's max / min (0: the selection's own B1)
+#endif
 #ifndef Q3T_CP_PREDIV
 #define Q3T_CP_PREDIV 1   // the head workgroups publish the rows divided by T (0: the selecting workgroups divide)
 #endif
@@ -105,7 +108,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
     CLds &S = X.S;
     const int i = blockIdx.x - QW, t = threadIdx.x, l16 = t & 15, grp = t >> 4;
     const float temp = p.sel.temperature;
-    const bool samp = temp > 0.0f;
+    const bool samp = temp > 0.0f && Q3T_CP_RANGE;
     uint4 wq[4][8];
     float4 nw;
     auto issue_qkv = [&](int l) {
@@ -345,10 +348,11 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         // and hands it to the O workgroups (the residual row of layer 0)
         const int hph = ph_of(pass, NLC, 0);
         const bool samp = p.sel.temperature > 0.0f;
+        constexpr bool RNG = Q3T_CP_RANGE;
         const float u = uniform24(spre.seed, spre.utt, (uint64_t)spre.frame, (uint64_t)pass);   // select_token_pre's u
         uint32_t u8[8], mm[2];
         PROF(hph, 0);
-        if (samp) g_wait_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
+        if (samp && RNG) g_wait_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
         else g_wait<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
         PROF(hph, 1);
         float v[SEL_VPT_MAX];
@@ -361,6 +365,8 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             sel = -1;
         } else if (!samp) {
             sel = sel_argmax(v, CPV, 8, S.sel);
+        } else if (!RNG) {
+            sel = select_token_pre<SEL_CP>(sp, spre, v, S.sel);
         } else {   // the row arrives divided by T with the 64 producers' max / min (lane l: producer l)
             float mx = wave_max(__uint_as_float(mm[0])), mn = -wave_max(-__uint_as_float(mm[1]));
             if constexpr (!Q3T_CP_PREDIV) {   // the raw row: divide here (x -> x / T is monotonic, so the max / min of

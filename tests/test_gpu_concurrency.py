@@ -154,3 +154,41 @@ def test_queue_single_slot_fault_recovers():
     finally:
         flt.close()
         ref.close()
+
+
+def _hbm_used():
+    """device 0's used HBM in bytes (hipMemGetInfo through the HIP runtime libq3t.so links)"""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+    return total.value - free.value
+
+
+def test_hbm_per_context_and_replica():
+    """per-context HBM: the bench's single-slot context (weights, KV, state, the code predictor's 520 MB per-token QKV
+    table) and a replica of it on the same device, which copies the weights but shares the table (one copy per device
+    and weight file, engine.cpp CpTables); the table is freed with the last context that uses it"""
+    import q3t
+    tts, tok = synth_dir("full")
+    u0 = _hbm_used()
+    a = q3t.Engine(tts, tok, device=0, max_slots=1, max_ctx=544)
+    u1 = _hbm_used()
+    r = a.replica(0, 1, 544)
+    u2 = _hbm_used()
+    try:
+        assert a.persist_kernels() & 4 and r.persist_kernels() & 4
+        ctx_mb, rep_mb = (u1 - u0) / 2**20, (u2 - u1) / 2**20
+        print(f"HBM per context: {ctx_mb:.0f} MiB (first, table included), replica {rep_mb:.0f} MiB (table shared)")
+        assert rep_mb < ctx_mb - 400, (ctx_mb, rep_mb)
+        H = a.cfg["hidden"]
+        hid = (np.random.default_rng(3).standard_normal((1, H)) * 1.5).astype(np.float32)
+        ca = a.codepred_frame(hid, [77], temperature=0.9, top_k=50, seed=5, frame=3)
+        cr = r.codepred_frame(hid, [77], temperature=0.9, top_k=50, seed=5, frame=3)
+        assert np.array_equal(ca, cr)
+    finally:
+        r.close()
+        a.close()
+    u3 = _hbm_used()
+    print(f"after both closed: {(u3 - u0) / 2**20:.0f} MiB above the start")
+    assert u3 - u0 < 64 * 2**20

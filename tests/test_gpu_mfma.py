@@ -129,3 +129,42 @@ def test_mfma_generate_over_64_slots_matches_oracle():
     finally:
         orc.close()
         eng.close()
+
+
+@pytest.mark.parametrize("table", ["0", "1"])
+def test_mfma_codepred_table_on_off_matches_oracle(table):
+    """the batched code predictor with layer 0 of passes 1..15 read from the per-token QKV table (Q3T_MM_CP_TABLE=1,
+    the 1-slot GEMV's rows) and computed by the MFMA GEMM (=0): both teacher-forced against the oracle at the same
+    tolerance, greedy and sampled (the table is built for any batched context, persistent kernels or not)"""
+    import q3t
+    tts, tok = synth_dir("full")
+    old = os.environ.get("Q3T_MM_CP_TABLE")
+    os.environ["Q3T_MM_CP_TABLE"] = table
+    try:
+        eng = q3t.Engine(tts, None, device=0, max_slots=8, max_ctx=64)
+    finally:
+        if old is None:
+            del os.environ["Q3T_MM_CP_TABLE"]
+        else:
+            os.environ["Q3T_MM_CP_TABLE"] = old
+    orc = Oracle(tts, None)
+    try:
+        H = eng.cfg["hidden"]
+        rng = np.random.default_rng(17)
+        hid = rng.standard_normal((8, H)).astype(np.float32)
+        cb0 = rng.integers(0, 2048, 8).astype(np.int32)
+        off = 0
+        codes, lg = eng.codepred_frame(hid, cb0, temperature=0.0, want_logits=True)
+        for s in range(8):
+            ol = orc.cp_frame_forced(hid[s], int(cb0[s]), codes[s])
+            assert np.abs(lg[s] - ol).max() < LOGIT_TOL["full"]
+            off += sum(check_token(ol[i], int(codes[s, i]), 0.0, 0, 0.0) for i in range(15))
+        codes = eng.codepred_frame(hid, cb0, temperature=0.9, top_k=50, seed=8, frame=2)
+        from oracle_py import uniform
+        for s in range(8):
+            ol = orc.cp_frame_forced(hid[s], int(cb0[s]), codes[s])
+            off += sum(check_token(ol[i], int(codes[s, i]), 0.9, 50, uniform(8, s, 2, i + 1)) for i in range(15))
+        assert off <= 8, off   # of 240 decisions
+    finally:
+        orc.close()
+        eng.close()
