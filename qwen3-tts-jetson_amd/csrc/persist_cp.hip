@@ -71,7 +71,7 @@ static_assert(NQ * 64 == QKVN && NQ * 32 == CPV && NO * 32 == H && NU * 32 == IN
 struct CLds {
     uint16_t xs[INTER];          // f16 activation tile of the current phase
     float xr[32];                // residual rows of this workgroup (O / DN)
-    float red[4][32];            // K-slice partial sums [wave][row] (O / DN)
+    float red[2][4][32];         // K-slice partial sums [layer parity][wave][row] (O / DN)
     float outv[64];              // QKV / head rows staged for one whole-line publish
     double dscr[8];
     float hs[32];                // SwiGLU outputs (GU)
@@ -411,9 +411,11 @@ __device__ __forceinline__ void role_o(Ctx &X) {
         }
     };
     issue(0);
+    int it = 0;   // phase executions: the parity of S.red
     for (int pass = 0; pass < NPASS; ++pass) {
         for (int l = 0; l < NLC; ++l) {
             if (pass == 0 && l == NLC - 1) continue;
+            const int par = it++ & 1;
             const int ph = ph_of(pass, l, 2);
             if (t < 32) {   // the residual rows x_l[32i + t]
                 const int row = 32 * i + t;
@@ -442,7 +444,7 @@ __device__ __forceinline__ void role_o(Ctx &X) {
             Q3T_CP_WAIT<4>(p.gattn + 4 * t, X.tag(ph_of(pass, l, 1)), u, X.c);
             PROF(ph, 1);
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
-            __syncthreads();
+            wave_lds_sync();   // wave w polled exactly the K slice [512 w, 512 w + 512) it multiplies
             float acc[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -454,11 +456,12 @@ __device__ __forceinline__ void role_o(Ctx &X) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 acc[j] = group_sum<16>(acc[j]);
-                if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+                if (l16 == 0) S.red[par][wave][4 * j + grp4] = acc[j];
             }
             __syncthreads();
             if (t < 32) {
-                const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
+                const float (&rd)[4][32] = S.red[par];
+                const float s = rd[0][t] + rd[1][t] + rd[2][t] + rd[3][t];
                 g_put(p.gx2 + 32 * i + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
             }
             PROF(ph, 2);
@@ -548,9 +551,11 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
         }
     };
     issue(0);
+    int it = 0;   // phase executions: the parity of S.red
     for (int pass = 0; pass < NPASS; ++pass) {
         for (int l = 0; l < NLC; ++l) {
             if (pass == 0 && l == NLC - 1) continue;
+            const int par = it++ & 1;
             const int ph = ph_of(pass, l, 4);
             if (t < n) {   // the residual rows x'_l (published a phase earlier)
                 uint32_t u1[1];
@@ -564,7 +569,7 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
             *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t + 8) = make_uint2(u[4], u[5]);
-            __syncthreads();
+            wave_lds_sync();   // wave w polled exactly the K slice [768 w, 768 w + 768) it multiplies
             float acc[5];
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
@@ -576,11 +581,12 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 acc[j] = group_sum<16>(acc[j]);
-                if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+                if (l16 == 0) S.red[par][wave][4 * j + grp4] = acc[j];
             }
             __syncthreads();
             if (t < n) {
-                const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
+                const float (&rd)[4][32] = S.red[par];
+                const float s = rd[0][t] + rd[1][t] + rd[2][t] + rd[3][t];
                 g_put(p.gx + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
             }
             PROF(ph, 2);

@@ -134,6 +134,20 @@ __device__ __forceinline__ void g_wait_gated(const uint64_t *base, uint32_t tag,
     g_wait<N, STRIDE, RUN>(base, tag, out, c);
 }
 
+// LDS written by this wave, then read by this wave only: the wave's own LDS traffic drained, no workgroup barrier
+// (the slowest wave's poll no longer holds the others' dot products).  Q3T_WAVE_SYNC=0: a workgroup barrier.
+#ifndef Q3T_WAVE_SYNC
+#define Q3T_WAVE_SYNC 1
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+    if constexpr (Q3T_WAVE_SYNC) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ float4 f4_of(const uint32_t (&u)[4]) {
     return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
 }

@@ -80,7 +80,7 @@ template <int CPW>
 struct TLds {
     uint16_t xs[INTER];
     float xr[32];
-    float red[4][32];
+    float red[2][4][32];   // [layer parity][wave][row]
     float outv[128];             // QKV / head / O rows staged for one whole-line publish
     double dscr[8];
     float hs[32];
@@ -463,7 +463,7 @@ __device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
         *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t + 8) = make_uint2(u[4], u[5]);
-        __syncthreads();
+        wave_lds_sync();   // wave w polled exactly the K slice [768 w, 768 w + 768) it multiplies
         float acc[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
@@ -475,11 +475,12 @@ __device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             acc[j] = group_sum<16>(acc[j]);
-            if (l16 == 0) S.red[wave][4 * j + grp4] = acc[j];
+            if (l16 == 0) S.red[l & 1][wave][4 * j + grp4] = acc[j];
         }
         __syncthreads();
         if (t < n) {
-            const float s = S.red[0][t] + S.red[1][t] + S.red[2][t] + S.red[3][t];
+            const float (&rd)[4][32] = S.red[l & 1];
+            const float s = rd[0][t] + rd[1][t] + rd[2][t] + rd[3][t];
             g_put(p.gx + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
         }
         PROF(ph, 2);
