@@ -50,7 +50,7 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 #define Q3T_CP_PREDIV 1   // the head workgroups publish the rows divided by T (0: the selecting workgroups divide)
 #endif
 #ifndef Q3T_CP_WAIT
-#define Q3T_CP_WAIT g_wait   // development: g_wait_gated
+#define Q3T_CP_WAIT g_waitc   // contiguous granules (16-byte loads; development: g_wait_gated)
 #endif
 
 namespace q3t {
@@ -243,7 +243,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             } else {
                 uint32_t u[2];
                 PROF(ph, 0);
-                Q3T_CP_WAIT<2, 64>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
+                g_wait<2, 64>(p.gqkv + gi, X.tag(ph_of(pass, l, 0)), u, X.c);
                 PROF(ph, 1);
                 xr[0] = __uint_as_float(u[0]);
                 xr[1] = __uint_as_float(u[1]);
@@ -352,8 +352,13 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         const float u = uniform24(spre.seed, spre.utt, (uint64_t)spre.frame, (uint64_t)pass);   // select_token_pre's u
         uint32_t u8[8], mm[2];
         PROF(hph, 0);
-        if (samp && RNG) g_wait_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
-        else g_wait<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
+        if constexpr (Q3T_POLL16) {
+            if (samp && RNG) g_wait16_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
+            else g_waitc<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
+        } else {
+            if (samp && RNG) g_wait_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
+            else g_wait<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
+        }
         PROF(hph, 1);
         float v[SEL_VPT_MAX];
 #pragma unroll

@@ -80,6 +80,101 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
     for (int i = 0; i < N; ++i) out[i] = (uint32_t)v[i];
 }
 
+// ---------------------------------------------------------------- 16-byte poll loads
+// Two granules per global_load_dwordx4 sc1 (each 8-byte half was written by ONE 8-byte sc1 store and is checked against
+// its own tag, so a pair torn between its halves only costs another poll).  The compiler does not model these inline
+// asm loads: every load is issued, then ONE s_waitcnt vmcnt(0) that names all destinations as in-out operands, so no
+// destination register is read or reused before the wait.  (Q3T_POLL16=0: the 8-byte atomic loads of g_wait.)
+#ifndef Q3T_POLL16
+#define Q3T_POLL16 1
+#endif
+__device__ __forceinline__ void ld16_sc1_issue(const uint64_t *p, u32x4_t &r) {
+    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=&v"(r) : "v"(p) : "memory");
+}
+template <int M>
+__device__ __forceinline__ void ld16_sc1_wait(u32x4_t (&r)[M]) {
+    if constexpr (M == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]) : : "memory");
+    else if constexpr (M == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) : : "memory");
+    else if constexpr (M == 3) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]) : : "memory");
+    else if constexpr (M == 4) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : : "memory");
+    else if constexpr (M == 5) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) : : "memory");
+    else if constexpr (M == 6) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]) : : "memory");
+    else if constexpr (M == 8) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) : : "memory");
+    else static_assert(M == 0, "ld16_sc1_wait: unsupported count");
+}
+// g_wait over RUNS runs of RUN contiguous granules (RUN even, 16-B aligned), run k at base + k * STRIDE
+template <int RUNS, int RUN, int STRIDE = 0>
+__device__ __forceinline__ void g_wait16(const uint64_t *base, uint32_t tag, uint32_t (&out)[RUNS * RUN], Ctl &c) {
+    static_assert(RUN % 2 == 0, "pairs");
+    constexpr int M = RUNS * RUN / 2;
+    u32x4_t r[M];
+    unsigned it = 0;
+    while (true) {
+#pragma unroll
+        for (int k = 0; k < RUNS; ++k)
+#pragma unroll
+            for (int j = 0; j < RUN / 2; ++j) ld16_sc1_issue(base + k * STRIDE + 2 * j, r[k * (RUN / 2) + j]);
+        ld16_sc1_wait<M>(r);
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;
+        if (ok || c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                c.abort = true;
+                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        out[2 * m] = r[m].x;
+        out[2 * m + 1] = r[m].z;
+    }
+}
+// g_wait_pair with 16-byte loads: N contiguous granules at a and M at b (both even, 16-B aligned)
+template <int N, int M2>
+__device__ __forceinline__ void g_wait16_pair(const uint64_t *a, const uint64_t *b, uint32_t tag, uint32_t (&oa)[N], uint32_t (&ob)[M2],
+                                              Ctl &c) {
+    static_assert(N % 2 == 0 && M2 % 2 == 0, "pairs");
+    constexpr int M = (N + M2) / 2;
+    u32x4_t r[M];
+    unsigned it = 0;
+    while (true) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) ld16_sc1_issue(a + 2 * j, r[j]);
+#pragma unroll
+        for (int j = 0; j < M2 / 2; ++j) ld16_sc1_issue(b + 2 * j, r[N / 2 + j]);
+        ld16_sc1_wait<M>(r);
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;
+        if (ok || c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                c.abort = true;
+                __hip_atomic_fetch_or(c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        if constexpr (Q3T_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(Q3T_POLL_SLEEP);
+    }
+#pragma unroll
+    for (int m = 0; m < N / 2; ++m) { oa[2 * m] = r[m].x; oa[2 * m + 1] = r[m].z; }
+#pragma unroll
+    for (int m = 0; m < M2 / 2; ++m) { ob[2 * m] = r[N / 2 + m].x; ob[2 * m + 1] = r[N / 2 + m].z; }
+}
+// the contiguous form of g_wait: N granules at base (16-B aligned)
+template <int N>
+__device__ __forceinline__ void g_waitc(const uint64_t *base, uint32_t tag, uint32_t (&out)[N], Ctl &c) {
+    if constexpr (Q3T_POLL16 && N % 2 == 0) g_wait16<1, N>(base, tag, out, c);
+    else g_wait<N>(base, tag, out, c);
+}
+
 // g_wait over two granule runs a[0..N) and b[0..M) in one poll loop (one round trip per poll for both)
 template <int N, int M>
 __device__ __forceinline__ void g_wait_pair(const uint64_t *a, const uint64_t *b, uint32_t tag, uint32_t (&oa)[N], uint32_t (&ob)[M],

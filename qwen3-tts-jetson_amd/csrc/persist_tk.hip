@@ -168,7 +168,8 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
         } else {
             uint32_t u[4];
             PROF(ph, 0);
-            g_wait_gated<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u, X.c);
+            g_gate(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), X.c);
+            g_waitc<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u, X.c);
             PROF(ph, 1);
             x = f4_of(u);
         }
@@ -377,12 +378,14 @@ __device__ __forceinline__ void tk_gu(Ctx<CPW> &X) {
             xr = layer0_x4(p);
         } else {
             uint32_t u4[4];
-            g_wait<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u4, X.c);
+            g_waitc<4>(p.gx + 4 * t, X.tag(5 * (l - 1) + 4), u4, X.c);
             xr = f4_of(u4);
         }
         uint32_t u[16];   // K-slice sums o_w of rows 4t..4t+3 (w = 0..3)
         PROF(ph, 0);
-        g_wait_gated<16, H, 4>(p.gop + 4 * t, X.tag(5 * l + 2), u, X.c);
+        g_gate(p.gop + 4 * t, X.tag(5 * l + 2), X.c);
+        if constexpr (Q3T_POLL16) g_wait16<4, 4, H>(p.gop + 4 * t, X.tag(5 * l + 2), u, X.c);
+        else g_wait<16, H, 4>(p.gop + 4 * t, X.tag(5 * l + 2), u, X.c);
         PROF(ph, 1);
         float x[4];
 #pragma unroll
@@ -458,7 +461,8 @@ __device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
         }
         uint32_t u[6];
         PROF(ph, 0);
-        g_wait_gated<6>(p.gh + 6 * t, X.tag(5 * l + 3), u, X.c);
+        g_gate(p.gh + 6 * t, X.tag(5 * l + 3), X.c);
+        g_waitc<6>(p.gh + 6 * t, X.tag(5 * l + 3), u, X.c);
         PROF(ph, 1);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
         *reinterpret_cast<uint2 *>(S.xs + 12 * t + 4) = make_uint2(u[2], u[3]);
@@ -733,7 +737,7 @@ __device__ __forceinline__ void tk_sel(Ctx<CPW> &X) {
     __syncthreads();
     uint32_t u[VOC / 256];
     PROF(hph, 0);
-    g_wait<VOC / 256>(p.glog + t * (VOC / 256), X.tag(hph), u, X.c);
+    g_waitc<VOC / 256>(p.glog + t * (VOC / 256), X.tag(hph), u, X.c);
     PROF(hph, 1);
     if (p.sel.mode != SEL_NONE) {
         float v[SEL_VPT_MAX];
