@@ -208,7 +208,7 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
     const int hph = 5 * nl;
     uint32_t u[4];
     PROF(hph, 0);
-    Q3T_TK_WAIT_ATT<4>(p.gx + 4 * t, X.tag(5 * (nl - 1) + 4), u, X.c);
+    g_waitc<4>(p.gx + 4 * t, X.tag(5 * (nl - 1) + 4), u, X.c);
     PROF(hph, 1);
     rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, i == 0 ? p.hidden : nullptr);
     __syncthreads();
