@@ -131,22 +131,30 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         for (int e = 0; e < 8; ++e) q8[h][e] = h < R ? q_s[h][li * 8 + e] : 0.0f;
     float sc[NP][RMAX];
     bool ok[NP];
+    uint32_t qp[RMAX][4];
+#pragma unroll
+    for (int h = 0; h < RMAX; ++h) pack_q8(q8[h], qp[h]);
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
         const int j = j0 + pi * PPP + pg;
         ok[pi] = j <= pos;
-        float k8[8];
-        if (j == pos) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) k8[e] = kn_s[li * 8 + e];
-        } else {
-            unpack8(kr[pi], k8);
-        }
 #pragma unroll
         for (int h = 0; h < RMAX; ++h) {
-            float s = 0.0f;
+            float s;
+            if constexpr (Q3T_ATTN_DOT2) {   // score8 (q3t_common.h): identical in every single-slot attention kernel
+                s = score8(j == pos ? pack8f(&kn_s[li * 8]) : kr[pi], qp[h]);
+            } else {
+                float k8[8];
+                if (j == pos) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);   // explicit fma: identical in k_attn and persist.hip
+                    for (int e = 0; e < 8; ++e) k8[e] = kn_s[li * 8 + e];
+                } else {
+                    unpack8(kr[pi], k8);
+                }
+                s = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);   // explicit fma: identical in k_attn and persist.hip
+            }
             s = group_sum<LPP>(s);
             sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
         }
@@ -174,7 +182,7 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         float l = 0.0f;
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
-            pr[pi][h] = ok[pi] ? expf(__fsub_rn(sc[pi][h], M[h])) : 0.0f;
+            pr[pi][h] = ok[pi] ? exp_sm(__fsub_rn(sc[pi][h], M[h])) : 0.0f;
             l += pr[pi][h];
         }
         if constexpr (LPP == 16) l = rows_sum(l);
@@ -698,20 +706,26 @@ __global__ void __launch_bounds__(PF_THREADS) k_prefill_attn(const PrefillAttnPa
         float q8[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) q8[e] = q_s[i][h][li * 8 + e];
+        uint32_t qp[4];
+        pack_q8(q8, qp);
         float sc[PMAX];
         float m = -INFINITY;
 #pragma unroll
         for (int j = 0; j < PMAX; ++j) {   // rows j >= plen hold stale LDS: computed, then masked
             float d = 0.0f;
+            if constexpr (Q3T_ATTN_DOT2) {
+                d = score8(pack8f(&k_s[j][li * 8]), qp);
+            } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) d = __fmaf_rn(k_s[j][li * 8 + e], q8[e], d);
+                for (int e = 0; e < 8; ++e) d = __fmaf_rn(k_s[j][li * 8 + e], q8[e], d);
+            }
             d = group_sum<LPP>(d);
             sc[j] = j <= i ? __fmul_rn(d, kq_scale) : -INFINITY;
             m = fmaxf(m, sc[j]);
         }
         float pj[PMAX];
 #pragma unroll
-        for (int j = 0; j < PMAX; ++j) pj[j] = j <= i ? expf(__fsub_rn(sc[j], m)) : 0.0f;
+        for (int j = 0; j < PMAX; ++j) pj[j] = j <= i ? exp_sm(__fsub_rn(sc[j], m)) : 0.0f;
         const float l = tree16(pj);
         uint16_t *o = p.out + (size_t)(u * plen + i) * p.nH * D + (size_t)(g * R + h) * D + li * 8;
 #pragma unroll

@@ -358,24 +358,32 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 for (int e = 0; e < 8; ++e) q8[h][e] = S.q_s[h][li * 8 + e];
             float sc[NP][R];
             bool ok[NP];
+            uint32_t qp[R][4];
+#pragma unroll
+            for (int h = 0; h < R; ++h) pack_q8(q8[h], qp[h]);
 #pragma unroll
             for (int pi = 0; pi < NP; ++pi) {
                 const int j = j0 + pi * 16 + pg;
                 ok[pi] = j <= pos;
-                float k8[8];
-                if (j == pos) {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) k8[e] = S.kn_s[li * 8 + e];
-                } else {
-                    const uint32_t ww[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) { k8[2 * e] = h2f(ww[e] & 0xffff); k8[2 * e + 1] = h2f(ww[e] >> 16); }
-                }
 #pragma unroll
                 for (int h = 0; h < R; ++h) {
-                    float s = 0.0f;
+                    float s;
+                    if constexpr (Q3T_ATTN_DOT2) {
+                        s = score8(j == pos ? pack8f(&S.kn_s[li * 8]) : kr[pi], qp[h]);
+                    } else {
+                        float k8[8];
+                        if (j == pos) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);   // explicit fma: identical in k_attn and persist.hip
+                            for (int e = 0; e < 8; ++e) k8[e] = S.kn_s[li * 8 + e];
+                        } else {
+                            const uint32_t ww[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) { k8[2 * e] = h2f(ww[e] & 0xffff); k8[2 * e + 1] = h2f(ww[e] >> 16); }
+                        }
+                        s = 0.0f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);   // explicit fma: identical in k_attn and persist.hip
+                    }
                     s = group_sum<16>(s);
                     sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
                 }
@@ -400,7 +408,7 @@ __global__ void __launch_bounds__(256) k_persist(const PersistParams p) {
                 float lsum = 0.0f;
 #pragma unroll
                 for (int pi = 0; pi < NP; ++pi) {
-                    pr[pi][h] = ok[pi] ? expf(__fsub_rn(sc[pi][h], M[h])) : 0.0f;
+                    pr[pi][h] = ok[pi] ? exp_sm(__fsub_rn(sc[pi][h], M[h])) : 0.0f;
                     lsum += pr[pi][h];
                 }
                 lsum = rows_sum(lsum);

@@ -284,13 +284,13 @@ __device__ __forceinline__ void role_att(Ctx &X) {
             for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) q8[h][e] = S.q_s[h][li * 8 + e];
+            const uint4 kk = *reinterpret_cast<const uint4 *>(&S.kc[l][pg][li * 8]);
             {
-                const uint4 kk = *reinterpret_cast<const uint4 *>(&S.kc[l][pg][li * 8]);
                 const uint4 vv = *reinterpret_cast<const uint4 *>(&S.vc[l][pg][li * 8]);
                 const uint32_t kw[4] = {kk.x, kk.y, kk.z, kk.w}, vw[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    k8[2 * e] = h2f(kw[e] & 0xffff); k8[2 * e + 1] = h2f(kw[e] >> 16);
+                    if constexpr (!Q3T_ATTN_DOT2) { k8[2 * e] = h2f(kw[e] & 0xffff); k8[2 * e + 1] = h2f(kw[e] >> 16); }
                     v8[2 * e] = h2f(vw[e] & 0xffff); v8[2 * e + 1] = h2f(vw[e] >> 16);
                 }
             }
@@ -298,8 +298,14 @@ __device__ __forceinline__ void role_att(Ctx &X) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 float s = 0.0f;
+                if constexpr (Q3T_ATTN_DOT2) {   // score8 (q3t_common.h), as k_attn
+                    uint32_t qp[4];
+                    pack_q8(q8[h], qp);
+                    s = score8(kk, qp);
+                } else {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);
+                    for (int e = 0; e < 8; ++e) s = __fmaf_rn(k8[e], q8[h][e], s);
+                }
                 s = group_sum<16>(s);
                 sc[h] = ok ? __fmul_rn(s, kq_scale) : -INFINITY;
                 const float m = rows_max(sc[h]);
@@ -309,7 +315,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) M[h] = fmaxf(fmaxf(S.wred[0][h], S.wred[1][h]), fmaxf(S.wred[2][h], S.wred[3][h]));
 #pragma unroll
-            for (int h = 0; h < 2; ++h) pr[h] = ok ? expf(__fsub_rn(sc[h], M[h])) : 0.0f;
+            for (int h = 0; h < 2; ++h) pr[h] = ok ? exp_sm(__fsub_rn(sc[h], M[h])) : 0.0f;
             {   // rows_sum of both heads at once: row 0 ends with head 0's (r0 + r1) + (r2 + r3), row 1 with head 1's
                 const float lsum = rows_sum_pair(pr[0], pr[1]);
                 if ((lane & 47) == 0) S.wsum[wave][lane >> 4] = lsum;   // lanes 0, 16

@@ -570,24 +570,32 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) q8[h][e] = S.q_s[h][li * 8 + e];
         float sc[NP][R];
+        uint32_t qp[R][4];
+#pragma unroll
+        for (int h = 0; h < R; ++h) pack_q8(q8[h], qp[h]);
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
             const int j = j0 + pi * 16 + pg;
             const bool ok = j <= pos;
-            float k8[8];
-            if (j == pos) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) k8[e] = S.kn_s[li * 8 + e];
-            } else {
-                const uint32_t ww[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { k8[2 * e] = h2f(ww[e] & 0xffff); k8[2 * e + 1] = h2f(ww[e] >> 16); }
-            }
 #pragma unroll
             for (int h = 0; h < R; ++h) {
-                float sv = 0.0f;
+                float sv;
+                if constexpr (Q3T_ATTN_DOT2) {
+                    sv = score8(j == pos ? pack8f(&S.kn_s[li * 8]) : kr[pi], qp[h]);
+                } else {
+                    float k8[8];
+                    if (j == pos) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) sv = __fmaf_rn(k8[e], q8[h][e], sv);   // explicit fma: identical in k_attn
+                        for (int e = 0; e < 8; ++e) k8[e] = S.kn_s[li * 8 + e];
+                    } else {
+                        const uint32_t ww[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) { k8[2 * e] = h2f(ww[e] & 0xffff); k8[2 * e + 1] = h2f(ww[e] >> 16); }
+                    }
+                    sv = 0.0f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) sv = __fmaf_rn(k8[e], q8[h][e], sv);   // explicit fma: identical in k_attn
+                }
                 sv = group_sum<16>(sv);
                 sc[pi][h] = ok ? __fmul_rn(sv, kq_scale) : -INFINITY;
             }
@@ -627,7 +635,7 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                 for (int q = 0; q < 4; ++q) {
                     const int pi = 4 * cc + q;
                     const bool ok = j0 + pi * 16 + pg <= pos;
-                    pr[q][h] = ok ? expf(__fsub_rn(sc[pi][h], M[cc][h])) : 0.0f;
+                    pr[q][h] = ok ? exp_sm(__fsub_rn(sc[pi][h], M[cc][h])) : 0.0f;
                     ls[h] += pr[q][h];
                 }
             }

@@ -44,6 +44,30 @@ __device__ __forceinline__ float dot8(const uint4 &a, const uint4 &b, float acc)
     acc = __builtin_amdgcn_fdot2(__builtin_bit_cast(half2_t, a.w), __builtin_bit_cast(half2_t, b.w), acc, false);
     return acc;
 }
+__device__ __forceinline__ float score8(const uint4 &k, const uint32_t (&qp)[4]) {
+    return dot8(k, make_uint4(qp[0], qp[1], qp[2], qp[3]), 0.0f);
+}
+
+// ---------------------------------------------------------------- decode-attention score / softmax arithmetic
+// One lane's share of a q.k score: 8 dims, k as packed f16 (the cache's own bits), q as 4 packed f16 pairs (q is
+// f16-rounded before the scores, so the packing is exact), summed by v_dot2_f32_f16 onto 0 in dim order (dot8).
+// Every single-slot attention kernel (k_attn, k_prefill_attn, persist.hip, persist_tk.hip, persist_cp.hip) scores and
+// exponentiates with these two functions, so the persistent kernels stay bit-identical to the launch-per-op graph.
+#ifndef Q3T_ATTN_DOT2
+#define Q3T_ATTN_DOT2 1
+#endif
+__device__ __forceinline__ uint32_t pk_f16x2(float a, float b) {   // exact for f16-representable a, b
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+__device__ __forceinline__ void pack_q8(const float (&q8)[8], uint32_t (&qp)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) qp[e] = pk_f16x2(q8[2 * e], q8[2 * e + 1]);
+}
+__device__ __forceinline__ uint4 pack8f(const float *x) {   // 8 f16-exact floats -> packed f16
+    return make_uint4(pk_f16x2(x[0], x[1]), pk_f16x2(x[2], x[3]), pk_f16x2(x[4], x[5]), pk_f16x2(x[6], x[7]));
+}
+// the softmax exponential of (score - max) <= 0: v_exp_f32 on x * log2(e)
+__device__ __forceinline__ float exp_sm(float x) { return Q3T_ATTN_DOT2 ? __expf(x) : expf(x); }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // 16-byte load through a global (address space 1) pointer: global_load_dwordx4, never a flat load (a flat load counts
