@@ -324,7 +324,10 @@ __device__ __forceinline__ void role_att(Ctx &X) {
                 // 8 + k, 12 + k (value n = 8 h + e), each (r0 + r1) + (r2 + r3) as rows_sum
                 float v16[16], c8[8];
 #pragma unroll
-                for (int n = 0; n < 16; ++n) v16[n] = __fmaf_rn(pr[n >> 3], ok ? v8[n & 7] : 0.0f, 0.0f);
+                for (int n = 0; n < 16; n += 2) {   // packed fmas onto 0 (v_pk_fma_f32), the same roundings
+                    v16[n] = v16[n + 1] = 0.0f;
+                    fma2(pr[n >> 3], ok ? v8[n & 7] : 0.0f, ok ? v8[(n + 1) & 7] : 0.0f, v16[n], v16[n + 1]);
+                }
 #pragma unroll
                 for (int m = 0; m < 8; ++m) {
                     const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v16[2 * m]), __float_as_uint(v16[2 * m + 1]), false, false);

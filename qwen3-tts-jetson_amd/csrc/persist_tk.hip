@@ -665,7 +665,8 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
 #pragma unroll
                 for (int h = 0; h < R; ++h)
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr[q][h], ok ? v8[e] : 0.0f, acc[h][e]);
+                    for (int e = 0; e < 8; e += 2)   // packed fmas (v_pk_fma_f32), the same roundings
+                        fma2(pr[q][h], ok ? v8[e] : 0.0f, ok ? v8[e + 1] : 0.0f, acc[h][e], acc[h][e + 1]);
             }
             // rows_sum of the 16 accumulators as a reduce-scatter (12 row swaps in place of 32): row k ends with values
             // k, 4 + k, 8 + k, 12 + k (value n = 8 h + e), each (r0 + r1) + (r2 + r3) as rows_sum

@@ -69,6 +69,22 @@ __device__ __forceinline__ uint4 pack8f(const float *x) {   // 8 f16-exact float
 // the softmax exponential of (score - max) <= 0: v_exp_f32 on x * log2(e)
 __device__ __forceinline__ float exp_sm(float x) { return Q3T_ATTN_DOT2 ? __expf(x) : expf(x); }
 
+// two fmas as one v_pk_fma_f32 (each lane element is the IEEE fma of its pair: bit-identical to two __fmaf_rn)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+#ifndef Q3T_PK_FMA
+#define Q3T_PK_FMA 1
+#endif
+__device__ __forceinline__ void fma2(float a, float b0, float b1, float &c0, float &c1) {
+    if constexpr (Q3T_PK_FMA) {
+        const f32x2_t r = __builtin_elementwise_fma(f32x2_t{a, a}, f32x2_t{b0, b1}, f32x2_t{c0, c1});
+        c0 = r.x;
+        c1 = r.y;
+    } else {
+        c0 = __fmaf_rn(a, b0, c0);
+        c1 = __fmaf_rn(a, b1, c1);
+    }
+}
+
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // 16-byte load through a global (address space 1) pointer: global_load_dwordx4, never a flat load (a flat load counts
 // in both vmcnt and lgkmcnt, so its waits also drain the LDS traffic around it)

@@ -601,6 +601,11 @@ __device__ __forceinline__ void sel_prefetch(const SelectSpec &sp, int s, SelPre
     }
 }
 
+// Calling rule of every selection entry point (select_token_pre / select_token_regs / select_token / select_slot,
+// sel_sample, sel_sample_range): the workgroup runs a barrier between two selections, and SelLds is not aliased by LDS
+// the caller writes in between.  The selection writes its histogram, candidate list and per-wave slots without a
+// leading barrier (the previous selection's readers are behind the caller's barrier); all current callers (gemv_kernel.h's
+// kSel / kSelG loops, kernels.hip, k_tk_roles, k_cp_roles, k_persist) keep the rule.
 // the token of a slot from its prefetched inputs (uniform over the workgroup), or -1 if the slot is done; no side
 // effects.  MODE: SEL_CB0 / SEL_CP at compile time (the code-predictor path carries none of the CB0 rules)
 template <int MODE>
