@@ -92,6 +92,7 @@ Options Options::from_env() {
     o.cp_qkv_table = env_flag("Q3T_CP_QKV_TABLE", true);
     o.cp_roles = env_flag("Q3T_CP_ROLES", true);
     o.mm_cp_table = env_flag("Q3T_MM_CP_TABLE", true);
+    o.fold_advance = env_flag("Q3T_FOLD_ADVANCE", true);
     o.tk_roles = env_flag("Q3T_TK_ROLES", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
@@ -988,7 +989,7 @@ SelectSpec Engine::select_spec(int mode, const GenParams &gp, int frame_offset, 
 // gather_input: the step embedding (tts_transformer.cpp:2529-2553) is assembled by layer 0's QKV prologue from the
 // frame's 16 codes (PRO_RMS_G16) instead of being read from x_
 // select_next: the codec head's last workgroup also selects CB0 of the NEXT frame (frame_ + 1) in the same launch
-bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed) {
+bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed, bool *fold_advance) {
     const int H = c_.hidden;
     const size_t kv_layer = (size_t)max_slots_ * c_.n_kv * max_ctx_ * c_.head_dim;
     const int max_splits = (max_ctx_ + ATTN_CHUNK - 1) / ATTN_CHUNK;
@@ -1005,7 +1006,13 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         p.head = codec_head_; p.out_norm = out_norm_; p.hidden = hidden_; p.logits = logits_;
         if (select_next) p.sel = select_spec(SEL_CB0, gp_, 1, 0);
         p.prof = pprof_;
-        if (tk_roles_) return persist_tk_roles(p, s);
+        if (tk_roles_) {
+            if (fold_advance && opt_.fold_advance) {
+                p.adv_pos = pos_; p.adv_frame = frame_; p.adv_done = done_;
+                *fold_advance = true;
+            }
+            return persist_tk_roles(p, s);
+        }
         return persist_talker_step(p, s);
     }
     StackInput in0;
@@ -1184,8 +1191,9 @@ bool Engine::enqueue_frame(int S, hipStream_t s) {
     const bool mm = use_mm(S);
 #endif
     if (!enqueue_cp_frame(S, s, nullptr, mm)) return false;
-    if (!enqueue_talker(S, s, true, fused_select_, mm)) return false;
-    return advance(pos_, frame_, done_, S, s);
+    bool folded = false;   // the single-slot role kernel advances pos / frame itself
+    if (!enqueue_talker(S, s, true, fused_select_, mm, &folded)) return false;
+    return folded || advance(pos_, frame_, done_, S, s);
 }
 
 bool Engine::graph_for(std::map<int, hipGraphExec_t> &cache, int S, bool (Engine::*fn)(int, hipStream_t)) {

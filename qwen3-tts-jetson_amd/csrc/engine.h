@@ -63,6 +63,7 @@ struct Options {
     bool cp_qkv_table = true;   // Q3T_CP_QKV_TABLE: the persistent code-predictor frame reads layer 0's QKV rows from a table
     bool cp_roles = true;       // Q3T_CP_ROLES: that frame on role-specialised workgroups (persist_cp.hip)
     bool mm_cp_table = true;    // Q3T_MM_CP_TABLE: batched code predictor, layer 0 of passes 1..15 from the QKV table
+    bool fold_advance = true;   // Q3T_FOLD_ADVANCE: the single-slot role talker kernel advances pos / frame (no k_advance)
     bool tk_roles = true;       // Q3T_TK_ROLES: the 1-slot talker step on role-specialised workgroups (persist_tk.hip)
     bool attn_split = false;
     unsigned persist_fault_at = 0;
@@ -173,7 +174,8 @@ private:
     bool ensure_pinned(size_t bytes);
     bool ensure_qout(size_t bytes);
     bool enqueue_talker_step(int S, hipStream_t s);
-    bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed = false);
+    bool enqueue_talker(int S, hipStream_t s, bool gather_input, bool select_next, bool prenormed = false,
+                        bool *fold_advance = nullptr);
     SelectSpec select_spec(int mode, const GenParams &gp, int frame_offset, int step) const;
     bool enqueue_cp_frame(int S, hipStream_t s, float *logits_host = nullptr, bool talker_next = false);
     bool enqueue_frame(int S, hipStream_t s);

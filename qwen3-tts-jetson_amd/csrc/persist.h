@@ -57,6 +57,11 @@ struct PersistParams {
     // code-predictor frame (1.7B): the pass inputs of passes 1..15 as projected f32 rows [3072 + 14 * 2048][1024] in
     // place of the f16 table rows (gs.tabs), same row order as qkvtab; x_in is then the projected pass-0 input
     const float *xtab = nullptr;
+    // frame graph (k_tk_roles only): after its commit the selecting workgroup advances slot 0 exactly as k_advance
+    // would (pos + 1, frame + 1 unless done), so the frame needs no k_advance launch.  Null: no advance (stage replays,
+    // talker_forward)
+    int *adv_pos = nullptr, *adv_frame = nullptr;
+    const int *adv_done = nullptr;
     uint64_t *prof = nullptr;      // development timeline [256][PROF_PH][4] (null = off)
     int roles_split = 0;           // persist_tk.hip: attention splits per kv group (set by the launcher)
     unsigned *seq = nullptr, *head_ticket = nullptr, *err = nullptr;

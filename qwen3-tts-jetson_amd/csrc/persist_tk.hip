@@ -757,6 +757,12 @@ __device__ __forceinline__ void tk_sel(Ctx<CPW> &X) {
     __syncthreads();
     if (t == 0) {
         if (tok >= 0) select_commit(p.sel, 0, tok);
+        // k_advance folded into the launch (every workgroup read pos / frame at its start or in layer 0, long before
+        // this point; the next launch sees the stores)
+        if (p.adv_pos && !(p.adv_done && p.adv_done[0] >= 0)) {
+            p.adv_pos[0] += 1;
+            p.adv_frame[0] += 1;
+        }
         __hip_atomic_store(p.seq, X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     PROF(hph, 2);
