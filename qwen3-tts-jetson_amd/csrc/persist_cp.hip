@@ -40,6 +40,9 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_PUT_FIRST   // a role's publish: the other waves issue the next weight prefetch only after wave 0's store
+#define Q3T_CP_PUT_FIRST 1   // (their loads, 128 KB per QKV workgroup, otherwise queue ahead of it in the CU's memory pipe)
+#endif
 #ifndef Q3T_CP_MMS
 #define Q3T_CP_MMS 16   // granule stride of the head workgroups' max / min pairs (16: a line each; 2: packed)
 #endif
@@ -164,6 +167,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             // waves into shared lines make the next edge slower
             if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
             PROF(ph, 2);
+            if (Q3T_CP_PUT_FIRST) __syncthreads();   // the publish store enters the CU's memory pipe before the prefetch
             if (l + 1 < NLC) issue_qkv(l + 1);
             else if (pass >= 1) issue_head(pass);
             else issue_qkv(1);   // pass 0 has no head; layer 0 of the next passes comes from the table
@@ -193,6 +197,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             if (l16 == 0) S.outv[16 * j + grp] = lg;
         }
         __syncthreads();
+        PROF(hph, 3);   // (development timeline: head rows reduced)
         if (t < 64) {   // wave 0, ONE store instruction: lanes 0..31 publish the rows, lanes 32 / 33 (sampling) their max
                         // and finite min
             // sampling: the rows divided by T (the selection's first step, the same IEEE division) and the 32 rows'
@@ -206,6 +211,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             if (t < 32) p.logits[32 * i + t] = lg;   // read after the launch only (host, tests)
         }
         PROF(hph, 2);
+        if (Q3T_CP_PUT_FIRST) __syncthreads();
         if (pass + 1 < NPASS) issue_qkv(1);
     }
 }
@@ -479,6 +485,7 @@ __device__ __forceinline__ void role_o(Ctx &X) {
                 g_put(p.gx2 + 32 * i + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
             }
             PROF(ph, 2);
+            if (Q3T_CP_PUT_FIRST) __syncthreads();
             const int nl = (l + 1 < NLC && !(pass == 0 && l + 1 == NLC - 1)) ? l + 1 : 0;
             if (!(pass + 1 == NPASS && l + 1 == NLC)) issue(nl);
         }
@@ -542,6 +549,7 @@ __device__ __forceinline__ void role_gu(Ctx &X) {
             __syncthreads();
             if (t < 16) g_put(p.gh + 16 * i + t, (uint32_t)f2h(S.hs[2 * t]) | ((uint32_t)f2h(S.hs[2 * t + 1]) << 16), X.tag(ph));
             PROF(ph, 2);
+            if (Q3T_CP_PUT_FIRST) __syncthreads();
             const int nl = (l + 1 < NLC && !(pass == 0 && l + 1 == NLC - 1)) ? l + 1 : 0;
             if (!(pass + 1 == NPASS && l + 1 == NLC)) issue(nl);
         }
@@ -604,6 +612,7 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
                 g_put(p.gx + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
             }
             PROF(ph, 2);
+            if (Q3T_CP_PUT_FIRST) __syncthreads();
             const int nl = (l + 1 < NLC && !(pass == 0 && l + 1 == NLC - 1)) ? l + 1 : 0;
             if (!(pass + 1 == NPASS && l + 1 == NLC)) issue(nl);
         }

@@ -52,6 +52,9 @@ constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of pos
 // workgroups' combine sweeps shared the CU with the partials' producers: 0.385 vs 0.376 ms at position 266, 0.392 vs
 // 0.382 at 500, 0.480 vs 0.476 at 1500.  Beside the QKV workgroups, which issue the next layer's rows right at the
 // QKV -> attention edge, a split's poll arrived 2.3 us late (round 4, before the gated polls).
+#ifndef Q3T_TK_PUT_FIRST   // a role's publish: the other waves issue the next layer's weight prefetch only after wave 0's
+#define Q3T_TK_PUT_FIRST 0   // store instruction (their loads otherwise queue ahead of it in the CU's memory pipe)
+#endif
 #ifndef Q3T_TK_PAIR
 #define Q3T_TK_PAIR 1   // development: 0 = O, gate/up, down, QKV; 1 = down, O, gate/up, QKV (the splits beside down)
 #endif
@@ -192,6 +195,7 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
         // into shared lines make the next edge slower
         if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
         PROF(ph, 2);
+        if (Q3T_TK_PUT_FIRST) __syncthreads();
         if (l + 1 < nl) {
             issue_qkv(l + 1);
         } else {   // codec head rows 48i + 16j + grp
@@ -345,6 +349,7 @@ __device__ __forceinline__ void tk_o(Ctx<CPW> &X) {
         // two store instructions (waves 0, 1: whole lines each) publish the slice sums of the 128 rows
         if (t < 128) g_put(p.gop + (size_t)w * H + 128 * rb + t, __float_as_uint(S.outv[t]), X.tag(ph));
         PROF(ph, 2);
+        if (Q3T_TK_PUT_FIRST) __syncthreads();
         if (l + 1 < nl) issue(l + 1);
     }
 }
@@ -421,6 +426,7 @@ __device__ __forceinline__ void tk_gu(Ctx<CPW> &X) {
         __syncthreads();
         if (t < 16) g_put(p.gh + 16 * i + t, (uint32_t)f2h(S.hs[2 * t]) | ((uint32_t)f2h(S.hs[2 * t + 1]) << 16), X.tag(ph));
         PROF(ph, 2);
+        if (Q3T_TK_PUT_FIRST) __syncthreads();
         if (l + 1 < nl) issue(l + 1);
     }
 }
@@ -488,6 +494,7 @@ __device__ __forceinline__ void tk_dn(Ctx<CPW> &X) {
             g_put(p.gx + lo + t, __float_as_uint(S.xr[t] + s), X.tag(ph));
         }
         PROF(ph, 2);
+        if (Q3T_TK_PUT_FIRST) __syncthreads();
         if (l + 1 < nl) issue(l + 1);
     }
 }

@@ -132,12 +132,17 @@ def test_gpu_speaker_embedding_matches_oracle(gpu_pair, seconds):
 
 @pytest.mark.gpu
 def test_gpu_speaker_embedding_drives_generation(gpu_pair):
-    """voice cloning chain: encode_speaker -> the speaker row of the prefill (build_prefill_graph's speaker slot)"""
-    from q3t_testutil import prompt
+    """voice cloning chain: encode_speaker -> the speaker row of the prefill (build_prefill_graph's speaker slot) ->
+    generate, teacher-forced against the oracle chain (the oracle's own speaker embedding and decisions).  Greedy codes
+    of the random-weight model are not compared one to one: the GPU and oracle embeddings differ by ~3e-4 relative, and
+    a near-tie at the first decision flips every later code, so each GPU decision is checked against the oracle's
+    logits for the GPU's own history instead (check_decisions, the same near-tie rule as the generate tests)."""
+    from q3t_testutil import check_decisions, prompt
     eng, o = gpu_pair
-    spk = eng.encode_speaker(voice_like(2.0))
+    x = voice_like(2.0)
+    spk, spk_o = eng.encode_speaker(x), o.encode_speaker(x)
     a = eng.generate([prompt("full")], speakers=[spk], max_len=8, temperature=0.0, force_frames=8)[0]
-    b = eng.generate([prompt("full")], speakers=[o.encode_speaker(voice_like(2.0))], max_len=8, temperature=0.0,
-                     force_frames=8)[0]
+    n = eng.generate([prompt("full")], max_len=8, temperature=0.0, force_frames=8)[0]
     assert a.shape == (8, 16)
-    assert (a == b).mean() > 0.9
+    assert (a != n).any()   # the speaker row reaches the decisions
+    check_decisions(o, prompt("full"), spk_o, a, max_len=8, force_frames=8)
