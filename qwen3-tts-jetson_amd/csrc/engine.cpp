@@ -801,9 +801,11 @@ static bool prefill_layer_attn(const PrefillAttnParams &pf, const Config &c, con
     return prefill_attn(q, s);
 }
 
-// weight prefetch of the batched talker stack: 0 off, 1 the norms before QKV and gate/up, 2 also the gate/up GEMM for
-// the down projection (its 64-token tiles leave a quarter of the CUs free)
-static const int g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return e ? std::atoi(e) : 2; }();
+// weight prefetch of the batched talker stack: 0 off (default), 1 the norms before QKV and gate/up, 2 also the gate/up
+// GEMM for the down projection (its 64-token tiles leave a quarter of the CUs free).  Off since round 5: level 2 saved
+// 0.3 % of the 64-slot step (1.5960 -> 1.5912 ms, two A/B pairs) for 755 MB more fabric reads per step (FETCH 3,111 ->
+// 3,866 MB: every prefetched line is read twice, once into the Infinity Cache and once by the GEMM)
+static const int g_mm_prefetch = [] { const char *e = std::getenv("Q3T_MM_PREFETCH"); return e ? std::atoi(e) : 0; }();
 // gate/up on 64-token tiles: 192 workgroups of one per CU instead of 384 (two on half the CUs, which set the tail);
 // the other projections keep 32-token tiles.  64-slot talker step 1.574 -> 1.549 ms (two A/B pairs,
 // tools/dev/exp_gutt.sh); the tile never changes a row's arithmetic.  Q3T_MM_GU_TT=1 restores 32-token tiles.

@@ -1,4 +1,5 @@
-"""dev: split a frame-loop kernel trace into code-predictor and talker phases.  Frames are delimited by k_advance;
+"""dev: split a frame-loop kernel trace into code-predictor and talker phases.  Frames are delimited by k_advance (or,
+when the persistent talker step folds the advance in, by that step);
 the talker phase is the last TALKER_KERNELS (5 per layer x 28 + codec head = 141) kernels before it, everything
 earlier in the frame is the code-predictor phase.  Prints per-kernel avg durations and per-phase spans."""
 import collections
@@ -23,11 +24,18 @@ for row in rows:
         cur = []
     else:
         cur.append(row)
+        # the persistent talker step folds the advance in (no k_advance launch): it closes the frame itself
+        if persistent and row[2].startswith(("k_tk_roles", "k_persist<0")) and not any(r[2] == "k_advance" for r in rows):
+            frames.append(cur)
+            cur = []
 print(f"({len(rows)} kernels, {sum(1 for r in rows if r[2] == 'k_advance')} k_advance, {len(frames)} chunks, "
       f"persistent={persistent}, chunk sizes {[len(f) for f in frames[:6]]})")
 frames = [f for f in frames[1:] if len(f) > TALKER_KERNELS]
 if persistent:   # the frame loop's first chunk ends in the prefill; every later chunk is [cp frame, talker step]
     frames = [f for f in frames if len(f) >= 2]   # first chunk holds prefill/setup kernels
+    # folded advance: keep the frame-loop chunks [code-predictor frame, talker step] (the later chunks hold the vocoder
+    # and the time_stage replays)
+    frames = [f for f in frames if len(f) <= 4 and f[-2][2].startswith(("k_cp_roles", "k_persist<1"))]
 agg = {"cp": collections.defaultdict(list), "talker": collections.defaultdict(list)}
 spans = {"cp": [], "talker": [], "frame": []}
 for f in frames:
