@@ -52,6 +52,9 @@ constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of pos
 // workgroups' combine sweeps shared the CU with the partials' producers: 0.385 vs 0.376 ms at position 266, 0.392 vs
 // 0.382 at 500, 0.480 vs 0.476 at 1500.  Beside the QKV workgroups, which issue the next layer's rows right at the
 // QKV -> attention edge, a split's poll arrived 2.3 us late (round 4, before the gated polls).
+#ifndef Q3T_TK_HOIST   // attention: the new row's K / V share read once and selected per position pass (0: read under
+#define Q3T_TK_HOIST 1   // a branch in every pass)
+#endif
 #ifndef Q3T_TK_PUT_FIRST   // a role's publish: the other waves issue the next layer's weight prefetch only after wave 0's
 #define Q3T_TK_PUT_FIRST 0   // store instruction (their loads otherwise queue ahead of it in the CU's memory pipe)
 #endif
@@ -580,6 +583,12 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
         uint32_t qp[R][4];
 #pragma unroll
         for (int h = 0; h < R; ++h) pack_q8(q8[h], qp[h]);
+        // the new row's K / V share, read once: the position passes then select it without a branch, so the
+        // independent score chains interleave (a per-pass LDS read under a branch serialised them)
+        const uint4 knp = Q3T_TK_HOIST ? pack8f(&S.kn_s[li * 8]) : make_uint4(0, 0, 0, 0);
+        float vn8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vn8[e] = Q3T_TK_HOIST ? S.vn_s[li * 8 + e] : 0.0f;
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
             const int j = j0 + pi * 16 + pg;
@@ -587,7 +596,10 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
 #pragma unroll
             for (int h = 0; h < R; ++h) {
                 float sv;
-                if constexpr (Q3T_ATTN_DOT2) {
+                if constexpr (Q3T_ATTN_DOT2 && Q3T_TK_HOIST) {
+                    const uint4 kk = j == pos ? knp : kr[pi];
+                    sv = score8(kk, qp[h]);
+                } else if constexpr (Q3T_ATTN_DOT2) {
                     sv = score8(j == pos ? pack8f(&S.kn_s[li * 8]) : kr[pi], qp[h]);
                 } else {
                     float k8[8];
@@ -661,7 +673,14 @@ __device__ __forceinline__ void tk_att(Ctx<CPW> &X) {
                 const int j = j0 + pi * 16 + pg;
                 const bool ok = j <= pos;
                 float v8[8];
-                if (j == pos) {
+                if constexpr (Q3T_TK_HOIST) {
+                    const uint32_t ww[4] = {vr[pi].x, vr[pi].y, vr[pi].z, vr[pi].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v8[2 * e] = j == pos ? vn8[2 * e] : h2f(ww[e] & 0xffff);
+                        v8[2 * e + 1] = j == pos ? vn8[2 * e + 1] : h2f(ww[e] >> 16);
+                    }
+                } else if (j == pos) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v8[e] = S.vn_s[li * 8 + e];
                 } else {
