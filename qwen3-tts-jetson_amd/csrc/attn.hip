@@ -134,6 +134,12 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
     uint32_t qp[RMAX][4];
 #pragma unroll
     for (int h = 0; h < RMAX; ++h) pack_q8(q8[h], qp[h]);
+    // the new row's K / V share read once and selected per pass (persist_tk.hip: a per-pass LDS read under a branch
+    // serialised the independent score chains)
+    const uint4 knp = pack8f(&kn_s[li * 8]);
+    float vn8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vn8[e] = vn_s[li * 8 + e];
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
         const int j = j0 + pi * PPP + pg;
@@ -142,7 +148,8 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
         for (int h = 0; h < RMAX; ++h) {
             float s;
             if constexpr (Q3T_ATTN_DOT2) {   // score8 (q3t_common.h): identical in every single-slot attention kernel
-                s = score8(j == pos ? pack8f(&kn_s[li * 8]) : kr[pi], qp[h]);
+                const uint4 kk = j == pos ? knp : kr[pi];
+                s = score8(kk, qp[h]);
             } else {
                 float k8[8];
                 if (j == pos) {
@@ -201,12 +208,9 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
     for (int pi = 0; pi < NP; ++pi) {
         const int j = j0 + pi * PPP + pg;
         float v8[8];
-        if (j == pos) {
+        unpack8(vr[pi], v8);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v8[e] = vn_s[li * 8 + e];
-        } else {
-            unpack8(vr[pi], v8);
-        }
+        for (int e = 0; e < 8; ++e) v8[e] = j == pos ? vn8[e] : v8[e];
 #pragma unroll
         for (int h = 0; h < RMAX; ++h)
 #pragma unroll

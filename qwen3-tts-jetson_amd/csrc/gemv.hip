@@ -107,9 +107,18 @@ bool gemv(const GemvParams &p, hipStream_t s) {
     int ks = 4;
     for (int c : {1, 2, 4})
         if (blocks_for(c) >= gemv_min_blocks()) { ks = c; break; }
+#ifndef Q3T_GEMV_ROUNDS
+#define Q3T_GEMV_ROUNDS 1
+#endif
+    // rows wider than 1,024 (the 1.7B talker and its codec head; never a shape the persistent kernels restate): a grid
+    // of whole rounds of workgroups per CU (1.7B gate/up: 384 workgroups left half the CUs with two, 768 give all three)
+    if (Q3T_GEMV_ROUNDS && p.K > 1024 && ks < 4 && blocks_for(ks) % 256 != 0) ks *= 2;
     const int nsteps = (Kp / 128 + ks - 1) / ks;
-    int nl = nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 8 ? 8 : 0;
-    if (bt > 2 || Kp > 4096) nl = 0;
+    // NL: weight loads per lane issued up front (16 only for single-row launches; launch_nl streams the rest with NL 0).
+    // The loads' schedule only: the K order of every row is the same for any NL
+    int nl = nsteps <= 2 ? 2 : nsteps <= 4 ? 4 : nsteps <= 8 ? 8 : (nsteps <= 16 && bt == 1) ? 16 : 0;
+    if (nl == 0 && nsteps <= 24 && bt == 1 && p.pro == PRO_F16) nl = 24;
+    if (bt > 2 || Kp > (nl == 24 ? 6144 : 4096)) nl = 0;
     const dim3 grid((unsigned)((units + (16 / ks) - 1) / (16 / ks)), (unsigned)gy);
     const size_t lds = (size_t)bt * Kp * 2 + 16 * rpg * bt * 4 + 8 * sizeof(double) +
                        (p.pro == PRO_CPATT ? CPA_LDS : 0) + (p.sel.mode != SEL_NONE ? sizeof(SelLds) : 0) +

@@ -160,7 +160,8 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
     constexpr bool kF32 = PRO != PRO_F16 && !kAtt;
     constexpr int NT = PRO == PRO_RMS_G16 ? 16 : 1;
     constexpr int XB = BT <= 2 ? BT : 1;          // f32 activation rows held in registers at once
-    constexpr bool kXh = PRO == PRO_F16 && NL > 0;   // f16 activation rows prefetched into registers (K <= 4096)
+    constexpr bool kXh = PRO == PRO_F16 && NL > 0;   // f16 activation rows prefetched into registers (K <= 4096,
+    constexpr int XHN = NL >= 24 ? 3 : 2;             // NL 24: K <= 6144)
     const int K = p.K, N = p.N;
     const int Kp = (K + 127) & ~127;
     uint16_t *xs = reinterpret_cast<uint16_t *>(smem);
@@ -195,7 +196,7 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
     // ---------------- (1) activation rows of the first chunk, norm weights, epilogue operands
     float4 r[XB][4];
     float4 nwv[4], nbv[4];
-    uint4 xh[kXh ? BT : 1][2];
+    uint4 xh[kXh ? BT : 1][XHN];
     if constexpr (kF32 && !kGather) {
 #pragma unroll
         for (int q = 0; q < XB; ++q) issue_x_plain(p, b0 + min(q, nb - 1), r[q]);
@@ -211,7 +212,7 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
             const int src_row = b < nb ? (p.x_idx ? p.x_idx[b0 + b] : b0 + b) : 0;
             const uint16_t *src = reinterpret_cast<const uint16_t *>(p.x) + (size_t)src_row * p.ldx;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < XHN; ++t) {
                 const int k = tid * 8 + t * 2048;
                 xh[b][t] = ldg(reinterpret_cast<const uint4 *>(src + ((b < nb && k < K) ? k : 0)));
             }
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(256) k_gemv(const GemvParams p) {
 #pragma unroll
             for (int b = 0; b < BT; ++b)
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
+                for (int t = 0; t < XHN; ++t) {
                     const int k = tid * 8 + t * 2048;
                     if (k < Kp)
                         *reinterpret_cast<uint4 *>(xs + (size_t)b * Kp + k) = (b < nb && k < K) ? xh[b][t] : make_uint4(0, 0, 0, 0);
@@ -543,6 +544,11 @@ void launch_nl(const GemvParams &p, int nl, dim3 grid, size_t lds, hipStream_t s
         if (nl == 4) return launch_one<RPG, BT, KS, PRO, 4>(p, grid, lds, s);
         if (nl == 8) return launch_one<RPG, BT, KS, PRO, 8>(p, grid, lds, s);
     }
+    // single-row K <= 2048 per lane slice (the 1.7B talker's 2,048-wide QKV / gate-up / O rows): every weight load up front
+    if constexpr (BT == 1 && (PRO == PRO_RMS || PRO == PRO_F16 || PRO == PRO_F32))
+        if (nl == 16) return launch_one<RPG, BT, KS, PRO, 16>(p, grid, lds, s);
+    if constexpr (BT == 1 && PRO == PRO_F16)   // (the 1.7B down projection: K 6,144 in two slices of 3,072)
+        if (nl == 24) return launch_one<RPG, BT, KS, PRO, 24>(p, grid, lds, s);
     launch_one<RPG, BT, KS, PRO, 0>(p, grid, lds, s);
 }
 template <int RPG, int BT, int KS>
