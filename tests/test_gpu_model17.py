@@ -103,7 +103,7 @@ def test_full17_shapes_generate_and_vocoder():
         c = eng.cfg
         assert (c["hidden"], c["intermediate"], c["cp_hidden"], c["cp_intermediate"], c["has_mtp"]) == (2048, 6144, 1024, 3072, 1)
         # the talker step at the real widths (K 2,048 / 6,144 GEMVs: NL 16 / 24 weight loads in flight, whole-round
-        # grids) against the oracle, position by position (tolerances of test_gpu_parity.py's full model)
+        # grids) against the oracle, position by position (2e-3: ~2.5x the observed 7.8e-4)
         H = c["hidden"]
         rng = np.random.default_rng(5)
         kv = orc.kv_new(64, 0)
@@ -113,7 +113,7 @@ def test_full17_shapes_generate_and_vocoder():
             hg, lg = eng.talker_forward(e[None], [pos])
             ho, lo = orc.talker_step(kv, e, pos)
             worst = max(worst, rel_err(hg[0], ho), rel_err(lg[0], lo))
-            assert rel_err(hg[0], ho) < 5e-3 and rel_err(lg[0], lo) < 5e-3, (pos, rel_err(hg[0], ho), rel_err(lg[0], lo))
+            assert rel_err(hg[0], ho) < 2e-3 and rel_err(lg[0], lo) < 2e-3, (pos, rel_err(hg[0], ho), rel_err(lg[0], lo))
         orc.kv_free(kv)
         print(f"full17 talker step vs oracle: worst rel err {worst:.3g}")
         toks = prompt("full17")
