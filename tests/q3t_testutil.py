@@ -77,8 +77,9 @@ def check_token(lg, tok, temperature, top_k, u, keep_id=-1, tol_logit=5e-2, tol_
 
 
 def check_decisions(orc, toks, spk, codes, *, max_len, force_frames=0, temperature=0.0, top_k=50, seed=0, utt=0,
-                    rep=1.05, tol_logit=5e-2, tol_cdf=5e-2, max_off_frac=0.03, eos_id=2150, from_frame=0):
-    """Teacher-forced parity of a GPU-generated code sequence against the oracle.
+                    rep=1.05, tol_logit=2.5e-2, tol_cdf=2.5e-2, max_off_frac=0.03, eos_id=2150, from_frame=0):
+    """Teacher-forced parity of a GPU-generated code sequence against the oracle (per-decision tolerance 2.5e-2: ~2x
+    the worst observed in the GPU suite, 0.011 on the 16-slot batched family; it was 5e-2 through round 4).
 
     The oracle replays the GPU's codes (q3o_generate_forced) and records every decision's logits.  Greedy: each
     GPU token must be the oracle argmax or within tol_logit of it (near-tie); sampling: u*total must fall in the

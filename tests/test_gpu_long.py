@@ -67,7 +67,7 @@ def test_b1_generate_at_bench_lengths(full, nf, temperature):
         t0 = time.time()
         # sampling: a decision counts as "off" when u * total lands outside the GPU token's CDF interval by ANY amount;
         # with ~1e-2 logit noise (test_gpu_parity.py header) that happens on ~2 % of the decisions, each by <= 3e-3 of
-        # the mass (320 frames: 85 / 5120), so a 32-frame sample needs a 5 % bound; the 5e-2 per-decision bound holds
+        # the mass (320 frames: 85 / 5120), so a 32-frame sample needs a 5 % bound; the 2.5e-2 per-decision bound holds
         n_off, n_dec, worst = check_decisions(orc, toks, spk, out, max_len=nf, force_frames=nf,
                                               temperature=temperature, top_k=50, seed=77, utt=0,
                                               max_off_frac=0.03 if temperature <= 0 else 0.035)

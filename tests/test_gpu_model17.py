@@ -121,7 +121,7 @@ def test_full17_shapes_generate_and_vocoder():
         out = eng.generate([toks], speakers=[spk], max_len=12, temperature=0.0, force_frames=12)[0]
         assert out.shape == (12, 16)
         n_off, n_dec, worst = check_decisions(orc, toks, spk, out, max_len=12, force_frames=12, temperature=0.0,
-                                              tol_logit=8e-2, max_off_frac=0.05)
+                                              max_off_frac=0.05)
         print(f"full17 B=1 12 frames: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
         pcm = eng.vocoder(out)
         ref = orc.vocoder(out)
