@@ -40,6 +40,9 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_WPUB   // QKV phase: each wave publishes its own 16 rows (one line; 0: through LDS, wave 0 publishes all 64)
+#define Q3T_CP_WPUB 1
+#endif
 #ifndef Q3T_CP_PUT_FIRST   // a role's publish: the other waves issue the next weight prefetch only after wave 0's store
 #define Q3T_CP_PUT_FIRST 1   // (their loads, 128 KB per QKV workgroup, otherwise queue ahead of it in the CU's memory pipe)
 #endif
@@ -118,7 +121,9 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
         const uint16_t *W = S.layers[l].qkv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint16_t *r = W + (size_t)(64 * i + 16 * j + grp) * H + l16 * 8;
+            // Q3T_CP_WPUB: wave w owns rows 16w .. 16w + 15 (row 16w + 4j + lane / 16) and publishes them itself
+            const int row = Q3T_CP_WPUB ? 16 * (t >> 6) + 4 * j + (grp & 3) : 16 * j + grp;
+            const uint16_t *r = W + (size_t)(64 * i + row) * H + l16 * 8;
 #pragma unroll
             for (int tt = 0; tt < 8; ++tt) wq[j][tt] = ld16(r + tt * 128);
         }
@@ -157,15 +162,28 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
 #pragma unroll
                 for (int tt = 0; tt < 8; ++tt) acc[j] = dot8(wq[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), acc[j]);
             }
+            if constexpr (Q3T_CP_WPUB) {
+                // each wave publishes its 16 rows as one whole line: lane L < 16 takes row 4j + g (j = L / 4, g = L % 4)
+                // from lane 16 g of the group that reduced it (the l16 == 0 lane, as the LDS form), no barrier
+                float pv = 0.0f;
+                const int lane = t & 63;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[j] = group_sum<16>(acc[j]);
-                if (l16 == 0) S.outv[16 * j + grp] = acc[j];
+                for (int j = 0; j < 4; ++j) {
+                    const float v = __shfl(group_sum<16>(acc[j]), 16 * (lane & 3));
+                    if ((lane >> 2) == j) pv = v;
+                }
+                if (lane < 16) g_put(p.gqkv + 64 * i + 16 * (t >> 6) + lane, __float_as_uint(pv), X.tag(ph));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[j] = group_sum<16>(acc[j]);
+                    if (l16 == 0) S.outv[16 * j + grp] = acc[j];
+                }
+                __syncthreads();
+                // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four
+                // waves into shared lines make the next edge slower
+                if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
             }
-            __syncthreads();
-            // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four
-            // waves into shared lines make the next edge slower
-            if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
             PROF(ph, 2);
             if (Q3T_CP_PUT_FIRST) __syncthreads();   // the publish store enters the CU's memory pipe before the prefetch
             if (l + 1 < NLC) issue_qkv(l + 1);

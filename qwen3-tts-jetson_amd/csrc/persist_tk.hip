@@ -52,6 +52,9 @@ constexpr int R = NH / NKV, CHK = 64, PSLOT = 264, MAXCH = 32;   // chunk of pos
 // workgroups' combine sweeps shared the CU with the partials' producers: 0.385 vs 0.376 ms at position 266, 0.392 vs
 // 0.382 at 500, 0.480 vs 0.476 at 1500.  Beside the QKV workgroups, which issue the next layer's rows right at the
 // QKV -> attention edge, a split's poll arrived 2.3 us late (round 4, before the gated polls).
+#ifndef Q3T_TK_WPUB   // QKV phase: each wave publishes its own 16 rows (one line; 0: through LDS, wave 0 publishes all 64)
+#define Q3T_TK_WPUB 1
+#endif
 #ifndef Q3T_TK_HOIST   // attention: the new row's K / V share read once and selected per position pass (0: read under
 #define Q3T_TK_HOIST 1   // a branch in every pass)
 #endif
@@ -159,7 +162,9 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
         const uint16_t *W = S.layers[l].qkv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint16_t *r = W + (size_t)(64 * i + 16 * j + grp) * H + l16 * 8;
+            // Q3T_TK_WPUB: wave w owns rows 16w .. 16w + 15 (row 16w + 4j + lane / 16) and publishes them itself
+            const int row = Q3T_TK_WPUB ? 16 * (t >> 6) + 4 * j + (grp & 3) : 16 * j + grp;
+            const uint16_t *r = W + (size_t)(64 * i + row) * H + l16 * 8;
 #pragma unroll
             for (int tt = 0; tt < 8; ++tt) wq[j][tt] = ld16(r + tt * 128);
         }
@@ -188,15 +193,27 @@ __device__ __forceinline__ void tk_qkv(Ctx<CPW> &X) {
 #pragma unroll
             for (int tt = 0; tt < 8; ++tt) acc[j] = dot8(wq[j][tt], *reinterpret_cast<const uint4 *>(S.xs + l16 * 8 + tt * 128), acc[j]);
         }
+        if constexpr (Q3T_TK_WPUB) {
+            // each wave publishes its 16 rows as one whole line (persist_cp.hip role_qkv): no barrier
+            float pv = 0.0f;
+            const int lane = t & 63;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            acc[j] = group_sum<16>(acc[j]);
-            if (l16 == 0) S.outv[16 * j + grp] = acc[j];
+            for (int j = 0; j < 4; ++j) {
+                const float v = __shfl(group_sum<16>(acc[j]), 16 * (lane & 3));
+                if ((lane >> 2) == j) pv = v;
+            }
+            if (lane < 16) g_put(p.gqkv + 64 * i + 16 * (t >> 6) + lane, __float_as_uint(pv), X.tag(ph));
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[j] = group_sum<16>(acc[j]);
+                if (l16 == 0) S.outv[16 * j + grp] = acc[j];
+            }
+            __syncthreads();
+            // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four waves
+            // into shared lines make the next edge slower
+            if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
         }
-        __syncthreads();
-        // one store instruction of wave 0 publishes the 64 rows (4 whole lines): single-lane stores from four waves
-        // into shared lines make the next edge slower
-        if (t < 64) g_put(p.gqkv + 64 * i + t, __float_as_uint(S.outv[t]), X.tag(ph));
         PROF(ph, 2);
         if (Q3T_TK_PUT_FIRST) __syncthreads();
         if (l + 1 < nl) {
