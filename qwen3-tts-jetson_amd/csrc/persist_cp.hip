@@ -40,6 +40,9 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_GATE   // polls: lane 0 of each wave gates on the wave's first granule before the sweep (talker form)
+#define Q3T_CP_GATE 1
+#endif
 #ifndef Q3T_CP_WPUB   // QKV phase: each wave publishes its own 16 rows (one line; 0: through LDS, wave 0 publishes all 64)
 #define Q3T_CP_WPUB 1
 #endif
@@ -149,6 +152,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
             } else {
                 uint32_t u[4];
                 PROF(ph, 0);
+                if (Q3T_CP_GATE) g_gate(p.gx + 4 * t, X.tag(ph_of(pass, l - 1, 4)), X.c);
                 Q3T_CP_WAIT<4>(p.gx + 4 * t, X.tag(ph_of(pass, l - 1, 4)), u, X.c);
                 PROF(ph, 1);
                 x = f4_of(u);
@@ -195,6 +199,7 @@ __device__ __forceinline__ void role_qkv(Ctx &X) {
         const int hph = ph_of(pass, NLC, 0);
         uint32_t u[4];
         PROF(hph, 0);
+        if (Q3T_CP_GATE) g_gate(p.gx + 4 * t, X.tag(ph_of(pass, NLC - 1, 4)), X.c);
         Q3T_CP_WAIT<4>(p.gx + 4 * t, X.tag(ph_of(pass, NLC - 1, 4)), u, X.c);
         PROF(hph, 1);
         rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
@@ -479,6 +484,7 @@ __device__ __forceinline__ void role_o(Ctx &X) {
             }
             uint32_t u[4];
             PROF(ph, 0);
+            if (Q3T_CP_GATE) g_gate(p.gattn + 4 * t, X.tag(ph_of(pass, l, 1)), X.c);
             Q3T_CP_WAIT<4>(p.gattn + 4 * t, X.tag(ph_of(pass, l, 1)), u, X.c);
             PROF(ph, 1);
             *reinterpret_cast<uint4 *>(S.xs + 8 * t) = make_uint4(u[0], u[1], u[2], u[3]);
@@ -537,6 +543,7 @@ __device__ __forceinline__ void role_gu(Ctx &X) {
             const int ph = ph_of(pass, l, 3);
             uint32_t u[4];
             PROF(ph, 0);
+            if (Q3T_CP_GATE) g_gate(p.gx2 + 4 * t, X.tag(ph_of(pass, l, 2)), X.c);
             Q3T_CP_WAIT<4>(p.gx2 + 4 * t, X.tag(ph_of(pass, l, 2)), u, X.c);
             PROF(ph, 1);
             rms_to_f16(f4_of(u), nw, p.eps, S.xs, S.dscr, nullptr);
@@ -604,6 +611,7 @@ __device__ __forceinline__ void role_dn(Ctx &X) {
             }
             uint32_t u[6];
             PROF(ph, 0);
+            if (Q3T_CP_GATE) g_gate(p.gh + 6 * t, X.tag(ph_of(pass, l, 3)), X.c);
             Q3T_CP_WAIT<6>(p.gh + 6 * t, X.tag(ph_of(pass, l, 3)), u, X.c);
             PROF(ph, 1);
             *reinterpret_cast<uint2 *>(S.xs + 12 * t) = make_uint2(u[0], u[1]);
