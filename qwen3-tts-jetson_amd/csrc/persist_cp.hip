@@ -40,6 +40,9 @@ namespace q3t { __device__ uint64_t *g_selprof = nullptr; }
 
 #pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemv / k_attn / k_persist
 
+#ifndef Q3T_CP_SGATE   // the selection's logits poll behind the same one-lane gate
+#define Q3T_CP_SGATE 1
+#endif
 #ifndef Q3T_CP_GATE   // polls: lane 0 of each wave gates on the wave's first granule before the sweep (talker form)
 #define Q3T_CP_GATE 1
 #endif
@@ -390,6 +393,7 @@ __device__ __forceinline__ void role_att(Ctx &X) {
         const float u = uniform24(spre.seed, spre.utt, (uint64_t)spre.frame, (uint64_t)pass);   // select_token_pre's u
         uint32_t u8[8], mm[2];
         PROF(hph, 0);
+        if (Q3T_CP_SGATE) g_gate(p.glog + 8 * t, X.tag(hph), X.c);
         if constexpr (Q3T_POLL16) {
             if (samp && RNG) g_wait16_pair<8, 2>(p.glog + 8 * t, p.glog + CPV + MMS * lane, X.tag(hph), u8, mm, X.c);
             else g_waitc<8>(p.glog + 8 * t, X.tag(hph), u8, X.c);
