@@ -9,6 +9,7 @@
 // same launch (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores -> vmcnt(0) -> barrier -> one agent atomic
 // add; the last adder loads the partials with sc1 loads) -- no combine launch, no release/acquire cache flushes.
 #include "kernels.h"
+#include "attn_small.h"
 
 #include <type_traits>
 
@@ -496,111 +497,19 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
 
 
 // ------------------------------------------------------------------------------------------ batched code predictor:
-// <= 16 positions (export_code_predictor.py:132-231 step semantics), one wave per (slot, kv head).  The cached K/V rows
-// do not depend on this launch's QKV rows, so they are loaded first; then the head norms + RoPE (k_attn arithmetic),
-// the KV append, scores with one lane pair per (head, position) over 64 dims each, the softmax per head and P.V with
-// four output dims per lane.  No workgroup barrier beyond the wave's own LDS round trips.
+// <= 16 positions, one wave per (slot, kv head) (attn_small.h, shared with the persistent batched frame)
 template <int D, int R>
 __global__ void __launch_bounds__(64) k_attn_small(const AttnParams p) {
     static_assert(D == 128 && R == 2, "code-predictor heads: D 128, 2 q heads per kv head");
-    constexpr int NPOS = 16;
-    const int slot = blockIdx.x, g = blockIdx.y, lane = threadIdx.x;
+    const int slot = blockIdx.x, g = blockIdx.y;
+    __shared__ AttnSmallLds L;
     const int pos = p.pos[slot];
     const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
-    __shared__ float q_s[R][D];
-    __shared__ __attribute__((aligned(16))) uint16_t kh_s[D], vh_s[D];
-    __shared__ float pr_s[R][NPOS];
-    __shared__ float l_s[R];
-    // score lanes: head sh, position sj, K half sk (64 dims); P.V lanes: head vh, dims vd .. vd+3
-    const int sh = lane >> 5, sj = (lane >> 1) & 15, sk = lane & 1;
-    const int vh = lane >> 5, vd = (lane & 31) * 4;
-    const int jk = min(sj, max(pos - 1, 0));
-    uint4 kr[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) kr[e] = ldg16(p.kc + head_off + (size_t)jk * D + sk * 64 + e * 8);
-    uint2 vr[NPOS];
-#pragma unroll
-    for (int j = 0; j < NPOS; ++j) {
-        const int jv = min(j, max(pos - 1, 0));
-        vr[j] = *reinterpret_cast<const uint2 *>(p.vc + head_off + (size_t)jv * D + vd);
-    }
-    // head RMSNorm + NEOX RoPE of the 2 q heads and the new k, the new v f16-rounded (k_attn arithmetic)
     const int QKV = (p.nH + 2 * p.nKV) * D;
     const float *qkv = p.qkv_tab ? p.qkv_tab + (p.tab_row0 + (size_t)p.tab_tok[(size_t)slot * p.tab_ld + p.tab_col]) * QKV
                                  : p.qkv + (size_t)slot * QKV;
-    const float *rope = p.rope + (size_t)pos * D;
-    float xs[4][2];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const float *src = v < R ? qkv + (size_t)(g * R + v) * D : v == R ? qkv + (size_t)(p.nH + g) * D
-                                                                            : qkv + (size_t)(p.nH + p.nKV + g) * D;
-        xs[v][0] = src[lane];
-        xs[v][1] = src[lane + 64];
-    }
-    const float c = rope[2 * lane], sn = rope[2 * lane + 1];
-#pragma unroll
-    for (int v = 0; v < R + 1; ++v) {
-        const float *w = v == R ? p.kn : p.qn;
-        double ss = (double)__fmul_rn(xs[v][0], xs[v][0]) + (double)__fmul_rn(xs[v][1], xs[v][1]);
-        ss = wave_sum_d(ss);
-        const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
-        const float x0 = (xs[v][0] * scale) * w[lane], x1 = (xs[v][1] * scale) * w[lane + 64];
-        const float y0 = opaque(opaque(x0 * c) - opaque(x1 * sn));
-        const float y1 = opaque(opaque(x0 * sn) + opaque(x1 * c));
-        if (v == R) {
-            kh_s[lane] = f2h(y0);
-            kh_s[lane + 64] = f2h(y1);
-        } else {
-            q_s[v][lane] = f16r(y0);
-            q_s[v][lane + 64] = f16r(y1);
-        }
-    }
-    vh_s[lane] = f2h(xs[R + 1][0]);
-    vh_s[lane + 64] = f2h(xs[R + 1][1]);
-    p.kc[head_off + (size_t)pos * D + lane] = kh_s[lane];
-    p.kc[head_off + (size_t)pos * D + lane + 64] = kh_s[lane + 64];
-    p.vc[head_off + (size_t)pos * D + lane] = vh_s[lane];
-    p.vc[head_off + (size_t)pos * D + lane + 64] = vh_s[lane + 64];
-    __syncthreads();
-    // scores: the new row from LDS, cached rows from registers
-    if (sj == pos) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) kr[e] = *reinterpret_cast<const uint4 *>(&kh_s[sk * 64 + e * 8]);
-    }
-    float s = 0.0f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        float k8[8];
-        unpack8_cvt(kr[e], k8);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s = __fmaf_rn(k8[u], q_s[sh][sk * 64 + e * 8 + u], s);
-    }
-    s += __shfl_xor(s, 1);
-    const float kq_scale = 1.0f / sqrtf((float)D);
-    const float sc = sj <= pos ? __fmul_rn(s, kq_scale) : -INFINITY;
-    const float mx = group_max<32>(sc);
-    const float pv = sj <= pos ? expf(__fsub_rn(sc, mx)) : 0.0f;
-    const float lsum = group_sum<32>(sk == 0 ? pv : 0.0f);
-    if (sk == 0) pr_s[sh][sj] = pv;
-    if ((lane & 31) == 0) l_s[sh] = lsum;
-    __syncthreads();
-    // P.V: the new row from LDS
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < NPOS; ++j) {
-        if (j > pos) break;
-        const uint2 u = j == pos ? *reinterpret_cast<const uint2 *>(&vh_s[vd]) : vr[j];
-        const float pj = pr_s[vh][j];
-        acc[0] = __fmaf_rn(pj, h2f(u.x & 0xffff), acc[0]);
-        acc[1] = __fmaf_rn(pj, h2f(u.x >> 16), acc[1]);
-        acc[2] = __fmaf_rn(pj, h2f(u.y & 0xffff), acc[2]);
-        acc[3] = __fmaf_rn(pj, h2f(u.y >> 16), acc[3]);
-    }
-    const float l = l_s[vh];
-    uint2 o;
-    o.x = (uint32_t)f2h(acc[0] / l) | ((uint32_t)f2h(acc[1] / l) << 16);
-    o.y = (uint32_t)f2h(acc[2] / l) | ((uint32_t)f2h(acc[3] / l) << 16);
-    *reinterpret_cast<uint2 *>(p.out + (size_t)slot * p.nH * D + (size_t)(g * R + vh) * D + vd) = o;
+    attn_small_wave<false>(g, pos, p.nH, p.nKV, qkv, p.qn, p.kn, p.eps, p.rope + (size_t)pos * D, p.kc + head_off,
+                           p.vc + head_off, p.out + (size_t)slot * p.nH * D, L);
 }
 
 // ------------------------------------------------------------------ causal prefill attention

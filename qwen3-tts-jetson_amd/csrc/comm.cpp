@@ -87,9 +87,16 @@ bool comm_bcast_arenas(Comm *c, const std::vector<WeightArena *> &arenas, hipStr
             return false;
         }
     // 2) one broadcast per blob (>= hundreds of MB each: ring bandwidth over xGMI, not latency)
+    // the group is closed on every path: an enqueue error must not leave the communicator inside ncclGroupStart
     Q3T_NCCL(ncclGroupStart());
-    for (WeightArena *a : arenas) Q3T_NCCL(ncclBroadcast(a->base, a->base, a->used, ncclUint8, 0, c->nc, s));
-    Q3T_NCCL(ncclGroupEnd());
+    ncclResult_t first = ncclSuccess;
+    for (WeightArena *a : arenas) {
+        const ncclResult_t r = ncclBroadcast(a->base, a->base, a->used, ncclUint8, 0, c->nc, s);
+        if (r != ncclSuccess) { first = r; break; }
+    }
+    const ncclResult_t end = ncclGroupEnd();
+    if (first != ncclSuccess) { set_error(std::string("ncclBroadcast: ") + ncclGetErrorString(first)); return false; }
+    if (end != ncclSuccess) { set_error(std::string("ncclGroupEnd: ") + ncclGetErrorString(end)); return false; }
     Q3T_HIP(hipStreamSynchronize(s));
     return true;
 }

@@ -94,6 +94,7 @@ Options Options::from_env() {
     o.mm_cp_table = env_flag("Q3T_MM_CP_TABLE", true);
     o.fold_advance = env_flag("Q3T_FOLD_ADVANCE", true);
     o.tk_roles = env_flag("Q3T_TK_ROLES", true);
+    o.cpb = env_flag("Q3T_PERSIST_CPB", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
     o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
@@ -254,6 +255,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     }
 #endif
     if (!setup_persist()) return false;
+    if (!setup_cpb()) return false;
     if (!tok_gguf.empty()) {
         voc_.reset(new Vocoder());
         if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
@@ -522,6 +524,43 @@ bool Engine::setup_persist() {
     return true;
 }
 
+// the batched code-predictor frame (persist_cpb.hip): the 0.6B code-predictor shapes on the matrix-core family, with
+// layer 0 of passes 1..15 from the per-token QKV table (as decoder_stack_mm reads it), on a device that holds its 256
+// workgroups at one per CU
+bool Engine::setup_cpb() {
+    int n_cu = 0;
+    Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
+    cpb_ = opt_.cpb && mm_ok_ && max_slots_ > 1 && opt_.mm_cp_table && opt_.cp_qkv_table && !c_.has_mtp &&
+           c_.cp_vocab == 2048 && c_.codec_vocab == 3072 && CP_.size() == 5 && cp_head_.size() == 15 && cp_embd_.size() >= 14 &&
+           c_.cp_hidden == 1024 && c_.hidden == 1024 && c_.cp_inter == 3072 && c_.cp_heads == 16 && c_.cp_kv == 8 &&
+           c_.head_dim == 128 && n_cu >= 256 && cpb_resident(device_);
+    if (!cpb_) return true;
+    cpb_state_ = dalloc<uint8_t>(cpb_state_bytes());
+    if (!cpb_state_) { set_error("device allocation failed"); return false; }
+    if (!pl_cp_dev_) {
+        std::vector<PLayerW> cpl(CP_.size());
+        for (size_t i = 0; i < CP_.size(); ++i)
+            cpl[i] = PLayerW{CP_[i].qkv, CP_[i].o, CP_[i].gu, CP_[i].down, CP_[i].attn_norm, CP_[i].ffn_norm, CP_[i].qn, CP_[i].kn};
+        pl_cp_dev_ = dalloc<PLayerW>(cpl.size());
+        if (!pl_cp_dev_) { set_error("device allocation failed"); return false; }
+        Q3T_HIP(hipMemcpyAsync(pl_cp_dev_, cpl.data(), cpl.size() * sizeof(PLayerW), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+    }
+    if (!heads_dev_) {
+        heads_dev_ = dalloc<const uint16_t *>(16);
+        if (!heads_dev_) { set_error("device allocation failed"); return false; }
+        std::vector<const uint16_t *> hp(cp_head_.begin(), cp_head_.end());
+        Q3T_HIP(hipMemcpyAsync(heads_dev_, hp.data(), hp.size() * sizeof(void *), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+    }
+    return true;
+}
+// the slot counts the frame serves: the matrix-core family (decoder_stack_mm) with the split-K of <= 64 slots
+bool Engine::use_cpb(int S) const {
+    const int S_main = policy_slots_ > 0 ? policy_slots_ : S;
+    return cpb_ && cp_qkvtab_ && use_mm(S) && S <= 64 && S_main <= 64;
+}
+
 // The code predictor's per-token tables (the layer-0 QKV rows, 520 MB of f32; 1.7B: the projected pass inputs, 130 MB)
 // are functions of the weights alone.  One copy per device serves every context that loaded the same weight file
 // (path, size and modification time: replicas and test contexts of one model), built by the first of them on its own
@@ -692,13 +731,14 @@ bool Engine::persist_recover() {
     Q3T_HIP(hipStreamSynchronize(stream_));
     fprintf(stderr, "[q3t] persistent kernel flagged an in-launch hand-off fault on device %d: "
                     "falling back to the launch-per-op graphs for this context\n", device_);
-    Q3T_HIP(hipMemsetAsync(pstate_, 0, persist_state_bytes(), stream_));   // ordered before the re-run on stream_
+    if (pstate_) Q3T_HIP(hipMemsetAsync(pstate_, 0, persist_state_bytes(), stream_));   // ordered before the re-run on stream_
+    if (cpb_state_ && !cpb_clear(cpb_state_, stream_)) return false;
     Q3T_HIP(hipStreamSynchronize(stream_));
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
-    persist_ = persist_cp_ = cp_roles_ = tk_roles_ = false;
+    persist_ = persist_cp_ = cp_roles_ = tk_roles_ = cpb_ = false;
     // the tables (serving only the persistent frame) stay allocated until the context is destroyed: a hipFree here
     // would synchronise the device and invalidate graph captures other contexts' threads have in progress
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
@@ -754,7 +794,11 @@ bool Engine::persist_fault_hook(int S, int n_launches) {
 }
 
 bool Engine::persist_error() {
-    if (!persist_enabled() || !pstate_) return false;
+    if (cpb_ && cpb_state_) {
+        bool e = false;
+        if (!cpb_error(cpb_state_, stream_, &e) || e) return true;
+    }
+    if (!(persist_ || persist_cp_) || !pstate_) return false;
     PersistParams p;
     persist_carve(pstate_, p);
     // on the context's own (non-blocking) stream: a null-stream copy would order against, and break, graph captures
@@ -1085,6 +1129,19 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
         p.prof = pprof_;
         if (cp_roles_ && p.qkvtab) return persist_cp_roles(p, s);   // (1.7B: layer 0's residual rows from xtab)
         return persist_cp_frame(p, s);
+    }
+    if (use_cpb(S) && !logits_host) {   // batched: the whole frame as one persistent launch (persist_cpb.hip)
+        CpbParams p;
+        p.L = pl_cp_dev_; p.heads = heads_dev_; p.tabs = tabs16_dev_; p.out_norm = cp_out_norm_; p.qkvtab = cp_qkvtab_;
+        p.x_in = hidden_; p.rope = rope_; p.pos = cp_pos_; p.pos_ld = max_slots_; p.kc = cpkc_; p.vc = cpvc_;
+        p.kv_layer = kv_layer; p.logits = cp_logits_; p.sel = select_spec(SEL_CP, gp_, 0, 0); p.S = S; p.eps = c_.eps;
+        if (talker_next) {
+            p.talker_next = 1;
+            p.tx = x_; p.txn = xn_; p.tnw = L_[0].attn_norm;
+            p.tr = trailing_; p.tr_len = trailing_len_; p.frame = frame_; p.tr_ld = max_trailing_ * H; p.pad = tts_pad_;
+        }
+        p.state = cpb_state_;
+        return persist_cp_batched(p, s);
     }
     const bool fsel_all = fused_select_ && !use_mm(S);
     // deferred selection gathers the next pass's table row inside its QKV launch: not with a projected input (1.7B)
@@ -1439,7 +1496,7 @@ bool Engine::generate(int n_utt, const int32_t *const *tokens, const int *n_toke
     if (n_utt <= 0) return true;
     if (n_utt > max_slots_) { set_error("n_utt exceeds max_slots"); return false; }
     // only single-slot runs launch the persistent kernels: batched contexts on one device run concurrently
-    DeviceLock lk(persist_enabled() && n_utt == 1, device_);
+    DeviceLock lk(persist_exclusive(n_utt), device_);
     StreamState st;
     st.delivered.assign(n_utt, 0);
     st.stop_at.assign(n_utt, -1);
@@ -1951,7 +2008,7 @@ bool Engine::generate_queue_once(int n_utt, const int32_t *const *tokens, const 
 bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *n_tokens, const float *const *speaker,
                             const GenParams &gp, int32_t *codes, int *n_frames, int max_active) {
     const int S = std::min(max_slots_, std::max(n_utt, 1));
-    DeviceLock lk(persist_enabled() && S == 1, device_);
+    DeviceLock lk(persist_exclusive(S), device_);
     bool fault = false;
     if (generate_queue_once(n_utt, tokens, n_tokens, speaker, gp, codes, n_frames, max_active, &fault)) return true;
     if (!fault) return false;
@@ -1963,7 +2020,7 @@ bool Engine::generate_queue(int n_utt, const int32_t *const *tokens, const int *
 
 bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (S <= 0 || S > max_slots_ || pos < 0 || pos >= max_ctx_ || iters <= 0) { set_error("time_stage: bad arguments"); return false; }
-    DeviceLock lk(persist_enabled() && S == 1, device_);
+    DeviceLock lk(persist_exclusive(S), device_);
     std::vector<int> pv(S, pos), fr(S, 0), dn(S, -1);
     Q3T_HIP(hipMemcpyAsync(pos_, pv.data(), S * 4, hipMemcpyHostToDevice, stream_));
     Q3T_HIP(hipMemcpyAsync(frame_, fr.data(), S * 4, hipMemcpyHostToDevice, stream_));
@@ -2015,7 +2072,7 @@ bool Engine::talker_forward(int S, const float *embd, const int *pos, float *hid
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     for (int s = 0; s < S; ++s) if (pos[s] < 0 || pos[s] >= max_ctx_) { set_error("Context length exceeded"); return false; }
     const int H = c_.hidden;
-    DeviceLock lk(persist_enabled() && S == 1, device_);
+    DeviceLock lk(persist_exclusive(S), device_);
     for (int attempt = 0; attempt < 2; ++attempt) {
         Q3T_HIP(hipMemcpyAsync(x_, embd, (size_t)S * H * 4, hipMemcpyHostToDevice, stream_));
         Q3T_HIP(hipMemcpyAsync(pos_, pos, S * 4, hipMemcpyHostToDevice, stream_));
@@ -2036,7 +2093,7 @@ bool Engine::codepred_frame(int S, const float *hidden, const int *cb0, float te
     if (S <= 0 || S > max_slots_) { set_error("bad slot count"); return false; }
     const int H = c_.hidden;
     for (int s = 0; s < S; ++s) if (cb0[s] < 0 || cb0[s] >= c_.codec_vocab) { set_error("cb0 out of range"); return false; }
-    DeviceLock lk(persist_enabled() && S == 1, device_);
+    DeviceLock lk(persist_exclusive(S), device_);
     GenParams gp = gp_;
     gp.temperature = temperature; gp.top_k = top_k; gp.seed = seed;
     gp_ = gp;

@@ -95,4 +95,40 @@ bool persist_tk_roles_resident(int device, int n_ctx);
 int persist_chunk(int n_ctx);                    // positions per attention split workgroup
 size_t persist_qkv_table_rows();                 // rows of PersistParams::qkvtab (3072 + 14 * 2048)
 
+// ------------------------------------------------------------------ the batched code-predictor frame (persist_cpb.hip)
+// 1..64 slots, 0.6B code-predictor shapes, the launch-per-op matrix-core family of up to 64 slots (split-K 4): the whole
+// 16-pass frame of every slot as one persistent launch, bit-identical to enqueue_cp_frame's decoder_stack_mm graph
+struct CpbParams {
+    const PLayerW *L = nullptr;                  // device array [5]
+    const uint16_t *const *heads = nullptr;      // device array of the 15 lm_heads
+    const uint16_t *const *tabs = nullptr;       // device array [16]: codec_embd, code_pred.codec_embd[0..14]
+    const float *out_norm = nullptr;             // code-predictor output norm
+    const float *qkvtab = nullptr;               // layer 0's raw QKV row per table token (Engine::build_cp_qkv_table)
+    const float *x_in = nullptr;                 // [S][1024] talker hidden state (pass 0 input)
+    const float *rope = nullptr;
+    const int *pos = nullptr;                    // [16][pos_ld] position of pass p per slot
+    int pos_ld = 0;
+    uint16_t *kc = nullptr, *vc = nullptr;       // [5][pos_ld][8][16][128] f16
+    size_t kv_layer = 0;
+    float *logits = nullptr;                     // [S][2048]
+    SelectSpec sel;                              // SEL_CP (step set per pass), sel.tokens = the frame codes [S][16]
+    int S = 0;
+    float eps = 1e-6f;
+    // talker_next: after the last pass, the next talker step's embedding (16 table rows + trailing / pad row) into tx and
+    // its layer-0 RMSNorm (tnw) into txn (k_select_embed_norm nt = 16)
+    int talker_next = 0;
+    float *tx = nullptr;
+    uint16_t *txn = nullptr;
+    const float *tnw = nullptr;
+    const float *tr = nullptr, *pad = nullptr;
+    const int *tr_len = nullptr, *frame = nullptr;
+    int tr_ld = 0;
+    uint8_t *state = nullptr;                    // cpb_state_bytes(), zeroed once
+};
+size_t cpb_state_bytes();
+bool cpb_resident(int device);                   // both instantiations fit one workgroup per CU, >= 256 CUs
+bool persist_cp_batched(const CpbParams &p, hipStream_t s);
+bool cpb_error(const uint8_t *state, hipStream_t s, bool *err);   // a hand-off wait gave up
+bool cpb_clear(uint8_t *state, hipStream_t s);   // zero the flags and the error word
+
 }  // namespace q3t

@@ -1,0 +1,533 @@
+// persist_cpb.hip — the BATCHED code-predictor frame (4..64 slots, BASELINE configs[2]) as ONE persistent launch:
+// 16 passes of the 5-layer stack, lm_head[p-1] + token selection after pass p >= 1, and the next talker step's
+// embedding (src/tts_transformer.cpp:2153-2340, src/trt_code_predictor.cpp:484-600,
+// scripts/export_code_predictor.py:132-231).  It replaces the ~570-launch graph of decoder_stack_mm (engine.cpp) for one
+// frame, and computes the same bits: every projection is that graph's MFMA tile with the same K quarters, the same
+// split-K slices and the same LDS sum order (gemm_mfma.hip), every residual + RMSNorm is k_resid_norm's arithmetic, the
+// attention is k_attn_small's source (attn_small.h) and the selection is k_select_embed_norm's (select.h).
+//
+// Work per layer for S slots in NT token tiles of 32 (NT = 1: S <= 32, NT = 2: S <= 64), one 256-thread workgroup per CU:
+//
+//   job              count            workgroups        tile / input (per job)                    output
+//   RN_A / RN_F      1 per slot       192 + b           x[b] += 4 slabs; RMSNorm -> f16 row        xnA / xnF [b]
+//   QKV              128 x NT         [0, 128 NT)       32 rows x 32 tokens, K 1024 (xnA 64 KB)    qkv f32
+//   ATT              1 per slot       192 + b           8 kv groups (2 per wave), <= 16 positions  attn f16 [b]
+//   O                32 x 4 x NT      [0, 128 NT)       32 rows x 32 tokens x K slice 512          slabO f32 [z]
+//   GU               192              [0, 192)          32 rows (16 SwiGLU units) x 32 NT tokens   h f16
+//   DN               32 x 4 x NT      [0, 128 NT)       32 rows x 32 tokens x K slice 768          slabD f32 [z]
+//   HEAD (p >= 1)    64 x NT          [0, 64 NT)        32 rows x 32 tokens, K 1024 (final xnA)    logits f32
+//   SEL  (p >= 1)    1 per slot       192 + b           top-k / argmax of the slot's row, commit; next pass's x[b]
+//
+// The residual stream of slot b never leaves its RN workgroup: x[b] lives in registers (4 values per thread) for the
+// whole frame.  Hand-offs are MI355X_MICROARCH.md's flag form for bandwidth (hand-off table, row 1): every payload byte
+// is stored with an agent-scope (sc1) store, each storing wave waits vmcnt(0), a workgroup barrier, then ONE lane
+// stores the job's flag (sc1); a consumer wave polls the flags of exactly the producers whose bytes it reads (sc1
+// loads) and then loads the payload with sc1 loads.  A flag carries ((seq << 10) + phase + 1): seq is bumped once per
+// launch, so a flag of an earlier phase or launch never matches.  Payload buffers are single-buffered: every producer
+// reaches its next write of a buffer only through a chain of jobs that needs every reader of the previous contents to
+// have finished.  Every wait is bounded (persist_dev.h SPIN_LIMIT): a protocol fault ends the launch with *err set and
+// the engine falls back to the launch-per-op graph, which is bit-identical.
+#include "persist.h"
+#include "persist_dev.h"
+#include "attn_small.h"
+#include "select.h"
+
+#pragma clang fp contract(off)   // every rounding as written: bit-identical to k_gemm_mfma / k_resid_norm / k_attn_small
+
+namespace q3t {
+
+namespace {
+using namespace pdev;
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, CPV = 2048, VOC = 3072;
+constexpr int NLC = 5, NPASS = 16, G = 256, RN0 = 192, SMAX = 64;
+constexpr int BUF_RSRC = 0x00020000;   // buffer resource word 3 (gfx9 family)
+constexpr int SC1 = 16;                // buffer instruction cache policy: sc1
+
+enum Kind { K_RNA = 0, K_QKV = 1, K_ATT = 2, K_O = 3, K_RNF = 4, K_GU = 5, K_DN = 6, K_HEAD = 7 };
+__device__ __forceinline__ int ph_of(int pass, int l, int k) { return pass * 48 + l * 8 + k; }
+
+// ---------------------------------------------------------------- state block (cpb_state_bytes, zeroed once)
+struct StateLayout {
+    size_t xna = 0;
+    size_t xnf = xna + (size_t)SMAX * H * 2;
+    size_t qkv = xnf + (size_t)SMAX * H * 2;
+    size_t attn = qkv + (size_t)SMAX * QKVN * 4;
+    size_t slo = attn + (size_t)SMAX * NH * D * 2;
+    size_t sld = slo + (size_t)4 * SMAX * H * 4;
+    size_t h = sld + (size_t)4 * SMAX * H * 4;
+    size_t flags = h + (size_t)SMAX * INTER * 2;   // 8 kinds x 256 u32
+    size_t ctr = flags + 8 * 256 * 4;               // seq, err (own lines)
+    size_t total = ctr + 256;
+};
+
+struct BLds {
+    float red[4 * 2 * 16 * 64];   // MFMA K-quarter partial tiles [wave][tt][reg][lane]
+    SelLds sel;
+    AttnSmallLds att[4];
+    double dscr[4];
+    int toks[16];
+    PLayerW layers[NLC];
+    const uint16_t *heads[16];
+    const uint16_t *tabs[16];
+};
+
+struct Ctx {
+    const CpbParams &p;
+    BLds &S;
+    Ctl c;
+    unsigned seq;
+    unsigned *flags;
+    __amdgpu_buffer_rsrc_t rs;   // the whole state block
+    int S_;                      // slots
+    __device__ uint32_t tag(int ph) const { return (seq << 10) + (unsigned)ph + 1u; }
+    __device__ unsigned *flag(int kind, int j) const { return flags + kind * 256 + j; }
+};
+
+// ---------------------------------------------------------------- flag polls
+// every lane i < n of the wave polls flag idx(i); the wave leaves once all carry `tag` (bounded)
+template <class Idx>
+__device__ __forceinline__ void wait_flags(Ctx &X, int kind, int n, Idx idx, uint32_t tag) {
+    const int lane = threadIdx.x & 63;
+    const unsigned *f0 = X.flags + kind * 256;
+    const unsigned *fa = f0 + idx(lane < n ? lane : 0);
+    const unsigned *fb = f0 + idx(lane + 64 < n ? lane + 64 : 0);
+    unsigned it = 0;
+    while (true) {
+        bool ok = true;
+        if (lane < n) ok &= __hip_atomic_load(fa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
+        if (lane + 64 < n) ok &= __hip_atomic_load(fb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
+        if (__all(ok) || X.c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                X.c.abort = true;
+                __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);   // the payload loads stay behind the poll
+}
+
+// publish: every storing wave drains its sc1 stores, then one lane signals for the workgroup
+__device__ __forceinline__ void publish(Ctx &X, int kind, int j, uint32_t tag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(X.flag(kind, j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------- MFMA tile job (gemm_mfma.hip k_gemm_mfma numerics)
+// A = W[row0 + r][k], B = X[token][k] for lane (r = lane & 31, h = lane >> 5), k = kq + 64c + 32h + 8j: wave w owns the
+// K quarter starting at kq = kbase + w * 64 NCH.  wb[4c + j] holds the A fragments (issued one job ahead).
+template <int NCH>
+__device__ __forceinline__ void load_w(uint4 (&wb)[16], const uint16_t *W, int ldw, int row0, int kbase) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+    const uint16_t *p = W + (size_t)(row0 + r) * ldw + kbase + wave * (NCH * 64) + h * 32;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wb[4 * c + j] = ld16(p + c * 64 + j * 8);
+}
+
+// B fragments of NTT token tiles (tile tt: tokens t0[tt] + r, clamped to the last slot), sc1 loads of the hand-off
+// buffer at byte offset xoff (row stride ldx halves), then the MFMA chain in k_gemm_mfma's order
+template <int NCH, int NTT>
+__device__ __forceinline__ void mm_tile(Ctx &X, const uint4 (&wb)[16], size_t xoff, int ldx, int kbase, const int (&t0)[NTT],
+                                        f32x16_t (&acc)[NTT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+    u32x4_t xb[NTT][4 * NCH];
+#pragma unroll
+    for (int tt = 0; tt < NTT; ++tt) {
+        const int tok = min(t0[tt] + r, X.S_ - 1);
+        const int off = (int)(xoff + ((size_t)tok * ldx + kbase + wave * (NCH * 64) + h * 32) * 2);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xb[tt][4 * c + j] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, off + (c * 64 + j * 8) * 2, 0, SC1);
+    }
+#pragma unroll
+    for (int tt = 0; tt < NTT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[tt][i] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const half8_t a = __builtin_bit_cast(half8_t, wb[4 * c + j]);
+#pragma unroll
+            for (int tt = 0; tt < NTT; ++tt)
+                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(half8_t, xb[tt][4 * c + j]), acc[tt], 0, 0, 0);
+        }
+}
+
+// the 4 K quarters summed through LDS in wave order (k_gemm_mfma step 4); returns through red
+template <int NTT>
+__device__ __forceinline__ void mm_reduce(BLds &S, const f32x16_t (&acc)[NTT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int tt = 0; tt < NTT; ++tt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S.red[((wave * NTT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
+    __syncthreads();
+}
+template <int NTT>
+__device__ __forceinline__ float sum4(const BLds &S, int tt, int i) {
+    const int lane = threadIdx.x & 63;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += S.red[((w * NTT + tt) * 16 + i) * 64 + lane];
+    return v;
+}
+
+// plain f32 epilogue (QKV rows, lm_head logits, split-K slabs): token tl of tile tt, rows n0 .. n0+3 -> out[tok][n0]
+template <int NTT>
+__device__ __forceinline__ void epi_f32(Ctx &X, size_t obase, int ldo, int row0, const int (&t0)[NTT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int cc = 0; cc < NTT; ++cc) {
+        const int combo = wave + 4 * cc, tt = combo >> 2, q = combo & 3;
+        const int tok = t0[tt] + r;
+        if (tok >= X.S_) continue;
+        const int n0 = row0 + 8 * q + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = sum4<NTT>(X.S, tt, 4 * q + e);
+        const u32x4_t o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(o, X.rs, (int)(obase + ((size_t)tok * ldo + n0) * 4), 0, SC1);
+    }
+}
+
+// ---------------------------------------------------------------- the kernel
+template <int NT>
+__global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    BLds &S = *reinterpret_cast<BLds *>(smem);
+    const StateLayout SL;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, w = blockIdx.x;
+    Ctx X{p, S, Ctl{reinterpret_cast<unsigned *>(p.state + SL.ctr) + 32, false},
+          __hip_atomic_load(reinterpret_cast<unsigned *>(p.state + SL.ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+          reinterpret_cast<unsigned *>(p.state + SL.flags),
+          __builtin_amdgcn_make_buffer_rsrc(p.state, 0, (int)SL.total, BUF_RSRC), p.S};
+    const int NQJ = 128 * NT, NOJ = 128 * NT, NGJ = 192, NDJ = 128 * NT, NHJ = 64 * NT;
+    const bool rn = w >= RN0 && w < RN0 + p.S;
+    const int b = w - RN0, btt = b >> 5;
+    const bool hq = w < NQJ, ho = w < NOJ, hg = w < NGJ, hd = w < NDJ, hh = w < NHJ;
+    if (t < NLC) S.layers[t] = p.L[t];
+    if (t < 15) S.heads[t] = p.heads[t];
+    if (t < 16) S.tabs[t] = p.tabs[t];
+    if (rn && t < 16) S.toks[t] = p.sel.tokens[b * 16 + t];
+    __syncthreads();
+
+    // ---- the GEMM job sequence of this workgroup, weights issued one job ahead
+    uint4 wb[16];
+    int cp = 0, cl = 0, ck = K_QKV;   // slot of the job whose weights wb holds (cp = NPASS: none)
+    auto has = [&](int k) { return k == K_QKV ? hq : k == K_O ? ho : k == K_GU ? hg : k == K_DN ? hd : hh; };
+    auto advance = [&]() {
+        if (ck == K_QKV) {
+            if (cp == 0 && cl == NLC - 1) { cp = 1; cl = 0; ck = K_O; }
+            else ck = K_O;
+        } else if (ck == K_O) ck = K_GU;
+        else if (ck == K_GU) ck = K_DN;
+        else if (ck == K_DN) {
+            if (cl + 1 < NLC) { ++cl; ck = K_QKV; }
+            else { cl = NLC; ck = K_HEAD; }
+        } else { ++cp; cl = 0; ck = K_O; }
+    };
+    auto issue = [&]() {
+        while (cp < NPASS && !has(ck)) advance();
+        if (cp >= NPASS) return;
+        const PLayerW &Lw = S.layers[cl < NLC ? cl : 0];
+        switch (ck) {
+            case K_QKV: load_w<4>(wb, Lw.qkv, H, 32 * (w % 128), 0); break;
+            case K_O: load_w<2>(wb, Lw.o, NH * D, 32 * (w % 32), 512 * ((w / 32) % 4)); break;
+            case K_GU: load_w<4>(wb, Lw.gu, H, 32 * w, 0); break;
+            case K_DN: load_w<3>(wb, Lw.down, INTER, 32 * (w % 32), 768 * ((w / 32) % 4)); break;
+            default: load_w<4>(wb, S.heads[cp - 1], H, 32 * (w % 64), 0); break;
+        }
+    };
+    auto next_job = [&]() { advance(); issue(); };
+    bool pending = false;   // an RN workgroup issues the next job's weights after its RN step (its slab loads first)
+    auto after_job = [&]() { if (rn) pending = true; else next_job(); };
+    auto after_rn = [&]() { if (pending) { next_job(); pending = false; } };
+    issue();
+
+    // ---- the RN workgroups' residual row (thread t: elements 4t .. 4t+3)
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    // RMSNorm of x -> f16 row of slot b in the hand-off buffer `xo`, flag (kind, b)
+    auto norm_pub = [&](const float *nw, size_t xo, int kind, uint32_t tg) {
+        double ss = (double)(x.x * x.x) + (double)(x.y * x.y) + (double)(x.z * x.z) + (double)(x.w * x.w);
+        ss = block_sum_d(ss, S.dscr);
+        const float scale = 1.0f / sqrtf((float)(ss / H) + p.eps);
+        const float4 wv = ldf4(nw + 4 * t);
+        const float y0 = (x.x * scale) * wv.x, y1 = (x.y * scale) * wv.y, y2 = (x.z * scale) * wv.z, y3 = (x.w * scale) * wv.w;
+        const u32x2_t hv = {(uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16), (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16)};
+        __builtin_amdgcn_raw_buffer_store_b64(hv, X.rs, (int)(xo + ((size_t)b * H + 4 * t) * 2), 0, SC1);
+        publish(X, kind, b, tg);
+    };
+    // x += the 4 split-K slabs of slot b (k_resid_norm<4> order); wave w waits for the 8 row tiles x 4 slices it reads
+    auto fold = [&](int kind, size_t slab, uint32_t tg) {
+        wait_flags(X, kind, 32, [&](int i) { return (8 * wave + (i & 7)) + 32 * (i >> 3) + 128 * btt; }, tg);
+        u32x4_t pz[4];
+#pragma unroll
+        for (int z = 0; z < 4; ++z) pz[z] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, (int)(slab + (((size_t)z * SMAX + b) * H + 4 * t) * 4), 0, SC1);
+#pragma unroll
+        for (int z = 0; z < 4; ++z)
+            x = make_float4(x.x + __uint_as_float(pz[z].x), x.y + __uint_as_float(pz[z].y), x.z + __uint_as_float(pz[z].z),
+                            x.w + __uint_as_float(pz[z].w));
+    };
+
+    for (int pass = 0; pass < NPASS; ++pass) {
+        const int pos = rn ? p.pos[(size_t)pass * p.pos_ld + b] : 0;
+        for (int l = 0; l < NLC; ++l) {
+            const PLayerW &Lw = S.layers[l];
+            if (pass == 0 || l >= 1) {
+                // ---- RN_A: the layer's input row, normalised (pass 0 layer 0: the talker hidden state)
+                if (rn) {
+                    if (pass == 0 && l == 0) x = ldf4(p.x_in + (size_t)b * H + 4 * t);
+                    else fold(K_DN, SL.sld, X.tag(ph_of(pass, l - 1, K_DN)));
+                    norm_pub(Lw.attn_norm, SL.xna, K_RNA, X.tag(ph_of(pass, l, K_RNA)));
+                    after_rn();
+                }
+                // ---- QKV: rows 32 rt .. +31 of tile tt
+                if (hq) {
+                    const int rt = w % 128, tt = w / 128;
+                    const int nv = min(32, p.S - 32 * tt);
+                    wait_flags(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNA)));
+                    const int t0[1] = {32 * tt};
+                    f32x16_t acc[1];
+                    mm_tile<4, 1>(X, wb, SL.xna, H, 0, t0, acc);
+                    mm_reduce<1>(S, acc);
+                    epi_f32<1>(X, SL.qkv, QKVN, 32 * rt, t0);
+                    publish(X, K_QKV, w, X.tag(ph_of(pass, l, K_QKV)));
+                    after_job();
+                }
+            }
+            // ---- ATT: slot b's 8 kv groups, two per wave
+            if (rn) {
+                const bool tab = pass >= 1 && l == 0;
+                const float *row = tab ? p.qkvtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * CPV) + S.toks[pass - 1]) * QKVN
+                                       : reinterpret_cast<const float *>(p.state + SL.qkv) + (size_t)b * QKVN;
+                for (int gg = 0; gg < 2; ++gg) {
+                    const int g = wave + 4 * gg;
+                    if (!tab)
+                        wait_flags(X, K_QKV, 16, [&](int i) { return (i < 8 ? 8 * g + i : i < 12 ? 64 + 4 * g + i - 8 : 96 + 4 * g + i - 12) + 128 * btt; },
+                                   X.tag(ph_of(pass, l, K_QKV)));
+                    const size_t hoff = (size_t)l * p.kv_layer + (((size_t)b * NKV + g) * 16) * D;
+                    attn_small_wave<true>(g, pos, NH, NKV, row, Lw.qn, Lw.kn, p.eps, p.rope + (size_t)pos * D, p.kc + hoff, p.vc + hoff,
+                                          reinterpret_cast<uint16_t *>(p.state + SL.attn) + (size_t)b * NH * D, S.att[wave]);
+                }
+                if (!(pass == 0 && l == NLC - 1)) publish(X, K_ATT, b, X.tag(ph_of(pass, l, K_ATT)));
+                else __syncthreads();
+                after_rn();
+            }
+            if (pass == 0 && l == NLC - 1) continue;   // pass 0's last layer: only its K/V rows are ever read
+            // ---- O: split-K slab z of rows 32 rt .. +31, tile tt
+            if (ho) {
+                const int rt = w % 32, z = (w / 32) % 4, tt = w / 128;
+                const int nv = min(32, p.S - 32 * tt);
+                wait_flags(X, K_ATT, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_ATT)));
+                const int t0[1] = {32 * tt};
+                f32x16_t acc[1];
+                mm_tile<2, 1>(X, wb, SL.attn, NH * D, 512 * z, t0, acc);
+                mm_reduce<1>(S, acc);
+                epi_f32<1>(X, SL.slo + (size_t)z * SMAX * H * 4, H, 32 * rt, t0);
+                publish(X, K_O, w, X.tag(ph_of(pass, l, K_O)));
+                after_job();
+            }
+            // ---- RN_F
+            if (rn) {
+                fold(K_O, SL.slo, X.tag(ph_of(pass, l, K_O)));
+                norm_pub(Lw.ffn_norm, SL.xnf, K_RNF, X.tag(ph_of(pass, l, K_RNF)));
+                after_rn();
+            }
+            // ---- GU: 16 SwiGLU units (rows 32 rt .. +31, gate/up interleaved), every token tile
+            if (hg) {
+                wait_flags(X, K_RNF, p.S, [&](int i) { return i; }, X.tag(ph_of(pass, l, K_RNF)));
+                int t0[NT];
+#pragma unroll
+                for (int tt = 0; tt < NT; ++tt) t0[tt] = 32 * tt;
+                f32x16_t acc[NT];
+                mm_tile<4, NT>(X, wb, SL.xnf, H, 0, t0, acc);
+                mm_reduce<NT>(S, acc);
+                if (wave < NT * 2) {   // k_gemm_mfma SWIGLU epilogue: combo (tt, q)
+                    const int tt = wave >> 1, q = wave & 1, r = lane & 31, h = lane >> 5;
+                    const int tok = 32 * tt + r;
+                    if (tok < p.S) {
+                        const int unit = 16 * w + 8 * q + 4 * h;
+                        float hv[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4<NT>(S, tt, 4 * q + e)) * sum4<NT>(S, tt, 4 * (q + 2) + e);
+                        const u32x2_t o = {(uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16),
+                                           (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16)};
+                        __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)(SL.h + ((size_t)tok * INTER + unit) * 2), 0, SC1);
+                    }
+                }
+                publish(X, K_GU, w, X.tag(ph_of(pass, l, K_GU)));
+                after_job();
+            }
+            // ---- DN: split-K slab z of rows 32 rt .. +31, tile tt; wave w reads units [768 z + 192 w, +192)
+            if (hd) {
+                const int rt = w % 32, z = (w / 32) % 4, tt = w / 128;
+                wait_flags(X, K_GU, 12, [&](int i) { return 48 * z + 12 * wave + i; }, X.tag(ph_of(pass, l, K_GU)));
+                const int t0[1] = {32 * tt};
+                f32x16_t acc[1];
+                mm_tile<3, 1>(X, wb, SL.h, INTER, 768 * z, t0, acc);
+                mm_reduce<1>(S, acc);
+                epi_f32<1>(X, SL.sld + (size_t)z * SMAX * H * 4, H, 32 * rt, t0);
+                publish(X, K_DN, w, X.tag(ph_of(pass, l, K_DN)));
+                after_job();
+            }
+        }
+        if (pass == 0) {   // pass 1's input: the codec_embd row of CB0 (k_gather_sum, one table)
+            if (rn) {
+                const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[0] + (size_t)S.toks[0] * H + 4 * t);
+                x = make_float4(h2f(u.x & 0xffff), h2f(u.x >> 16), h2f(u.y & 0xffff), h2f(u.y >> 16));
+            }
+            continue;
+        }
+        // ---- final RMSNorm (output_norm) -> lm_head[pass - 1] -> selection of code `pass`
+        if (rn) {
+            fold(K_DN, SL.sld, X.tag(ph_of(pass, NLC - 1, K_DN)));
+            norm_pub(p.out_norm, SL.xna, K_RNA, X.tag(ph_of(pass, NLC, K_RNA)));
+            after_rn();
+        }
+        if (hh) {
+            const int rt = w % 64, tt = w / 64;
+            const int nv = min(32, p.S - 32 * tt);
+            wait_flags(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, NLC, K_RNA)));
+            const int t0[1] = {32 * tt};
+            f32x16_t acc[1];
+            mm_tile<4, 1>(X, wb, SL.xna, H, 0, t0, acc);
+            mm_reduce<1>(S, acc);
+            // logits into the context's buffer (p.logits, [S][2048]): its own resource
+            {
+                const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(p.logits, 0, p.S * CPV * 4, BUF_RSRC);
+                const int r = lane & 31, h = lane >> 5;
+                const int q = wave, tok = t0[0] + r;
+                if (tok < p.S) {
+                    const int n0 = 32 * rt + 8 * q + 4 * h;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = sum4<1>(S, 0, 4 * q + e);
+                    const u32x4_t o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+                    __builtin_amdgcn_raw_buffer_store_b128(o, lr, (tok * CPV + n0) * 4, 0, SC1);
+                }
+            }
+            publish(X, K_HEAD, w, X.tag(ph_of(pass, NLC, K_HEAD)));
+            after_job();
+        }
+        if (rn) {
+            if (wave == 0) wait_flags(X, K_HEAD, 64, [&](int i) { return i + 64 * btt; }, X.tag(ph_of(pass, NLC, K_HEAD)));
+            __syncthreads();
+            SelectSpec sp = p.sel;
+            sp.step = pass - 1;
+            const int tok = select_token<true>(sp, p.logits + (size_t)b * CPV, b, S.sel);   // -1: slot done
+            if (t == 0 && tok >= 0) {
+                select_commit(sp, b, tok);
+                S.toks[pass] = tok;
+            }
+            __syncthreads();
+            if (pass + 1 < NPASS) {   // the next pass's input: code_pred.codec_embd[pass - 1] row of this token
+                const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[pass] + (size_t)S.toks[pass] * H + 4 * t);
+                x = make_float4(h2f(u.x & 0xffff), h2f(u.x >> 16), h2f(u.y & 0xffff), h2f(u.y >> 16));
+            } else {
+                if (p.talker_next) {   // the next talker step's embedding + its layer-0 RMSNorm (k_select_embed_norm, nt 16)
+                    float a[4];
+                    {
+                        const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[0] + (size_t)S.toks[0] * H + 4 * t);
+                        a[0] = h2f(u.x & 0xffff); a[1] = h2f(u.x >> 16); a[2] = h2f(u.y & 0xffff); a[3] = h2f(u.y >> 16);
+                    }
+#pragma unroll
+                    for (int j = 1; j < 16; ++j) {
+                        const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[j] + (size_t)S.toks[j] * H + 4 * t);
+                        a[0] += h2f(u.x & 0xffff); a[1] += h2f(u.x >> 16); a[2] += h2f(u.y & 0xffff); a[3] += h2f(u.y >> 16);
+                    }
+                    const int fr = p.frame[b];
+                    const float *extra = fr < p.tr_len[b] ? p.tr + (size_t)b * p.tr_ld + (size_t)fr * H : p.pad + (size_t)b * H;
+                    const float4 e = ldf4(extra + 4 * t);
+                    a[0] += e.x; a[1] += e.y; a[2] += e.z; a[3] += e.w;
+                    const float4 xt = make_float4(a[0], a[1], a[2], a[3]);
+                    *reinterpret_cast<float4 *>(p.tx + (size_t)b * H + 4 * t) = xt;
+                    double ss = (double)(xt.x * xt.x) + (double)(xt.y * xt.y) + (double)(xt.z * xt.z) + (double)(xt.w * xt.w);
+                    ss = block_sum_d(ss, S.dscr);
+                    const float scale = 1.0f / sqrtf((float)(ss / H) + p.eps);
+                    const float4 wv = ldf4(p.tnw + 4 * t);
+                    const float y0 = (xt.x * scale) * wv.x, y1 = (xt.y * scale) * wv.y, y2 = (xt.z * scale) * wv.z, y3 = (xt.w * scale) * wv.w;
+                    uint2 hh2;
+                    hh2.x = (uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16);
+                    hh2.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
+                    *reinterpret_cast<uint2 *>(p.txn + (size_t)b * H + 4 * t) = hh2;
+                }
+                if (b == 0 && t == 0)   // every workgroup has read seq: each one's first job fed this last selection
+                    __hip_atomic_store(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            after_rn();
+        }
+    }
+}
+
+size_t cpb_lds() { return std::max(sizeof(BLds), (size_t)96 * 1024); }   // > 80 KB: one workgroup per CU
+
+template <int NT>
+bool cpb_attr() {
+    static bool done = false;
+    if (!done) {
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_cpb<NT>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)cpb_lds()));
+        done = true;
+    }
+    return true;
+}
+
+}  // namespace
+
+size_t cpb_state_bytes() { return StateLayout().total; }
+bool cpb_error(const uint8_t *state, hipStream_t s, bool *err) {
+    unsigned e = 0;
+    Q3T_HIP(hipMemcpyAsync(&e, state + StateLayout().ctr + 32 * 4, 4, hipMemcpyDeviceToHost, s));
+    Q3T_HIP(hipStreamSynchronize(s));
+    *err = e != 0;
+    return true;
+}
+bool cpb_clear(uint8_t *state, hipStream_t s) {   // after a fault: zero the flags and the error word (seq kept)
+    const StateLayout L;
+    Q3T_HIP(hipMemsetAsync(state + L.flags, 0, L.ctr - L.flags, s));
+    Q3T_HIP(hipMemsetAsync(state + L.ctr + 32 * 4, 0, 4, s));
+    return true;
+}
+
+bool cpb_resident(int device) {
+    int n_cu = 0, blocks = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < G) return false;
+    for (const void *k : {reinterpret_cast<const void *>(&k_cpb<1>), reinterpret_cast<const void *>(&k_cpb<2>)}) {
+        if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpb_lds()) != hipSuccess) return false;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, cpb_lds()) != hipSuccess || blocks < 1) return false;
+    }
+    return true;
+}
+
+bool persist_cp_batched(const CpbParams &p, hipStream_t s) {
+    if (!p.L || !p.heads || !p.tabs || !p.out_norm || !p.qkvtab || !p.x_in || !p.rope || !p.pos || !p.kc || !p.vc || !p.logits ||
+        !p.state || p.S < 1 || p.S > SMAX || p.sel.mode != SEL_CP || p.sel.V != CPV || !p.sel.tokens ||
+        (p.talker_next && !(p.tx && p.txn && p.tnw && p.tr && p.tr_len && p.frame && p.pad))) {
+        set_error("persist_cp_batched: bad parameters");
+        return false;
+    }
+    if (p.S <= 32) {
+        if (!cpb_attr<1>()) return false;
+        hipLaunchKernelGGL(k_cpb<1>, dim3(G), dim3(256), cpb_lds(), s, p);
+    } else {
+        if (!cpb_attr<2>()) return false;
+        hipLaunchKernelGGL(k_cpb<2>, dim3(G), dim3(256), cpb_lds(), s, p);
+    }
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
+}  // namespace q3t
