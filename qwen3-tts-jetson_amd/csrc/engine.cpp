@@ -537,6 +537,9 @@ bool Engine::setup_cpb() {
     if (!cpb_) return true;
     cpb_state_ = dalloc<uint8_t>(cpb_state_bytes());
     if (!cpb_state_) { set_error("device allocation failed"); return false; }
+#ifdef Q3T_DEV
+    if (std::getenv("Q3T_PERSIST_PROF") && !pprof_) pprof_ = dalloc<uint64_t>((size_t)PROF_WG * PROF_PH * 4);
+#endif
     if (!pl_cp_dev_) {
         std::vector<PLayerW> cpl(CP_.size());
         for (size_t i = 0; i < CP_.size(); ++i)
@@ -574,11 +577,19 @@ struct CpTables {
     size_t bytes = 0;
     bool built = false;
     std::mutex build;   // held by the building context; later users wait for the finished tables
-    ~CpTables() {
+    // drop whatever a failed build allocated, so the next context with the same key starts from scratch (no leaked HBM,
+    // no bytes counted twice)
+    void reset() {
+        int prev = -1;
+        hipGetDevice(&prev);
         if (device >= 0) hipSetDevice(device);
         if (qkv) hipFree(qkv);
         if (proj) hipFree(proj);
+        qkv = proj = nullptr;
+        bytes = 0;
+        if (prev >= 0) hipSetDevice(prev);   // the caller's current device is restored
     }
+    ~CpTables() { reset(); }
 };
 namespace {
 std::mutex g_cp_tables_m;
@@ -627,6 +638,12 @@ bool Engine::build_persist_tables() {
     cp_tables_ = cp_tables_for(device_, key);
     std::lock_guard<std::mutex> g(cp_tables_->build);
     if (!cp_tables_->built) {
+        // any failure below leaves the entry empty (not half-built) for the next context of this key
+        struct Undo {
+            CpTables *t;
+            bool armed = true;
+            ~Undo() { if (armed) t->reset(); }
+        } undo{cp_tables_.get()};
         table_iota_ = dalloc<int>(c_.codec_vocab);
         if (!table_iota_) { set_error("device allocation failed (table token iota)"); return false; }
         std::vector<int> ih(c_.codec_vocab);
@@ -656,6 +673,7 @@ bool Engine::build_persist_tables() {
         if (want_proj && !build_cp_proj_table()) return false;
         if (want_qkv && !build_cp_qkv_table()) return false;
         cp_tables_->built = true;
+        undo.armed = false;
     }
     cp_qkvtab_ = cp_tables_->qkv;
     cp_projtab_ = cp_tables_->proj;
@@ -1141,6 +1159,7 @@ bool Engine::enqueue_cp_frame(int S, hipStream_t s, float *logits_host, bool tal
             p.tr = trailing_; p.tr_len = trailing_len_; p.frame = frame_; p.tr_ld = max_trailing_ * H; p.pad = tts_pad_;
         }
         p.state = cpb_state_;
+        p.prof = pprof_;
         return persist_cp_batched(p, s);
     }
     const bool fsel_all = fused_select_ && !use_mm(S);

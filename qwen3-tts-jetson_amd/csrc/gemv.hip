@@ -34,6 +34,17 @@ static int g_min_blocks = [] {
 #endif
 }();
 static int gemv_min_blocks() { return g_min_blocks; }
+// compute units of the current device (cached per device id)
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cus[dev];
+}
 void gemv_set_min_blocks(int n) { g_min_blocks = n > 0 ? n : 256; }
 
 bool gemv(const GemvParams &p, hipStream_t s) {
@@ -111,8 +122,9 @@ bool gemv(const GemvParams &p, hipStream_t s) {
 #define Q3T_GEMV_ROUNDS 1
 #endif
     // rows wider than 1,024 (the 1.7B talker and its codec head; never a shape the persistent kernels restate): a grid
-    // of whole rounds of workgroups per CU (1.7B gate/up: 384 workgroups left half the CUs with two, 768 give all three)
-    if (Q3T_GEMV_ROUNDS && p.K > 1024 && ks < 4 && blocks_for(ks) % 256 != 0) ks *= 2;
+    // of whole rounds of workgroups per CU (1.7B gate/up: 384 workgroups left half the CUs with two, 768 give all three).
+    // Unlike NL below, ks changes the row's summation order: it depends on the device's CU count, fixed per device
+    if (Q3T_GEMV_ROUNDS && p.K > 1024 && ks < 4 && blocks_for(ks) % device_cus() != 0) ks *= 2;
     const int nsteps = (Kp / 128 + ks - 1) / ks;
     // NL: weight loads per lane issued up front (16 only for single-row launches; launch_nl streams the rest with NL 0).
     // The loads' schedule only: the K order of every row is the same for any NL

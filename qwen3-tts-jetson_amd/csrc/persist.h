@@ -124,6 +124,7 @@ struct CpbParams {
     const int *tr_len = nullptr, *frame = nullptr;
     int tr_ld = 0;
     uint8_t *state = nullptr;                    // cpb_state_bytes(), zeroed once
+    uint64_t *prof = nullptr;                    // development timeline [256][768][4] (null = off)
 };
 size_t cpb_state_bytes();
 bool cpb_resident(int device);                   // both instantiations fit one workgroup per CU, >= 256 CUs

@@ -90,9 +90,21 @@ struct Ctx {
 
 // ---------------------------------------------------------------- flag polls
 // every lane i < n of the wave polls flag idx(i); the wave leaves once all carry `tag` (bounded)
+#ifdef Q3T_DEV
+// development timeline (Q3T_PERSIST_PROF): thread 0 of each workgroup stamps phase ph, k = 0 wait start, 1 data ready,
+// 2 published; [workgroup][768 phases][4] s_memrealtime (100 MHz)
+#define CPROF(ph, k)                                                                                          \
+    do {                                                                                                      \
+        if (X.p.prof && threadIdx.x == 0) X.p.prof[((size_t)blockIdx.x * 768 + (ph)) * 4 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define CPROF(ph, k) ((void)0)
+#endif
 template <class Idx>
 __device__ __forceinline__ void wait_flags(Ctx &X, int kind, int n, Idx idx, uint32_t tag) {
     const int lane = threadIdx.x & 63;
+    const int ph_ = (int)((tag - 1u) & 1023u);
+    CPROF(ph_, 0);
     const unsigned *f0 = X.flags + kind * 256;
     const unsigned *fa = f0 + idx(lane < n ? lane : 0);
     const unsigned *fb = f0 + idx(lane + 64 < n ? lane + 64 : 0);
@@ -113,6 +125,7 @@ __device__ __forceinline__ void wait_flags(Ctx &X, int kind, int n, Idx idx, uin
         __builtin_amdgcn_s_sleep(1);
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);   // the payload loads stay behind the poll
+    CPROF(ph_, 1);
 }
 
 // publish: every storing wave drains its sc1 stores, then one lane signals for the workgroup
@@ -120,6 +133,7 @@ __device__ __forceinline__ void publish(Ctx &X, int kind, int j, uint32_t tag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(X.flag(kind, j), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    CPROF((int)((tag - 1u) & 1023u), 2);
 }
 
 // ---------------------------------------------------------------- MFMA tile job (gemm_mfma.hip k_gemm_mfma numerics)
@@ -433,6 +447,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 S.toks[pass] = tok;
             }
             __syncthreads();
+            CPROF(ph_of(pass, NLC, K_HEAD), 3);
             if (pass + 1 < NPASS) {   // the next pass's input: code_pred.codec_embd[pass - 1] row of this token
                 const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[pass] + (size_t)S.toks[pass] * H + 4 * t);
                 x = make_float4(h2f(u.x & 0xffff), h2f(u.x >> 16), h2f(u.y & 0xffff), h2f(u.y >> 16));

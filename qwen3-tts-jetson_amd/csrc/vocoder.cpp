@@ -440,6 +440,14 @@ bool Vocoder::decode_device(const int32_t *codes_dev, int F, float *pcm_dev, int
     return ok;
 }
 
+// the row GEMVs of a decode: kernel family and K split pinned to one batch size, so a row's arithmetic does not depend
+// on how many frame rows the launch covers (an utterance decoded alone, or padded into a batch, gives the same bits)
+static GemvParams row_gemv() {
+    GemvParams g;
+    g.family_b = 64;
+    return g;
+}
+
 // one decode of nb_ utterances of F frames: row-wise stages (RVQ, projections, norms, 1-tap convs) run over all
 // nb_*F rows, sequence stages (causal convs, transposed convs, attention) carry the utterance as grid z
 bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64_t *n_out, hipStream_t s) {
@@ -448,7 +456,7 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
     float *A = buf_[0], *B = buf_[1], *C = buf_[2];
     // 1) RVQ: latent = W_first . cb_first[c0] + sum_k W_rest . cb_rest_k[c_{k+1}]   (:650-703)
     if (!codes_cols(codes_dev, cols_, FR, 16, s)) return false;
-    GemvParams g;
+    GemvParams g = row_gemv();
     g.N = VH; g.K = cb_dim_; g.B = FR; g.pro = PRO_F16; g.ldx = cb_dim_; g.ldo = VH;
     for (int k = 0; k < 15; ++k) {
         g.W = vq_rest_out_; g.x = cb_rest_[k]; g.x_idx = cols_ + (size_t)(k + 1) * FR;
@@ -460,7 +468,7 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
     // 2) causal pre-conv k3 (left pad 2) -> [F][LAT]   (:705-718)
     if (!run_conv(pre_conv_, A, F, 2, 1, nullptr, C, nullptr, 0, s)) return false;
     // 3) input_proj + bias -> x [F][VH]
-    GemvParams ip;
+    GemvParams ip = row_gemv();
     ip.W = in_proj_; ip.N = VH; ip.K = LAT; ip.B = FR; ip.pro = PRO_F32; ip.x = C; ip.ldx = LAT;
     ip.bias = in_proj_b_; ip.out_f32 = A; ip.ldo = VH;
     if (!gemv(ip, s)) return false;
@@ -480,27 +488,27 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
             q.y = qkv; q.C_out = 3 * LAT; q.M = FR;
             if (!conv(q, s)) return false;
         } else {
-            GemvParams q;
+            GemvParams q = row_gemv();
             q.W = L.qkv; q.N = 3 * LAT; q.K = VH; q.B = FR; q.pro = PRO_RMS; q.x = x; q.ldx = VH; q.nw = L.attn_norm;
             q.eps = 1e-5f; q.out_f32 = qkv; q.ldo = 3 * LAT;
             if (!gemv(q, s)) return false;
         }
         if (!attn_prefill(qkv, rope_, att, F, n_heads_, head_dim_, s, nb_)) return false;
-        GemvParams o;
+        GemvParams o = row_gemv();
         o.W = L.o; o.N = VH; o.K = LAT; o.B = FR; o.pro = PRO_F16; o.x = att; o.ldx = LAT;
         o.scale = L.attn_scale; o.resid = x; o.ldr = VH; o.out_f32 = x; o.ldo = VH;
         if (!gemv(o, s)) return false;
-        GemvParams gu;
+        GemvParams gu = row_gemv();
         gu.W = L.gu; gu.N = 2 * ffn_; gu.K = VH; gu.B = FR; gu.pro = PRO_RMS; gu.x = x; gu.ldx = VH; gu.nw = L.ffn_norm;
         gu.eps = 1e-5f; gu.act = ACT_SWIGLU; gu.out_f16 = hm; gu.ldo = ffn_;
         if (!gemv(gu, s)) return false;
-        GemvParams dn;
+        GemvParams dn = row_gemv();
         dn.W = L.down; dn.N = VH; dn.K = ffn_; dn.B = FR; dn.pro = PRO_F16; dn.x = hm; dn.ldx = ffn_;
         dn.scale = L.ffn_scale; dn.resid = x; dn.ldr = VH; dn.out_f32 = x; dn.ldo = VH;
         if (!gemv(dn, s)) return false;
     }
     // final RMSNorm + output_proj + bias -> [F][LAT]   (:740-744)
-    GemvParams op;
+    GemvParams op = row_gemv();
     op.W = out_proj_; op.N = LAT; op.K = VH; op.B = FR; op.pro = PRO_RMS; op.x = x; op.ldx = VH; op.nw = pre_norm_;
     op.eps = 1e-5f; op.bias = out_proj_b_; op.out_f32 = B; op.ldo = LAT;
     if (!gemv(op, s)) return false;
@@ -529,12 +537,12 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
             c2.C_out = LAT; c2.M = (int)T1 * nb_; c2.bias = U.pw2_b; c2.scale = U.gamma; c2.resid = h; c2.y = h;
             if (!conv(c2, s)) return false;
         } else {
-            GemvParams p1;
+            GemvParams p1 = row_gemv();
             p1.W = U.pw1; p1.N = U.pw_dim; p1.K = LAT; p1.B = (int)T1 * nb_; p1.pro = PRO_LN; p1.x = dwo; p1.ldx = LAT;
             p1.nw = U.norm_w; p1.nb = U.norm_b; p1.eps = 1e-6f; p1.bias = U.pw1_b; p1.act = ACT_GELU;
             p1.out_f16 = pw; p1.ldo = U.pw_dim;
             if (!gemv(p1, s)) return false;
-            GemvParams p2;
+            GemvParams p2 = row_gemv();
             p2.W = U.pw2; p2.N = LAT; p2.K = U.pw_dim; p2.B = (int)T1 * nb_; p2.pro = PRO_F16; p2.x = pw; p2.ldx = U.pw_dim;
             p2.bias = U.pw2_b; p2.scale = U.gamma; p2.resid = h; p2.ldr = LAT; p2.out_f32 = h; p2.ldo = LAT;
             if (!gemv(p2, s)) return false;

@@ -44,7 +44,10 @@ def full():
     orc.close()
 
 
-def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max_off=None):
+MID = (224, 288)     # B=1: a middle window (KV positions 234..297) between the head and the tail
+
+
+def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max_off=None, mid=False):
     nf = out.shape[0]
     kw = dict(force_frames=nf, temperature=temperature, top_k=50, seed=seed, utt=utt)
     if max_off is None:
@@ -52,6 +55,8 @@ def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max
     res = []
     if head:   # frames [0, TAIL): the oracle replays the prefix only (max_len = TAIL: no early-stop semantics)
         res.append(check_decisions(orc, toks, spk, out[:TAIL], max_len=TAIL, max_off_frac=max_off, **kw))
+    if mid:   # frames [MID[0], MID[1]): the oracle replays the GPU's first MID[1] frames, deciding the window's
+        res.append(check_decisions(orc, toks, spk, out[:MID[1]], max_len=MID[1], from_frame=MID[0], max_off_frac=max_off, **kw))
     # frames [nf - TAIL, nf): the earlier frames advance the oracle's talker with the GPU's codes
     res.append(check_decisions(orc, toks, spk, out, max_len=nf, from_frame=nf - TAIL, max_off_frac=max_off, **kw))
     return res
@@ -59,7 +64,8 @@ def _check_head_tail(orc, toks, spk, out, temperature, seed, utt, head=True, max
 
 @pytest.mark.parametrize("temperature", [0.0, 0.9])
 def test_b1_512_frames_at_bench_context(full, temperature):
-    """k_persist<0,64> at n_ctx 544: 9 splits of 64 positions per kv group by the last frame (position 522)"""
+    """k_tk_roles at n_ctx 544: 9 splits of 64 positions per kv group by the last frame (position 522); frames 0-63,
+    224-287 and 448-511 (KV positions 10..73, 234..297, 458..521) teacher-forced against the oracle"""
     import q3t
     tts, tok, orc = full
     eng = q3t.Engine(tts, None, device=0, max_slots=1, max_ctx=MAX_CTX)
@@ -72,7 +78,7 @@ def test_b1_512_frames_at_bench_context(full, temperature):
         assert out.shape == (NF, 16)
         assert eng.persist_status() == 0
         t0 = time.time()
-        for n_off, n_dec, worst in _check_head_tail(orc, toks, spk, out, temperature, 1000, 0):
+        for n_off, n_dec, worst in _check_head_tail(orc, toks, spk, out, temperature, 1000, 0, mid=True):
             print(f"B=1 512 frames T={temperature}: {n_dec - n_off}/{n_dec} exact, worst {worst:.3g}")
         print(f"  oracle {time.time() - t0:.1f} s")
     finally:

@@ -1,0 +1,72 @@
+"""dev: timeline of the batched persistent code-predictor frame (persist_cpb.hip, Q3T_PERSIST_PROF=1, development
+library).  Per hand-off kind, averaged over passes 1..15 and layers: the producers' publish skew, the edge (median
+consumer data-ready minus the LAST producer's publish) and the consumers' span from data-ready to their own publish.
+Clock: s_memrealtime (100 MHz).  Usage: python tools/dev/cpb_timeline.py [slots]"""
+import os
+import sys
+
+import numpy as np
+
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(R, "qwen3-tts-jetson_amd"), os.path.join(R, "tests")]
+os.environ["Q3T_PERSIST_PROF"] = "1"
+os.environ.setdefault("Q3T_DEV_LIB", "1")
+import q3t  # noqa: E402
+from q3t_testutil import synth_dir  # noqa: E402
+
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+tts, _ = synth_dir("full")
+eng = q3t.Engine(tts, None, device=0, max_slots=S, max_ctx=96)
+assert eng.persist_kernels() & 16
+ms = eng.time_stage(1, S, 0, 10)
+T = eng.debug_read(5, 256 * 768 * 4 * 8).view(np.uint64)[: 256 * 768 * 4].reshape(256, 768, 4).astype(np.int64)
+valid = T > 0
+t0 = T[valid].min()
+T = np.where(valid, (T - t0) * 1e-2, np.nan)   # microseconds
+print(f"{S}-slot code-predictor frame: {ms * 1e3:.1f} us per replay; stamped span {np.nanmax(T) - np.nanmin(T):.1f} us")
+NAMES = ["RN_A", "QKV", "ATT", "O", "RN_F", "GU", "DN", "HEAD"]
+# producer kind -> the kind its consumers publish
+NEXT = {0: 1, 1: 2, 2: 3, 3: 4, 4: 5, 5: 6, 6: 0, 7: None}
+
+
+def ph(p, l, k):
+    return p * 48 + l * 8 + k
+
+
+rows = {k: ([], [], []) for k in range(8)}
+for p in range(1, 16):
+    for l in range(6):
+        for k in range(8):
+            x = ph(p, l, k)
+            pub = T[:, x, 2]
+            rdy = T[:, x, 1]
+            if np.isnan(pub).all() or np.isnan(rdy).all():
+                continue
+            last = np.nanmax(pub)
+            skew = last - np.nanmin(pub)
+            edge = np.nanmedian(rdy) - last
+            nk = NEXT[k]
+            span = np.nan
+            if nk is not None:
+                nl = l + 1 if nk == 0 else l
+                if nk == 0 and l == 4:
+                    nl = 5
+                y = ph(p, nl, nk)
+                c = ~np.isnan(rdy) & ~np.isnan(T[:, y, 2])
+                if c.any():
+                    span = np.nanmedian(T[c, y, 2] - rdy[c])
+            rows[k][0].append(skew)
+            rows[k][1].append(edge)
+            rows[k][2].append(span)
+print(f"{'hand-off':8s} {'pub skew':>9s} {'edge':>7s} {'consumer body':>14s}   [us, mean over passes 1..15]")
+for k in range(8):
+    s, e, b = (np.nanmean(v) if len(v) and not np.isnan(v).all() else np.nan for v in rows[k])
+    print(f"{NAMES[k]:8s} {s:9.2f} {e:7.2f} {b:14.2f}")
+# one pass end to end
+for p in (1, 8):
+    a = np.nanmin(T[:, ph(p, 0, 0):ph(p + 1, 0, 0), :]) if p < 15 else np.nan
+    b = np.nanmin(T[:, ph(p + 1, 0, 0):ph(p + 2, 0, 0), :]) if p < 14 else np.nan
+    print(f"pass {p}: {b - a:.1f} us")
+head = [np.nanmax(T[:, ph(p, 5, 7), 2]) - np.nanmax(T[:, ph(p, 5, 0), 2]) for p in range(1, 16)]
+sel = [np.nanmax(T[:, ph(p, 5, 7), 3]) - np.nanmax(T[:, ph(p, 5, 7), 2]) for p in range(1, 16)]
+print(f"final norm -> head published {np.nanmean(head):.2f} us; head published -> selected {np.nanmean(sel):.2f} us")
