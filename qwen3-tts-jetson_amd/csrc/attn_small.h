@@ -73,46 +73,84 @@ __device__ __forceinline__ void unpack8_cvt(const uint4 u, float (&f)[8]) {
 }
 }  // namespace asm_detail
 
-// One (slot, kv head g) of the code predictor's attention at position pos (< 16), 2 q heads of D = 128.
-//   qkv:   the slot's raw Q | K | V row ((nH + 2 nKV) * D f32: the QKV projection, or the per-token table row)
+// The cached K / V rows one lane needs (positions < pos; the new row comes from LDS): they do not depend on this step's
+// QKV row, so a caller issues them before it waits for that row
+struct AttnSmallKV {
+    uint4 kr[8];
+    uint2 vr[16];
+};
+template <bool SC1>
+__device__ __forceinline__ void attn_small_load_kv(int pos, const uint16_t *kc, const uint16_t *vc, AttnSmallKV &kv) {
+    using namespace asm_detail;
+    constexpr int D = 128, NPOS = 16;
+    const int lane = threadIdx.x & 63;
+    const int sj = (lane >> 1) & 15, sk = lane & 1, vd = (lane & 31) * 4;
+    const int jk = min(sj, max(pos - 1, 0));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) kv.kr[e] = ld_k16<SC1>(kc + (size_t)jk * D + sk * 64 + e * 8);
+#pragma unroll
+    for (int j = 0; j < NPOS; ++j) {
+        const int jv = min(j, max(pos - 1, 0));
+        kv.vr[j] = ld_v8<SC1>(vc + (size_t)jv * D + vd);
+    }
+}
+
+// the lane's per-layer / per-position operands: RoPE (cos, sin) of its dimension pair, q / k head-norm weights
+struct AttnSmallAux {
+    float c, sn, qw0, qw1, kw0, kw1;
+};
+__device__ __forceinline__ void attn_small_load_aux(const float *rope_row, const float *qn, const float *kn, AttnSmallAux &a) {
+    const int lane = threadIdx.x & 63;
+    a.c = rope_row[2 * lane];
+    a.sn = rope_row[2 * lane + 1];
+    a.qw0 = qn[lane];
+    a.qw1 = qn[lane + 64];
+    a.kw0 = kn[lane];
+    a.kw1 = kn[lane + 64];
+}
+
+// lane's share of the raw QKV values of kv group g: xs[v][e] = element lane + 64 e of q head 2g (v 0), q head 2g+1 (1),
+// k (2), v (3) of the slot's Q | K | V row ((nH + 2 nKV) * D f32: the QKV projection, or the per-token table row)
+__device__ __forceinline__ int attn_small_src(int g, int v, int nH, int nKV) {
+    constexpr int D = 128, R = 2;
+    return v < R ? (g * R + v) * D : v == R ? (nH + g) * D : (nH + nKV + g) * D;
+}
+template <bool SC1>
+__device__ __forceinline__ void attn_small_load_qkv(const float *qkv, int g, int nH, int nKV, float (&xs)[4][2]) {
+    using namespace asm_detail;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const float *src = qkv + attn_small_src(g, v, nH, nKV);
+        xs[v][0] = ld_f<SC1>(src + lane);
+        xs[v][1] = ld_f<SC1>(src + lane + 64);
+    }
+}
+
+// One (slot, kv head g) of the code predictor's attention at position pos (< 16), 2 q heads of D = 128, from the cached
+// rows `kv` (attn_small_load_kv) and the raw QKV values `xs` (attn_small_load_qkv).
 //   kc/vc: this (layer, slot, kv head)'s cache [16][D] f16; out: the slot's attention row [nH * D] f16
 template <bool SC1>
-__device__ __forceinline__ void attn_small_wave(int g, int pos, int nH, int nKV, const float *qkv, const float *qn,
-                                                const float *kn, float eps, const float *rope_row, uint16_t *kc,
-                                                uint16_t *vc, uint16_t *out, AttnSmallLds &L) {
+__device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float (&xs)[4][2], const AttnSmallAux &aux, int g,
+                                                   int pos, float eps, uint16_t *kc, uint16_t *vc, uint16_t *out,
+                                                   AttnSmallLds &L) {
     using namespace asm_detail;
     constexpr int D = 128, R = 2, NPOS = 16;
     const int lane = threadIdx.x & 63;
     // score lanes: head sh, position sj, K half sk (64 dims); P.V lanes: head vh, dims vd .. vd+3
     const int sh = lane >> 5, sj = (lane >> 1) & 15, sk = lane & 1;
     const int vh = lane >> 5, vd = (lane & 31) * 4;
-    const int jk = min(sj, max(pos - 1, 0));
-    uint4 kr[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) kr[e] = ld_k16<SC1>(kc + (size_t)jk * D + sk * 64 + e * 8);
-    uint2 vr[NPOS];
-#pragma unroll
-    for (int j = 0; j < NPOS; ++j) {
-        const int jv = min(j, max(pos - 1, 0));
-        vr[j] = ld_v8<SC1>(vc + (size_t)jv * D + vd);
-    }
+    uint4 (&kr)[8] = kvr.kr;
+    uint2 (&vr)[NPOS] = kvr.vr;
     // head RMSNorm + NEOX RoPE of the 2 q heads and the new k, the new v f16-rounded (k_attn arithmetic)
-    float xs[4][2];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const float *src = v < R ? qkv + (size_t)(g * R + v) * D : v == R ? qkv + (size_t)(nH + g) * D
-                                                                        : qkv + (size_t)(nH + nKV + g) * D;
-        xs[v][0] = ld_f<SC1>(src + lane);
-        xs[v][1] = ld_f<SC1>(src + lane + 64);
-    }
-    const float c = rope_row[2 * lane], sn = rope_row[2 * lane + 1];
+    const float c = aux.c, sn = aux.sn;
 #pragma unroll
     for (int v = 0; v < R + 1; ++v) {
-        const float *w = v == R ? kn : qn;
+        const float w0 = v == R ? aux.kw0 : aux.qw0, w1 = v == R ? aux.kw1 : aux.qw1;
         double ss = (double)__fmul_rn(xs[v][0], xs[v][0]) + (double)__fmul_rn(xs[v][1], xs[v][1]);
         ss = wave_sum_d(ss);
         const float scale = 1.0f / sqrtf((float)(ss / D) + eps);
-        const float x0 = (xs[v][0] * scale) * w[lane], x1 = (xs[v][1] * scale) * w[lane + 64];
+        const float x0 = (xs[v][0] * scale) * w0, x1 = (xs[v][1] * scale) * w1;
         const float y0 = opaque(opaque(x0 * c) - opaque(x1 * sn));
         const float y1 = opaque(opaque(x0 * sn) + opaque(x1 * c));
         if (v == R) {
@@ -155,14 +193,15 @@ __device__ __forceinline__ void attn_small_wave(int g, int pos, int nH, int nKV,
     // P.V: the new row from LDS
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < NPOS; ++j) {
-        if (j > pos) break;
-        const uint2 u = j == pos ? *reinterpret_cast<const uint2 *>(&L.vh_s[vd]) : vr[j];
-        const float pj = L.pr_s[vh][j];
-        acc[0] = __fmaf_rn(pj, h2f(u.x & 0xffff), acc[0]);
-        acc[1] = __fmaf_rn(pj, h2f(u.x >> 16), acc[1]);
-        acc[2] = __fmaf_rn(pj, h2f(u.y & 0xffff), acc[2]);
-        acc[3] = __fmaf_rn(pj, h2f(u.y >> 16), acc[3]);
+    for (int j = 0; j < NPOS; ++j) {   // positions 0..pos in order (a guard, not a break: j stays a constant, vr in registers)
+        if (j <= pos) {
+            const uint2 u = j == pos ? *reinterpret_cast<const uint2 *>(&L.vh_s[vd]) : vr[j];
+            const float pj = L.pr_s[vh][j];
+            acc[0] = __fmaf_rn(pj, h2f(u.x & 0xffff), acc[0]);
+            acc[1] = __fmaf_rn(pj, h2f(u.x >> 16), acc[1]);
+            acc[2] = __fmaf_rn(pj, h2f(u.y & 0xffff), acc[2]);
+            acc[3] = __fmaf_rn(pj, h2f(u.y >> 16), acc[3]);
+        }
     }
     const float l = L.l_s[vh];
     uint2 o;
@@ -175,6 +214,19 @@ __device__ __forceinline__ void attn_small_wave(int g, int pos, int nH, int nKV,
     } else {
         *reinterpret_cast<uint2 *>(dst) = o;
     }
+}
+
+template <bool SC1>
+__device__ __forceinline__ void attn_small_wave(int g, int pos, int nH, int nKV, const float *qkv, const float *qn,
+                                                const float *kn, float eps, const float *rope_row, uint16_t *kc,
+                                                uint16_t *vc, uint16_t *out, AttnSmallLds &L) {
+    AttnSmallKV kv;
+    attn_small_load_kv<SC1>(pos, kc, vc, kv);
+    float xs[4][2];
+    attn_small_load_qkv<SC1>(qkv, g, nH, nKV, xs);
+    AttnSmallAux aux;
+    attn_small_load_aux(rope_row, qn, kn, aux);
+    attn_small_compute<SC1>(kv, xs, aux, g, pos, eps, kc, vc, out, L);
 }
 
 }  // namespace q3t

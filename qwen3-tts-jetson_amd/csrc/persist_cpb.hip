@@ -9,7 +9,7 @@
 // Work per layer for S slots in NT token tiles of 32 (NT = 1: S <= 32, NT = 2: S <= 64), one 256-thread workgroup per CU:
 //
 //   job              count            workgroups        tile / input (per job)                    output
-//   RN_A / RN_F      1 per slot       192 + b           x[b] += 4 slabs; RMSNorm -> f16 row        xnA / xnF [b]
+//   RN_A / RN_F      1 per slot       128 + 2b          x[b] += 4 slabs; RMSNorm -> f16 row        xnA / xnF [b]
 //   QKV              128 x NT         [0, 128 NT)       32 rows x 32 tokens, K 1024 (xnA 64 KB)    qkv f32
 //   ATT              1 per slot       192 + b           8 kv groups (2 per wave), <= 16 positions  attn f16 [b]
 //   O                32 x 4 x NT      [0, 128 NT)       32 rows x 32 tokens x K slice 512          slabO f32 [z]
@@ -44,29 +44,34 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 constexpr int H = 1024, NH = 16, NKV = 8, D = 128, QKVN = (NH + 2 * NKV) * D, INTER = 3072, CPV = 2048, VOC = 3072;
-constexpr int NLC = 5, NPASS = 16, G = 256, RN0 = 192, SMAX = 64;
+constexpr int NLC = 5, NPASS = 16, G = 256, SW0 = 128, SMAX = 64;
 constexpr int BUF_RSRC = 0x00020000;   // buffer resource word 3 (gfx9 family)
 constexpr int SC1 = 16;                // buffer instruction cache policy: sc1
+constexpr int SC1V = SC1 | (int)0x80000000u;   // sc1, volatile (a poll's load is re-issued every iteration)
 
 enum Kind { K_RNA = 0, K_QKV = 1, K_ATT = 2, K_O = 3, K_RNF = 4, K_GU = 5, K_DN = 6, K_HEAD = 7 };
 __device__ __forceinline__ int ph_of(int pass, int l, int k) { return pass * 48 + l * 8 + k; }
 
 // ---------------------------------------------------------------- state block (cpb_state_bytes, zeroed once)
+// xna / xnf / attn / h: f16 payloads behind flags; qkv, slo, sld, logits: {f32, tag} granules (8 B each, no flag)
 struct StateLayout {
     size_t xna = 0;
     size_t xnf = xna + (size_t)SMAX * H * 2;
     size_t qkv = xnf + (size_t)SMAX * H * 2;
-    size_t attn = qkv + (size_t)SMAX * QKVN * 4;
+    size_t attn = qkv + (size_t)SMAX * QKVN * 8;
     size_t slo = attn + (size_t)SMAX * NH * D * 2;
-    size_t sld = slo + (size_t)4 * SMAX * H * 4;
-    size_t h = sld + (size_t)4 * SMAX * H * 4;
-    size_t flags = h + (size_t)SMAX * INTER * 2;   // 8 kinds x 256 u32
+    size_t sld = slo + (size_t)4 * SMAX * H * 8;
+    size_t h = sld + (size_t)4 * SMAX * H * 8;
+    size_t lg = h + (size_t)SMAX * INTER * 2;
+    size_t flags = lg + (size_t)SMAX * CPV * 8;     // 8 kinds x 256 u32
     size_t ctr = flags + 8 * 256 * 4;               // seq, err (own lines)
     size_t total = ctr + 256;
 };
 
 struct BLds {
-    float red[4 * 2 * 16 * 64];   // MFMA K-quarter partial tiles [wave][tt][reg][lane]
+    // the next job's A fragments [wave][16 rt + 4c + j][lane] (LDS-DMA, issued one job ahead); once a job's MFMAs are
+    // done, wave w's region holds its K-quarter partial tiles [rt][reg][lane] (f32)
+    uint4 wl[4][32][64];
     SelLds sel;
     AttnSmallLds att[4];
     double dscr[4];
@@ -92,7 +97,7 @@ struct Ctx {
 // every lane i < n of the wave polls flag idx(i); the wave leaves once all carry `tag` (bounded)
 #ifdef Q3T_DEV
 // development timeline (Q3T_PERSIST_PROF): thread 0 of each workgroup stamps phase ph, k = 0 wait start, 1 data ready,
-// 2 published; [workgroup][768 phases][4] s_memrealtime (100 MHz)
+// 2 published, 3 computed; [workgroup][768 phases][4] s_memrealtime (100 MHz)
 #define CPROF(ph, k)                                                                                          \
     do {                                                                                                      \
         if (X.p.prof && threadIdx.x == 0) X.p.prof[((size_t)blockIdx.x * 768 + (ph)) * 4 + (k)] = wall_clock64(); \
@@ -104,6 +109,7 @@ template <class Idx>
 __device__ __forceinline__ void wait_flags(Ctx &X, int kind, int n, Idx idx, uint32_t tag) {
     const int lane = threadIdx.x & 63;
     const int ph_ = (int)((tag - 1u) & 1023u);
+    (void)ph_;
     CPROF(ph_, 0);
     const unsigned *f0 = X.flags + kind * 256;
     const unsigned *fa = f0 + idx(lane < n ? lane : 0);
@@ -128,6 +134,14 @@ __device__ __forceinline__ void wait_flags(Ctx &X, int kind, int n, Idx idx, uin
     CPROF(ph_, 1);
 }
 
+// the same for a whole workgroup: wave 0 polls every flag, the others load after the barrier it then joins (the polling
+// traffic of one wave instead of four)
+template <class Idx>
+__device__ __forceinline__ void wait_flags_wg(Ctx &X, int kind, int n, Idx idx, uint32_t tag) {
+    if (threadIdx.x < 64) wait_flags(X, kind, n, idx, tag);
+    __syncthreads();
+}
+
 // publish: every storing wave drains its sc1 stores, then one lane signals for the workgroup
 __device__ __forceinline__ void publish(Ctx &X, int kind, int j, uint32_t tag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -136,85 +150,139 @@ __device__ __forceinline__ void publish(Ctx &X, int kind, int j, uint32_t tag) {
     CPROF((int)((tag - 1u) & 1023u), 2);
 }
 
-// ---------------------------------------------------------------- MFMA tile job (gemm_mfma.hip k_gemm_mfma numerics)
-// A = W[row0 + r][k], B = X[token][k] for lane (r = lane & 31, h = lane >> 5), k = kq + 64c + 32h + 8j: wave w owns the
-// K quarter starting at kq = kbase + w * 64 NCH.  wb[4c + j] holds the A fragments (issued one job ahead).
-template <int NCH>
-__device__ __forceinline__ void load_w(uint4 (&wb)[16], const uint16_t *W, int ldw, int row0, int kbase) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-    const uint16_t *p = W + (size_t)(row0 + r) * ldw + kbase + wave * (NCH * 64) + h * 32;
+// spin until every granule a lane loads (issue(r) fills r) carries `tag` (bounded, as wait_flags)
+template <int M, class Issue>
+__device__ __forceinline__ void poll_gran(Ctx &X, uint32_t tag, u32x4_t (&r)[M], Issue issue) {
+    unsigned it = 0;
+    // gate: lane 0 alone polls its own granules first, so the wave's full sweeps start once the data is arriving
+    if ((threadIdx.x & 63) == 0) {
+        while (true) {
+            issue(r);
+            bool ok = true;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+            for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;
+            if (ok || X.c.abort) break;
+            if ((++it & 255u) == 0 && (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT)) {
+                X.c.abort = true;
+                __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    X.c.abort = __shfl(X.c.abort ? 1 : 0, 0) != 0;
+    it = 0;
+    while (true) {
+        issue(r);
+        bool ok = true;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wb[4 * c + j] = ld16(p + c * 64 + j * 8);
+        for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;
+        if (__all(ok) || X.c.abort) break;
+        ++it;
+        if ((it & 255u) == 0) {
+            if (__hip_atomic_load(X.c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u || it >= SPIN_LIMIT) {
+                X.c.abort = true;
+                __hip_atomic_fetch_or(X.c.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
-// B fragments of NTT token tiles (tile tt: tokens t0[tt] + r, clamped to the last slot), sc1 loads of the hand-off
-// buffer at byte offset xoff (row stride ldx halves), then the MFMA chain in k_gemm_mfma's order
-template <int NCH, int NTT>
-__device__ __forceinline__ void mm_tile(Ctx &X, const uint4 (&wb)[16], size_t xoff, int ldx, int kbase, const int (&t0)[NTT],
-                                        f32x16_t (&acc)[NTT]) {
+// ---------------------------------------------------------------- MFMA tile job (gemm_mfma.hip k_gemm_mfma numerics)
+// A job is RT = 2 row tiles of 32 rows (64 rows) x one 32-token tile: both row tiles share every activation fragment, so
+// the activation rows every job pulls through the fabric (the sc1 hand-off reads, which bound these phases) are half
+// those of 32-row jobs.  Per row tile the arithmetic is k_gemm_mfma's: A = W[row0 + 32 rt + r][k], B = X[token][k] for
+// lane (r = lane & 31, h = lane >> 5), k = kq + 64c + 32h + 8j, wave w owning the K quarter kq = kbase + 64 NCH w, the
+// MFMA chain in (c, j) order, the 4 quarters summed through LDS in wave order.
+constexpr int RT = 2;
+template <int NCH>
+__device__ __forceinline__ void load_w(BLds &S, const uint16_t *W, int ldw, int row0, int kbase) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-    u32x4_t xb[NTT][4 * NCH];
+#ifdef CPB_EXP_NOW   // timing experiment (development variant builds): no weight loads
+    return;
+#endif
 #pragma unroll
-    for (int tt = 0; tt < NTT; ++tt) {
-        const int tok = min(t0[tt] + r, X.S_ - 1);
-        const int off = (int)(xoff + ((size_t)tok * ldx + kbase + wave * (NCH * 64) + h * 32) * 2);
+    for (int rt = 0; rt < RT; ++rt) {
+        const uint16_t *p = W + (size_t)(row0 + 32 * rt + r) * ldw + kbase + wave * (NCH * 64) + h * 32;
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) xb[tt][4 * c + j] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, off + (c * 64 + j * 8) * 2, 0, SC1);
+            for (int j = 0; j < 4; ++j)
+                __builtin_amdgcn_global_load_lds(p + c * 64 + j * 8, (__attribute__((address_space(3))) void *)&S.wl[wave][16 * rt + 4 * c + j][0],
+                                                 16, 0, 0);
     }
-#pragma unroll
-    for (int tt = 0; tt < NTT; ++tt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[tt][i] = 0.0f;
+}
+
+// B fragments of tokens t0 + r (clamped to the last slot): sc1 loads of the hand-off buffer at byte offset xoff (row
+// stride ldx halves), then the MFMA chains; the K-quarter partials land in the wave's LDS region (its A slots, consumed)
+template <int NCH>
+__device__ __forceinline__ void mm_tile(Ctx &X, size_t xoff, int ldx, int kbase, int t0) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+    u32x4_t xb[4 * NCH];
+    const int tok = min(t0 + r, X.S_ - 1);
+    const int off = (int)(xoff + ((size_t)tok * ldx + kbase + wave * (NCH * 64) + h * 32) * 2);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const half8_t a = __builtin_bit_cast(half8_t, wb[4 * c + j]);
-#pragma unroll
-            for (int tt = 0; tt < NTT; ++tt)
-                acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(half8_t, xb[tt][4 * c + j]), acc[tt], 0, 0, 0);
+#ifdef CPB_EXP_NOX   // timing experiment (development variant builds): no activation loads
+            xb[4 * c + j] = u32x4_t{(unsigned)off, 0u, 0u, 0u};
+#else
+            xb[4 * c + j] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, off + (c * 64 + j * 8) * 2, 0, SC1);
+#endif
         }
-}
-
-// the 4 K quarters summed through LDS in wave order (k_gemm_mfma step 4); returns through red
-template <int NTT>
-__device__ __forceinline__ void mm_reduce(BLds &S, const f32x16_t (&acc)[NTT]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    f32x16_t acc[RT];
 #pragma unroll
-    for (int tt = 0; tt < NTT; ++tt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) S.red[((wave * NTT + tt) * 16 + i) * 64 + lane] = acc[tt][i];
+        for (int i = 0; i < 16; ++i) acc[rt][i] = 0.0f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's weight DMA (and the B fragments) have landed
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const half8_t bf = __builtin_bit_cast(half8_t, xb[4 * c + j]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+                acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8_t, X.S.wl[wave][16 * rt + 4 * c + j][lane]), bf,
+                                                                 acc[rt], 0, 0, 0);
+        }
+    // every A slot this wave reads has been read (the MFMAs consumed them): the region takes the partials
+    float *red = reinterpret_cast<float *>(&X.S.wl[wave][0][0]);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(rt * 16 + i) * 64 + lane] = acc[rt][i];
     __syncthreads();
 }
-template <int NTT>
-__device__ __forceinline__ float sum4(const BLds &S, int tt, int i) {
-    const int lane = threadIdx.x & 63;
+// register i of row tile rt, lane `src`, summed over the 4 K quarters in wave order (k_gemm_mfma sum4)
+__device__ __forceinline__ float sum4(const BLds &S, int rt, int i, int src) {
     float v = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) v += S.red[((w * NTT + tt) * 16 + i) * 64 + lane];
+    for (int w = 0; w < 4; ++w) v += reinterpret_cast<const float *>(&S.wl[w][0][0])[(rt * 16 + i) * 64 + src];
     return v;
 }
 
-// plain f32 epilogue (QKV rows, lm_head logits, split-K slabs): token tl of tile tt, rows n0 .. n0+3 -> out[tok][n0]
-template <int NTT>
-__device__ __forceinline__ void epi_f32(Ctx &X, size_t obase, int ldo, int row0, const int (&t0)[NTT]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+// granule epilogue (QKV rows, split-K slabs, lm_head logits): {f32, tag} granules out[tok][row0 ..] with 8-byte sc1
+// stores (MI355X_MICROARCH.md handoff-1to1: the payload carries its own tag, no drain and no flag).  Thread t takes token
+// t / 8 and, for store k, row 8k + t % 8 of each row tile: each store instruction writes 64 contiguous bytes per token
+// (whole lines over four stores).  Register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r.
+__device__ __forceinline__ void epi_gran(Ctx &X, size_t obase, int ldo, int row0, int t0, uint32_t tag) {
+    const int t = threadIdx.x, tl = t >> 3, c = t & 7;
+    const int tok = t0 + tl;
+    if (tok < X.S_) {
 #pragma unroll
-    for (int cc = 0; cc < NTT; ++cc) {
-        const int combo = wave + 4 * cc, tt = combo >> 2, q = combo & 3;
-        const int tok = t0[tt] + r;
-        if (tok >= X.S_) continue;
-        const int n0 = row0 + 8 * q + 4 * h;
-        float v[4];
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = sum4<NTT>(X.S, tt, 4 * q + e);
-        const u32x4_t o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(o, X.rs, (int)(obase + ((size_t)tok * ldo + n0) * 4), 0, SC1);
+            for (int k = 0; k < 4; ++k) {
+                const float v = sum4(X.S, rt, (c & 3) + 4 * k, tl + 32 * ((c >> 2) & 1));
+                const u32x2_t g = {__float_as_uint(v), tag};
+                __builtin_amdgcn_raw_buffer_store_b64(g, X.rs, (int)(obase + ((size_t)tok * ldo + row0 + 32 * rt + 8 * k + c) * 8), 0, SC1);
+            }
     }
+    __syncthreads();   // the LDS region is the next job's DMA target
 }
 
 // ---------------------------------------------------------------- the kernel
@@ -228,20 +296,24 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
           __hip_atomic_load(reinterpret_cast<unsigned *>(p.state + SL.ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
           reinterpret_cast<unsigned *>(p.state + SL.flags),
           __builtin_amdgcn_make_buffer_rsrc(p.state, 0, (int)SL.total, BUF_RSRC), p.S};
-    const int NQJ = 128 * NT, NOJ = 128 * NT, NGJ = 192, NDJ = 128 * NT, NHJ = 64 * NT;
-    const bool rn = w >= RN0 && w < RN0 + p.S;
-    const int b = w - RN0, btt = b >> 5;
-    const bool hq = w < NQJ, ho = w < NOJ, hg = w < NGJ, hd = w < NDJ, hh = w < NHJ;
+    // GEMM jobs: 64 rows x one token tile; QKV / O / DN on [0, 64 NT), gate/up on [0, 96 NT), lm_head on [0, 32 NT)
+    const int NQJ = 64 * NT, NGJ = 96 * NT, NHJ = 32 * NT;
+    // slot workgroups: SW0 + 2b + hf for slot b, half hf (kv groups 4 hf .. 4 hf + 3); the even one (rn) also keeps the
+    // slot's residual row, runs its norms and commits its selections
+    const int sw = w - SW0;
+    const bool slot = sw >= 0 && sw < 2 * p.S;
+    const int b = sw >> 1, hf = sw & 1;
+    const bool rn = slot && hf == 0;
+    const bool hq = w < NQJ, hg = w < NGJ, hh = w < NHJ;
     if (t < NLC) S.layers[t] = p.L[t];
     if (t < 15) S.heads[t] = p.heads[t];
     if (t < 16) S.tabs[t] = p.tabs[t];
-    if (rn && t < 16) S.toks[t] = p.sel.tokens[b * 16 + t];
+    if (slot && t < 16) S.toks[t] = p.sel.tokens[b * 16 + t];
     __syncthreads();
 
     // ---- the GEMM job sequence of this workgroup, weights issued one job ahead
-    uint4 wb[16];
-    int cp = 0, cl = 0, ck = K_QKV;   // slot of the job whose weights wb holds (cp = NPASS: none)
-    auto has = [&](int k) { return k == K_QKV ? hq : k == K_O ? ho : k == K_GU ? hg : k == K_DN ? hd : hh; };
+    int cp = 0, cl = 0, ck = K_QKV;   // slot of the job whose weights S.wl holds (cp = NPASS: none)
+    auto has = [&](int k) { return k == K_GU ? hg : k == K_HEAD ? hh : hq; };
     auto advance = [&]() {
         if (ck == K_QKV) {
             if (cp == 0 && cl == NLC - 1) { cp = 1; cl = 0; ck = K_O; }
@@ -258,16 +330,18 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         if (cp >= NPASS) return;
         const PLayerW &Lw = S.layers[cl < NLC ? cl : 0];
         switch (ck) {
-            case K_QKV: load_w<4>(wb, Lw.qkv, H, 32 * (w % 128), 0); break;
-            case K_O: load_w<2>(wb, Lw.o, NH * D, 32 * (w % 32), 512 * ((w / 32) % 4)); break;
-            case K_GU: load_w<4>(wb, Lw.gu, H, 32 * w, 0); break;
-            case K_DN: load_w<3>(wb, Lw.down, INTER, 32 * (w % 32), 768 * ((w / 32) % 4)); break;
-            default: load_w<4>(wb, S.heads[cp - 1], H, 32 * (w % 64), 0); break;
+            case K_QKV: load_w<4>(S, Lw.qkv, H, 64 * (w % 64), 0); break;
+            case K_O: load_w<2>(S, Lw.o, NH * D, 64 * (w % 16), 512 * ((w / 16) % 4)); break;
+            case K_GU: load_w<4>(S, Lw.gu, H, 64 * (w % 96), 0); break;
+            case K_DN: load_w<3>(S, Lw.down, INTER, 64 * (w % 16), 768 * ((w / 16) % 4)); break;
+            default: load_w<4>(S, S.heads[cp - 1], H, 64 * (w % 32), 0); break;
         }
     };
     auto next_job = [&]() { advance(); issue(); };
-    bool pending = false;   // an RN workgroup issues the next job's weights after its RN step (its slab loads first)
-    auto after_job = [&]() { if (rn) pending = true; else next_job(); };
+    // a slot workgroup issues the next job's weights after its next slot step (whose loads then go first), at the latest
+    // when that job starts
+    bool pending = false;
+    auto after_job = [&]() { if (slot) pending = true; else next_job(); };
     auto after_rn = [&]() { if (pending) { next_job(); pending = false; } };
     issue();
 
@@ -281,102 +355,129 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         const float4 wv = ldf4(nw + 4 * t);
         const float y0 = (x.x * scale) * wv.x, y1 = (x.y * scale) * wv.y, y2 = (x.z * scale) * wv.z, y3 = (x.w * scale) * wv.w;
         const u32x2_t hv = {(uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16), (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16)};
+        CPROF((int)((tg - 1u) & 1023u), 3);
         __builtin_amdgcn_raw_buffer_store_b64(hv, X.rs, (int)(xo + ((size_t)b * H + 4 * t) * 2), 0, SC1);
         publish(X, kind, b, tg);
     };
-    // x += the 4 split-K slabs of slot b (k_resid_norm<4> order); wave w waits for the 8 row tiles x 4 slices it reads
-    auto fold = [&](int kind, size_t slab, uint32_t tg) {
-        wait_flags(X, kind, 32, [&](int i) { return (8 * wave + (i & 7)) + 32 * (i >> 3) + 128 * btt; }, tg);
-        u32x4_t pz[4];
+    // x += the 4 split-K slabs of slot b (k_resid_norm<4> order): thread t polls the 16 granules of its 4 elements
+    auto fold = [&](size_t slab, uint32_t tg) {
+        const int ph_ = (int)((tg - 1u) & 1023u);
+        (void)ph_;
+        CPROF(ph_, 0);
+        u32x4_t pz[8];
+        poll_gran<8>(X, tg, pz, [&](u32x4_t (&r)[8]) {
 #pragma unroll
-        for (int z = 0; z < 4; ++z) pz[z] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, (int)(slab + (((size_t)z * SMAX + b) * H + 4 * t) * 4), 0, SC1);
+            for (int z = 0; z < 4; ++z)
+#pragma unroll
+                for (int hh2 = 0; hh2 < 2; ++hh2)
+                    r[2 * z + hh2] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, (int)(slab + (((size_t)z * SMAX + b) * H + 4 * t + 2 * hh2) * 8), 0, SC1V);
+        });
+        CPROF(ph_, 1);
 #pragma unroll
         for (int z = 0; z < 4; ++z)
-            x = make_float4(x.x + __uint_as_float(pz[z].x), x.y + __uint_as_float(pz[z].y), x.z + __uint_as_float(pz[z].z),
-                            x.w + __uint_as_float(pz[z].w));
+            x = make_float4(x.x + __uint_as_float(pz[2 * z].x), x.y + __uint_as_float(pz[2 * z].z), x.z + __uint_as_float(pz[2 * z + 1].x),
+                            x.w + __uint_as_float(pz[2 * z + 1].z));
     };
 
     for (int pass = 0; pass < NPASS; ++pass) {
-        const int pos = rn ? p.pos[(size_t)pass * p.pos_ld + b] : 0;
+        const int pos = slot ? p.pos[(size_t)pass * p.pos_ld + b] : 0;
         for (int l = 0; l < NLC; ++l) {
             const PLayerW &Lw = S.layers[l];
             if (pass == 0 || l >= 1) {
                 // ---- RN_A: the layer's input row, normalised (pass 0 layer 0: the talker hidden state)
                 if (rn) {
                     if (pass == 0 && l == 0) x = ldf4(p.x_in + (size_t)b * H + 4 * t);
-                    else fold(K_DN, SL.sld, X.tag(ph_of(pass, l - 1, K_DN)));
+                    else fold(SL.sld, X.tag(ph_of(pass, l - 1, K_DN)));
                     norm_pub(Lw.attn_norm, SL.xna, K_RNA, X.tag(ph_of(pass, l, K_RNA)));
                     after_rn();
                 }
-                // ---- QKV: rows 32 rt .. +31 of tile tt
+                // ---- QKV: rows 64 rp .. +63 of tile tt -> granules
                 if (hq) {
-                    const int rt = w % 128, tt = w / 128;
+                    after_rn();
+                    const int rp = w % 64, tt = w / 64;
                     const int nv = min(32, p.S - 32 * tt);
-                    wait_flags(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNA)));
-                    const int t0[1] = {32 * tt};
-                    f32x16_t acc[1];
-                    mm_tile<4, 1>(X, wb, SL.xna, H, 0, t0, acc);
-                    mm_reduce<1>(S, acc);
-                    epi_f32<1>(X, SL.qkv, QKVN, 32 * rt, t0);
-                    publish(X, K_QKV, w, X.tag(ph_of(pass, l, K_QKV)));
+                    wait_flags_wg(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNA)));
+                    mm_tile<4>(X, SL.xna, H, 0, 32 * tt);
+                    CPROF(ph_of(pass, l, K_QKV), 3);
+                    epi_gran(X, SL.qkv, QKVN, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_QKV)));
+                    CPROF(ph_of(pass, l, K_QKV), 2);
                     after_job();
                 }
             }
-            // ---- ATT: slot b's 8 kv groups, two per wave
-            if (rn) {
+            // ---- ATT: kv group 4 hf + wave of slot b (one wave each); its cached K / V rows are loaded before the wait
+            if (slot) {
                 const bool tab = pass >= 1 && l == 0;
-                const float *row = tab ? p.qkvtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * CPV) + S.toks[pass - 1]) * QKVN
-                                       : reinterpret_cast<const float *>(p.state + SL.qkv) + (size_t)b * QKVN;
-                for (int gg = 0; gg < 2; ++gg) {
-                    const int g = wave + 4 * gg;
-                    if (!tab)
-                        wait_flags(X, K_QKV, 16, [&](int i) { return (i < 8 ? 8 * g + i : i < 12 ? 64 + 4 * g + i - 8 : 96 + 4 * g + i - 12) + 128 * btt; },
-                                   X.tag(ph_of(pass, l, K_QKV)));
-                    const size_t hoff = (size_t)l * p.kv_layer + (((size_t)b * NKV + g) * 16) * D;
-                    attn_small_wave<true>(g, pos, NH, NKV, row, Lw.qn, Lw.kn, p.eps, p.rope + (size_t)pos * D, p.kc + hoff, p.vc + hoff,
-                                          reinterpret_cast<uint16_t *>(p.state + SL.attn) + (size_t)b * NH * D, S.att[wave]);
+                const int g = 4 * hf + wave;
+                const size_t hoff = (size_t)l * p.kv_layer + (((size_t)b * NKV + g) * 16) * D;
+                AttnSmallKV kv;
+                attn_small_load_kv<true>(pos, p.kc + hoff, p.vc + hoff, kv);
+                AttnSmallAux aux;
+                attn_small_load_aux(p.rope + (size_t)pos * D, Lw.qn, Lw.kn, aux);
+                float xs[4][2];
+                if (tab) {   // layer 0 of passes 1..15: the per-token table row of the previous pass's token
+                    attn_small_load_qkv<false>(p.qkvtab + ((size_t)(pass == 1 ? 0 : VOC + (pass - 2) * CPV) + S.toks[pass - 1]) * QKVN,
+                                               g, NH, NKV, xs);
+                } else {     // the QKV jobs' granules of slot b
+                    const uint32_t tg = X.tag(ph_of(pass, l, K_QKV));
+                    CPROF(ph_of(pass, l, K_QKV), 0);
+                    u32x4_t gq[4];   // {v, e = 0} / {v, e = 1} of q0, q1, k, v (x, y: e 0; z, w: e 1)
+                    poll_gran<4>(X, tg, gq, [&](u32x4_t (&r)[4]) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const size_t o = SL.qkv + ((size_t)b * QKVN + attn_small_src(g, v, NH, NKV) + lane) * 8;
+                            const u32x2_t a = __builtin_amdgcn_raw_buffer_load_b64(X.rs, (int)o, 0, SC1V);
+                            const u32x2_t c = __builtin_amdgcn_raw_buffer_load_b64(X.rs, (int)(o + 64 * 8), 0, SC1V);
+                            r[v] = u32x4_t{a.x, a.y, c.x, c.y};
+                        }
+                    });
+                    CPROF(ph_of(pass, l, K_QKV), 1);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) { xs[v][0] = __uint_as_float(gq[v].x); xs[v][1] = __uint_as_float(gq[v].z); }
                 }
-                if (!(pass == 0 && l == NLC - 1)) publish(X, K_ATT, b, X.tag(ph_of(pass, l, K_ATT)));
+                attn_small_compute<true>(kv, xs, aux, g, pos, p.eps, p.kc + hoff, p.vc + hoff,
+                                         reinterpret_cast<uint16_t *>(p.state + SL.attn) + (size_t)b * NH * D, S.att[wave]);
+                CPROF(ph_of(pass, l, K_ATT), 3);
+                if (!(pass == 0 && l == NLC - 1)) publish(X, K_ATT, sw, X.tag(ph_of(pass, l, K_ATT)));
                 else __syncthreads();
                 after_rn();
             }
             if (pass == 0 && l == NLC - 1) continue;   // pass 0's last layer: only its K/V rows are ever read
-            // ---- O: split-K slab z of rows 32 rt .. +31, tile tt
-            if (ho) {
-                const int rt = w % 32, z = (w / 32) % 4, tt = w / 128;
+            // ---- O: split-K slab z of rows 64 rp .. +63, tile tt
+            if (hq) {
+                after_rn();
+                const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
                 const int nv = min(32, p.S - 32 * tt);
-                wait_flags(X, K_ATT, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_ATT)));
-                const int t0[1] = {32 * tt};
-                f32x16_t acc[1];
-                mm_tile<2, 1>(X, wb, SL.attn, NH * D, 512 * z, t0, acc);
-                mm_reduce<1>(S, acc);
-                epi_f32<1>(X, SL.slo + (size_t)z * SMAX * H * 4, H, 32 * rt, t0);
-                publish(X, K_O, w, X.tag(ph_of(pass, l, K_O)));
+                // wave w multiplies heads 4 z + w: kv group (4 z + w) / 2, published by the slots' half (4 z + w) / 8
+                // (wave 0 polls both halves' flags of the slice: 4 z + w for w < 4 spans one half)
+                wait_flags_wg(X, K_ATT, nv, [&](int i) { return 2 * (32 * tt + i) + ((4 * z) >> 3); }, X.tag(ph_of(pass, l, K_ATT)));
+                mm_tile<2>(X, SL.attn, NH * D, 512 * z, 32 * tt);
+                CPROF(ph_of(pass, l, K_O), 3);
+                epi_gran(X, SL.slo + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_O)));
+                CPROF(ph_of(pass, l, K_O), 2);
                 after_job();
             }
             // ---- RN_F
             if (rn) {
-                fold(K_O, SL.slo, X.tag(ph_of(pass, l, K_O)));
+                fold(SL.slo, X.tag(ph_of(pass, l, K_O)));
                 norm_pub(Lw.ffn_norm, SL.xnf, K_RNF, X.tag(ph_of(pass, l, K_RNF)));
                 after_rn();
             }
-            // ---- GU: 16 SwiGLU units (rows 32 rt .. +31, gate/up interleaved), every token tile
+            // ---- GU: 32 SwiGLU units (rows 64 rp .. +63, gate/up interleaved in 16-row blocks), tile tt
             if (hg) {
-                wait_flags(X, K_RNF, p.S, [&](int i) { return i; }, X.tag(ph_of(pass, l, K_RNF)));
-                int t0[NT];
-#pragma unroll
-                for (int tt = 0; tt < NT; ++tt) t0[tt] = 32 * tt;
-                f32x16_t acc[NT];
-                mm_tile<4, NT>(X, wb, SL.xnf, H, 0, t0, acc);
-                mm_reduce<NT>(S, acc);
-                if (wave < NT * 2) {   // k_gemm_mfma SWIGLU epilogue: combo (tt, q)
-                    const int tt = wave >> 1, q = wave & 1, r = lane & 31, h = lane >> 5;
+                after_rn();
+                const int rp = w % 96, tt = w / 96;
+                const int nv = min(32, p.S - 32 * tt);
+                wait_flags_wg(X, K_RNF, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNF)));
+                mm_tile<4>(X, SL.xnf, H, 0, 32 * tt);
+                CPROF(ph_of(pass, l, K_GU), 3);
+                {   // k_gemm_mfma SWIGLU epilogue per row tile: wave = (rt, q)
+                    const int rt = wave >> 1, q = wave & 1, r = lane & 31, h = lane >> 5;
                     const int tok = 32 * tt + r;
                     if (tok < p.S) {
-                        const int unit = 16 * w + 8 * q + 4 * h;
+                        const int unit = 32 * rp + 16 * rt + 8 * q + 4 * h;
                         float hv[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4<NT>(S, tt, 4 * q + e)) * sum4<NT>(S, tt, 4 * (q + 2) + e);
+                        for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4(S, rt, 4 * q + e, lane)) * sum4(S, rt, 4 * (q + 2) + e, lane);
                         const u32x2_t o = {(uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16),
                                            (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16)};
                         __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)(SL.h + ((size_t)tok * INTER + unit) * 2), 0, SC1);
@@ -385,16 +486,15 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 publish(X, K_GU, w, X.tag(ph_of(pass, l, K_GU)));
                 after_job();
             }
-            // ---- DN: split-K slab z of rows 32 rt .. +31, tile tt; wave w reads units [768 z + 192 w, +192)
-            if (hd) {
-                const int rt = w % 32, z = (w / 32) % 4, tt = w / 128;
-                wait_flags(X, K_GU, 12, [&](int i) { return 48 * z + 12 * wave + i; }, X.tag(ph_of(pass, l, K_GU)));
-                const int t0[1] = {32 * tt};
-                f32x16_t acc[1];
-                mm_tile<3, 1>(X, wb, SL.h, INTER, 768 * z, t0, acc);
-                mm_reduce<1>(S, acc);
-                epi_f32<1>(X, SL.sld + (size_t)z * SMAX * H * 4, H, 32 * rt, t0);
-                publish(X, K_DN, w, X.tag(ph_of(pass, l, K_DN)));
+            // ---- DN: split-K slab z of rows 64 rp .. +63, tile tt; wave w reads units [768 z + 192 w, +192)
+            if (hq) {
+                after_rn();
+                const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
+                wait_flags_wg(X, K_GU, 24, [&](int i) { return 24 * z + i + 96 * tt; }, X.tag(ph_of(pass, l, K_GU)));
+                mm_tile<3>(X, SL.h, INTER, 768 * z, 32 * tt);
+                CPROF(ph_of(pass, l, K_DN), 3);
+                epi_gran(X, SL.sld + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_DN)));
+                CPROF(ph_of(pass, l, K_DN), 2);
                 after_job();
             }
         }
@@ -407,48 +507,47 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         }
         // ---- final RMSNorm (output_norm) -> lm_head[pass - 1] -> selection of code `pass`
         if (rn) {
-            fold(K_DN, SL.sld, X.tag(ph_of(pass, NLC - 1, K_DN)));
+            fold(SL.sld, X.tag(ph_of(pass, NLC - 1, K_DN)));
             norm_pub(p.out_norm, SL.xna, K_RNA, X.tag(ph_of(pass, NLC, K_RNA)));
             after_rn();
         }
         if (hh) {
-            const int rt = w % 64, tt = w / 64;
+            after_rn();
+            const int rp = w % 32, tt = w / 32;
             const int nv = min(32, p.S - 32 * tt);
-            wait_flags(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, NLC, K_RNA)));
-            const int t0[1] = {32 * tt};
-            f32x16_t acc[1];
-            mm_tile<4, 1>(X, wb, SL.xna, H, 0, t0, acc);
-            mm_reduce<1>(S, acc);
-            // logits into the context's buffer (p.logits, [S][2048]): its own resource
-            {
-                const __amdgpu_buffer_rsrc_t lr = __builtin_amdgcn_make_buffer_rsrc(p.logits, 0, p.S * CPV * 4, BUF_RSRC);
-                const int r = lane & 31, h = lane >> 5;
-                const int q = wave, tok = t0[0] + r;
-                if (tok < p.S) {
-                    const int n0 = 32 * rt + 8 * q + 4 * h;
-                    float v[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = sum4<1>(S, 0, 4 * q + e);
-                    const u32x4_t o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-                    __builtin_amdgcn_raw_buffer_store_b128(o, lr, (tok * CPV + n0) * 4, 0, SC1);
-                }
-            }
-            publish(X, K_HEAD, w, X.tag(ph_of(pass, NLC, K_HEAD)));
+            wait_flags_wg(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, NLC, K_RNA)));
+            mm_tile<4>(X, SL.xna, H, 0, 32 * tt);
+            CPROF(ph_of(pass, NLC, K_HEAD), 3);
+            epi_gran(X, SL.lg, CPV, 64 * rp, 32 * tt, X.tag(ph_of(pass, NLC, K_HEAD)));
+            CPROF(ph_of(pass, NLC, K_HEAD), 2);
             after_job();
         }
-        if (rn) {
-            if (wave == 0) wait_flags(X, K_HEAD, 64, [&](int i) { return i + 64 * btt; }, X.tag(ph_of(pass, NLC, K_HEAD)));
-            __syncthreads();
+        if (slot) {   // both halves select (the same token); the even one commits it
+            const uint32_t tg = X.tag(ph_of(pass, NLC, K_HEAD));
+            CPROF(ph_of(pass, NLC, K_HEAD), 0);
+            u32x4_t lr[4];   // thread t: logits 8t .. 8t+7 (select_token's exact-width ownership, V = 2048)
+            poll_gran<4>(X, tg, lr, [&](u32x4_t (&r)[4]) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    r[k] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, (int)(SL.lg + ((size_t)b * CPV + 8 * t + 2 * k) * 8), 0, SC1V);
+            });
+            CPROF(ph_of(pass, NLC, K_HEAD), 1);
+            float v[SEL_VPT_MAX];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { v[2 * k] = __uint_as_float(lr[k].x); v[2 * k + 1] = __uint_as_float(lr[k].z); }
+#pragma unroll
+            for (int e = 8; e < SEL_VPT_MAX; ++e) v[e] = -INFINITY;
             SelectSpec sp = p.sel;
             sp.step = pass - 1;
-            const int tok = select_token<true>(sp, p.logits + (size_t)b * CPV, b, S.sel);   // -1: slot done
+            const int tok = select_token_regs<SEL_CP>(sp, v, b, S.sel);   // -1: slot done
             if (t == 0 && tok >= 0) {
-                select_commit(sp, b, tok);
+                if (rn) select_commit(sp, b, tok);
                 S.toks[pass] = tok;
             }
             __syncthreads();
             CPROF(ph_of(pass, NLC, K_HEAD), 3);
-            if (pass + 1 < NPASS) {   // the next pass's input: code_pred.codec_embd[pass - 1] row of this token
+            if (!rn) {
+            } else if (pass + 1 < NPASS) {   // the next pass's input: code_pred.codec_embd[pass - 1] row of this token
                 const uint2 u = *reinterpret_cast<const uint2 *>(S.tabs[pass] + (size_t)S.toks[pass] * H + 4 * t);
                 x = make_float4(h2f(u.x & 0xffff), h2f(u.x >> 16), h2f(u.y & 0xffff), h2f(u.y >> 16));
             } else {
@@ -488,6 +587,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
 }
 
 size_t cpb_lds() { return std::max(sizeof(BLds), (size_t)96 * 1024); }   // > 80 KB: one workgroup per CU
+static_assert(sizeof(BLds) <= 160 * 1024, "LDS");
 
 template <int NT>
 bool cpb_attr() {

@@ -33,7 +33,7 @@ def ph(p, l, k):
     return p * 48 + l * 8 + k
 
 
-rows = {k: ([], [], []) for k in range(8)}
+rows = {k: ([], [], [], []) for k in range(8)}
 for p in range(1, 16):
     for l in range(6):
         for k in range(8):
@@ -47,6 +47,7 @@ for p in range(1, 16):
             edge = np.nanmedian(rdy) - last
             nk = NEXT[k]
             span = np.nan
+            comp = np.nan
             if nk is not None:
                 nl = l + 1 if nk == 0 else l
                 if nk == 0 and l == 4:
@@ -55,13 +56,17 @@ for p in range(1, 16):
                 c = ~np.isnan(rdy) & ~np.isnan(T[:, y, 2])
                 if c.any():
                     span = np.nanmedian(T[c, y, 2] - rdy[c])
+                    c3 = c & ~np.isnan(T[:, y, 3])
+                    if c3.any():
+                        comp = np.nanmedian(T[c3, y, 3] - rdy[c3])
             rows[k][0].append(skew)
             rows[k][1].append(edge)
             rows[k][2].append(span)
-print(f"{'hand-off':8s} {'pub skew':>9s} {'edge':>7s} {'consumer body':>14s}   [us, mean over passes 1..15]")
+            rows[k][3].append(comp)
+print(f"{'hand-off':8s} {'pub skew':>9s} {'edge':>7s} {'consumer body':>14s} {'(ready->computed)':>18s}   [us, mean over passes 1..15]")
 for k in range(8):
-    s, e, b = (np.nanmean(v) if len(v) and not np.isnan(v).all() else np.nan for v in rows[k])
-    print(f"{NAMES[k]:8s} {s:9.2f} {e:7.2f} {b:14.2f}")
+    s, e, b, c = (np.nanmean(v) if len(v) and not np.isnan(v).all() else np.nan for v in rows[k])
+    print(f"{NAMES[k]:8s} {s:9.2f} {e:7.2f} {b:14.2f} {c:18.2f}")
 # one pass end to end
 for p in (1, 8):
     a = np.nanmin(T[:, ph(p, 0, 0):ph(p + 1, 0, 0), :]) if p < 15 else np.nan
@@ -70,3 +75,18 @@ for p in (1, 8):
 head = [np.nanmax(T[:, ph(p, 5, 7), 2]) - np.nanmax(T[:, ph(p, 5, 0), 2]) for p in range(1, 16)]
 sel = [np.nanmax(T[:, ph(p, 5, 7), 3]) - np.nanmax(T[:, ph(p, 5, 7), 2]) for p in range(1, 16)]
 print(f"final norm -> head published {np.nanmean(head):.2f} us; head published -> selected {np.nanmean(sel):.2f} us")
+# one layer in detail: per kind, percentiles of data-ready and publish over the workgroups that stamped them, relative
+# to the previous layer's last DN publish, with the workgroup ranges of the slowest publishers
+if len(sys.argv) > 2:
+    p, l = 8, 2
+    base = np.nanmax(T[:, ph(p, l - 1, 6), 2])
+    for k in range(8):
+        x = ph(p, l if k else l, k)
+        for lab, col in (("ready", 1), ("computed", 3), ("publish", 2)):
+            v = T[:, x, col] - base
+            ok = ~np.isnan(v)
+            if not ok.any():
+                continue
+            q = np.percentile(v[ok], [0, 10, 50, 90, 100])
+            slow = np.argsort(np.where(ok, v, -1e9))[-6:][::-1]
+            print(f"{NAMES[k]:5s} {lab:8s} n={ok.sum():3d}  min {q[0]:6.2f} p10 {q[1]:6.2f} p50 {q[2]:6.2f} p90 {q[3]:6.2f} max {q[4]:6.2f}  slowest wg {list(slow)}")
