@@ -129,10 +129,11 @@ __device__ __forceinline__ void attn_small_load_qkv(const float *qkv, int g, int
 
 // One (slot, kv head g) of the code predictor's attention at position pos (< 16), 2 q heads of D = 128, from the cached
 // rows `kv` (attn_small_load_kv) and the raw QKV values `xs` (attn_small_load_qkv).
-//   kc/vc: this (layer, slot, kv head)'s cache [16][D] f16; out: the slot's attention row [nH * D] f16
-template <bool SC1>
+//   kc/vc: this (layer, slot, kv head)'s cache [16][D] f16; dst_of(e): where halves e .. e+3 (e a multiple of 4) of the
+//   slot's attention row [nH * D] f16 go
+template <bool SC1, class Dst>
 __device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float (&xs)[4][2], const AttnSmallAux &aux, int g,
-                                                   int pos, float eps, uint16_t *kc, uint16_t *vc, uint16_t *out,
+                                                   int pos, float eps, uint16_t *kc, uint16_t *vc, Dst dst_of,
                                                    AttnSmallLds &L) {
     using namespace asm_detail;
     constexpr int D = 128, R = 2, NPOS = 16;
@@ -207,7 +208,7 @@ __device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float
     uint2 o;
     o.x = (uint32_t)f2h(acc[0] / l) | ((uint32_t)f2h(acc[1] / l) << 16);
     o.y = (uint32_t)f2h(acc[2] / l) | ((uint32_t)f2h(acc[3] / l) << 16);
-    uint16_t *dst = out + (size_t)(g * R + vh) * D + vd;
+    uint16_t *dst = dst_of((g * R + vh) * D + vd);
     if constexpr (SC1) {
         __hip_atomic_store(reinterpret_cast<uint64_t *>(dst), ((uint64_t)o.y << 32) | o.x, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -226,7 +227,7 @@ __device__ __forceinline__ void attn_small_wave(int g, int pos, int nH, int nKV,
     attn_small_load_qkv<SC1>(qkv, g, nH, nKV, xs);
     AttnSmallAux aux;
     attn_small_load_aux(rope_row, qn, kn, aux);
-    attn_small_compute<SC1>(kv, xs, aux, g, pos, eps, kc, vc, out, L);
+    attn_small_compute<SC1>(kv, xs, aux, g, pos, eps, kc, vc, [&](int e) { return out + e; }, L);
 }
 
 }  // namespace q3t

@@ -49,6 +49,15 @@ constexpr int BUF_RSRC = 0x00020000;   // buffer resource word 3 (gfx9 family)
 constexpr int SC1 = 16;                // buffer instruction cache policy: sc1
 constexpr int SC1V = SC1 | (int)0x80000000u;   // sc1, volatile (a poll's load is re-issued every iteration)
 
+// The f16 activation buffers behind flags (xna, xnf, attn, h) are kept in the MFMA B-fragment order of their consumers:
+// 16-byte chunk k8 (halves 8 k8 .. 8 k8 + 7) of token tok at ((tok / 32 * kch + k8) * 32 + tok % 32) * 16 bytes, kch =
+// K / 8.  A consumer wave's load instruction for chunk column (c, j) then reads two runs of 32 consecutive chunks (whole
+// 64-byte sectors) instead of one 16-byte piece of 64 different sectors: sc1 loads are not merged in L1, so the
+// row-major order moved every activation byte four times over the CU's L2 path.
+__device__ __forceinline__ int fragoff(int kch, int tok, int k) {   // byte offset of half k (k % 4 == 0) of token tok
+    return (((tok >> 5) * kch + (k >> 3)) * 32 + (tok & 31)) * 16 + (k & 7) * 2;
+}
+
 enum Kind { K_RNA = 0, K_QKV = 1, K_ATT = 2, K_O = 3, K_RNF = 4, K_GU = 5, K_DN = 6, K_HEAD = 7 };
 __device__ __forceinline__ int ph_of(int pass, int l, int k) { return pass * 48 + l * 8 + k; }
 
@@ -215,14 +224,14 @@ __device__ __forceinline__ void load_w(BLds &S, const uint16_t *W, int ldw, int 
     }
 }
 
-// B fragments of tokens t0 + r (clamped to the last slot): sc1 loads of the hand-off buffer at byte offset xoff (row
-// stride ldx halves), then the MFMA chains; the K-quarter partials land in the wave's LDS region (its A slots, consumed)
+// B fragments of tokens t0 + r: sc1 loads of the hand-off buffer at byte offset xoff (fragment order, kch chunks per
+// token; the columns of tokens >= S read unwritten chunks and are never stored), then the MFMA chains; the K-quarter
+// partials land in the wave's LDS region (its A slots, consumed)
 template <int NCH>
-__device__ __forceinline__ void mm_tile(Ctx &X, size_t xoff, int ldx, int kbase, int t0) {
+__device__ __forceinline__ void mm_tile(Ctx &X, size_t xoff, int kch, int kbase, int t0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
     u32x4_t xb[4 * NCH];
-    const int tok = min(t0 + r, X.S_ - 1);
-    const int off = (int)(xoff + ((size_t)tok * ldx + kbase + wave * (NCH * 64) + h * 32) * 2);
+    const int off = (int)xoff + fragoff(kch, t0 + r, kbase + wave * (NCH * 64) + h * 32);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -230,7 +239,7 @@ __device__ __forceinline__ void mm_tile(Ctx &X, size_t xoff, int ldx, int kbase,
 #ifdef CPB_EXP_NOX   // timing experiment (development variant builds): no activation loads
             xb[4 * c + j] = u32x4_t{(unsigned)off, 0u, 0u, 0u};
 #else
-            xb[4 * c + j] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, off + (c * 64 + j * 8) * 2, 0, SC1);
+            xb[4 * c + j] = __builtin_amdgcn_raw_buffer_load_b128(X.rs, off + (c * 8 + j) * 512, 0, SC1);
 #endif
         }
     f32x16_t acc[RT];
@@ -356,7 +365,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         const float y0 = (x.x * scale) * wv.x, y1 = (x.y * scale) * wv.y, y2 = (x.z * scale) * wv.z, y3 = (x.w * scale) * wv.w;
         const u32x2_t hv = {(uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16), (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16)};
         CPROF((int)((tg - 1u) & 1023u), 3);
-        __builtin_amdgcn_raw_buffer_store_b64(hv, X.rs, (int)(xo + ((size_t)b * H + 4 * t) * 2), 0, SC1);
+        __builtin_amdgcn_raw_buffer_store_b64(hv, X.rs, (int)xo + fragoff(H / 8, b, 4 * t), 0, SC1);
         publish(X, kind, b, tg);
     };
     // x += the 4 split-K slabs of slot b (k_resid_norm<4> order): thread t polls the 16 granules of its 4 elements
@@ -397,7 +406,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                     const int rp = w % 64, tt = w / 64;
                     const int nv = min(32, p.S - 32 * tt);
                     wait_flags_wg(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNA)));
-                    mm_tile<4>(X, SL.xna, H, 0, 32 * tt);
+                    mm_tile<4>(X, SL.xna, H / 8, 0, 32 * tt);
                     CPROF(ph_of(pass, l, K_QKV), 3);
                     epi_gran(X, SL.qkv, QKVN, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_QKV)));
                     CPROF(ph_of(pass, l, K_QKV), 2);
@@ -434,8 +443,9 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
 #pragma unroll
                     for (int v = 0; v < 4; ++v) { xs[v][0] = __uint_as_float(gq[v].x); xs[v][1] = __uint_as_float(gq[v].z); }
                 }
+                uint16_t *const ab = reinterpret_cast<uint16_t *>(p.state + SL.attn);
                 attn_small_compute<true>(kv, xs, aux, g, pos, p.eps, p.kc + hoff, p.vc + hoff,
-                                         reinterpret_cast<uint16_t *>(p.state + SL.attn) + (size_t)b * NH * D, S.att[wave]);
+                                         [&](int e) { return ab + fragoff(NH * D / 8, b, e) / 2; }, S.att[wave]);
                 CPROF(ph_of(pass, l, K_ATT), 3);
                 if (!(pass == 0 && l == NLC - 1)) publish(X, K_ATT, sw, X.tag(ph_of(pass, l, K_ATT)));
                 else __syncthreads();
@@ -450,7 +460,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 // wave w multiplies heads 4 z + w: kv group (4 z + w) / 2, published by the slots' half (4 z + w) / 8
                 // (wave 0 polls both halves' flags of the slice: 4 z + w for w < 4 spans one half)
                 wait_flags_wg(X, K_ATT, nv, [&](int i) { return 2 * (32 * tt + i) + ((4 * z) >> 3); }, X.tag(ph_of(pass, l, K_ATT)));
-                mm_tile<2>(X, SL.attn, NH * D, 512 * z, 32 * tt);
+                mm_tile<2>(X, SL.attn, NH * D / 8, 512 * z, 32 * tt);
                 CPROF(ph_of(pass, l, K_O), 3);
                 epi_gran(X, SL.slo + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_O)));
                 CPROF(ph_of(pass, l, K_O), 2);
@@ -468,7 +478,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 const int rp = w % 96, tt = w / 96;
                 const int nv = min(32, p.S - 32 * tt);
                 wait_flags_wg(X, K_RNF, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNF)));
-                mm_tile<4>(X, SL.xnf, H, 0, 32 * tt);
+                mm_tile<4>(X, SL.xnf, H / 8, 0, 32 * tt);
                 CPROF(ph_of(pass, l, K_GU), 3);
                 {   // k_gemm_mfma SWIGLU epilogue per row tile: wave = (rt, q)
                     const int rt = wave >> 1, q = wave & 1, r = lane & 31, h = lane >> 5;
@@ -480,7 +490,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                         for (int e = 0; e < 4; ++e) hv[e] = silu_f(sum4(S, rt, 4 * q + e, lane)) * sum4(S, rt, 4 * (q + 2) + e, lane);
                         const u32x2_t o = {(uint32_t)f2h(hv[0]) | ((uint32_t)f2h(hv[1]) << 16),
                                            (uint32_t)f2h(hv[2]) | ((uint32_t)f2h(hv[3]) << 16)};
-                        __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)(SL.h + ((size_t)tok * INTER + unit) * 2), 0, SC1);
+                        __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.h + fragoff(INTER / 8, tok, unit), 0, SC1);
                     }
                 }
                 publish(X, K_GU, w, X.tag(ph_of(pass, l, K_GU)));
@@ -491,7 +501,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 after_rn();
                 const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
                 wait_flags_wg(X, K_GU, 24, [&](int i) { return 24 * z + i + 96 * tt; }, X.tag(ph_of(pass, l, K_GU)));
-                mm_tile<3>(X, SL.h, INTER, 768 * z, 32 * tt);
+                mm_tile<3>(X, SL.h, INTER / 8, 768 * z, 32 * tt);
                 CPROF(ph_of(pass, l, K_DN), 3);
                 epi_gran(X, SL.sld + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_DN)));
                 CPROF(ph_of(pass, l, K_DN), 2);
@@ -516,7 +526,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
             const int rp = w % 32, tt = w / 32;
             const int nv = min(32, p.S - 32 * tt);
             wait_flags_wg(X, K_RNA, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, NLC, K_RNA)));
-            mm_tile<4>(X, SL.xna, H, 0, 32 * tt);
+            mm_tile<4>(X, SL.xna, H / 8, 0, 32 * tt);
             CPROF(ph_of(pass, NLC, K_HEAD), 3);
             epi_gran(X, SL.lg, CPV, 64 * rp, 32 * tt, X.tag(ph_of(pass, NLC, K_HEAD)));
             CPROF(ph_of(pass, NLC, K_HEAD), 2);
