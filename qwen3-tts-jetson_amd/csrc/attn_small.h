@@ -131,10 +131,13 @@ __device__ __forceinline__ void attn_small_load_qkv(const float *qkv, int g, int
 // rows `kv` (attn_small_load_kv) and the raw QKV values `xs` (attn_small_load_qkv).
 //   kc/vc: this (layer, slot, kv head)'s cache [16][D] f16; dst_of(e): where halves e .. e+3 (e a multiple of 4) of the
 //   slot's attention row [nH * D] f16 go
-template <bool SC1, class Dst>
+struct AttnNoStamp {   // development timeline hook of attn_small_compute (persist_cpb.hip stamps)
+    __device__ void operator()(int) const {}
+};
+template <bool SC1, class Dst, class Stamp = AttnNoStamp>
 __device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float (&xs)[4][2], const AttnSmallAux &aux, int g,
                                                    int pos, float eps, uint16_t *kc, uint16_t *vc, Dst dst_of,
-                                                   AttnSmallLds &L) {
+                                                   AttnSmallLds &L, Stamp stamp = Stamp()) {
     using namespace asm_detail;
     constexpr int D = 128, R = 2, NPOS = 16;
     const int lane = threadIdx.x & 63;
@@ -164,7 +167,9 @@ __device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float
     }
     L.vh_s[lane] = f2h(xs[R + 1][0]);
     L.vh_s[lane + 64] = f2h(xs[R + 1][1]);
+    stamp(0);
     lds_fence<SC1>();
+    stamp(1);
     kc[(size_t)pos * D + lane] = L.kh_s[lane];
     kc[(size_t)pos * D + lane + 64] = L.kh_s[lane + 64];
     vc[(size_t)pos * D + lane] = L.vh_s[lane];
@@ -190,7 +195,9 @@ __device__ __forceinline__ void attn_small_compute(AttnSmallKV &kvr, const float
     const float lsum = group_sum<32>(sk == 0 ? pv : 0.0f);
     if (sk == 0) L.pr_s[sh][sj] = pv;
     if ((lane & 31) == 0) L.l_s[sh] = lsum;
+    stamp(2);
     lds_fence<SC1>();
+    stamp(3);
     // P.V: the new row from LDS
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll

@@ -206,6 +206,8 @@ __device__ __forceinline__ void poll_gran(Ctx &X, uint32_t tag, u32x4_t (&r)[M],
 // lane (r = lane & 31, h = lane >> 5), k = kq + 64c + 32h + 8j, wave w owning the K quarter kq = kbase + 64 NCH w, the
 // MFMA chain in (c, j) order, the 4 quarters summed through LDS in wave order.
 constexpr int RT = 2;
+constexpr int RS = 68;   // row stride (floats) of the K-quarter partial tiles in LDS: the epilogue's 16-byte token-quad
+                         // reads then fall on all 64 banks
 template <int NCH>
 __device__ __forceinline__ void load_w(BLds &S, const uint16_t *W, int ldw, int row0, int kbase) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
@@ -263,33 +265,46 @@ __device__ __forceinline__ void mm_tile(Ctx &X, size_t xoff, int kch, int kbase,
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) red[(rt * 16 + i) * 64 + lane] = acc[rt][i];
+        for (int i = 0; i < 16; ++i) red[(rt * 16 + i) * RS + lane] = acc[rt][i];
     __syncthreads();
 }
 // register i of row tile rt, lane `src`, summed over the 4 K quarters in wave order (k_gemm_mfma sum4)
 __device__ __forceinline__ float sum4(const BLds &S, int rt, int i, int src) {
     float v = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) v += reinterpret_cast<const float *>(&S.wl[w][0][0])[(rt * 16 + i) * 64 + src];
+    for (int w = 0; w < 4; ++w) v += reinterpret_cast<const float *>(&S.wl[w][0][0])[(rt * 16 + i) * RS + src];
     return v;
 }
 
 // granule epilogue (QKV rows, split-K slabs, lm_head logits): {f32, tag} granules out[tok][row0 ..] with 8-byte sc1
-// stores (MI355X_MICROARCH.md handoff-1to1: the payload carries its own tag, no drain and no flag).  Thread t takes token
-// t / 8 and, for store k, row 8k + t % 8 of each row tile: each store instruction writes 64 contiguous bytes per token
-// (whole lines over four stores).  Register i of lane (r, h) = tile row (i & 3) + 8 (i >> 2) + 4h, token r.
+// stores (MI355X_MICROARCH.md handoff-1to1: the payload carries its own tag, no drain and no flag).  Thread t takes job
+// row rho = t % 64 and the token quads 4 (t / 64) and 4 (t / 64) + 16: per wave 16-byte LDS reads of four tokens (8
+// reads instead of 32 scalar ones: the epilogue is latency-bound at one wave per SIMD), and every store instruction
+// writes 64 consecutive rows of one token (512 contiguous bytes).  Register i of lane (r, h) holds tile row
+// (i & 3) + 8 (i >> 2) + 4h of token r, so row rr of a tile is register (rr & 3) + 4 (rr >> 3) of half (rr >> 2) & 1.
 __device__ __forceinline__ void epi_gran(Ctx &X, size_t obase, int ldo, int row0, int t0, uint32_t tag) {
-    const int t = threadIdx.x, tl = t >> 3, c = t & 7;
-    const int tok = t0 + tl;
-    if (tok < X.S_) {
+    const int t = threadIdx.x, rho = t & 63, tq = t >> 6;
+    const int rt = rho >> 5, rr = rho & 31;
+    const int src4 = ((rt * 16 + (rr & 3) + 4 * (rr >> 3)) * RS + 32 * ((rr >> 2) & 1)) / 4 + tq;   // 16-byte units
+    uint4 q[2][4];   // all eight reads first (one LDS round trip), then the sums
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+    for (int hq = 0; hq < 2; ++hq)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float v = sum4(X.S, rt, (c & 3) + 4 * k, tl + 32 * ((c >> 2) & 1));
-                const u32x2_t g = {__float_as_uint(v), tag};
-                __builtin_amdgcn_raw_buffer_store_b64(g, X.rs, (int)(obase + ((size_t)tok * ldo + row0 + 32 * rt + 8 * k + c) * 8), 0, SC1);
-            }
+        for (int w = 0; w < 4; ++w) q[hq][w] = (&X.S.wl[w][0][0])[src4 + 4 * hq];
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {
+        const int r0 = 4 * tq + 16 * hq;
+        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // k_gemm_mfma sum4: ((0 + q0) + q1) + q2) + q3
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            v[0] += __uint_as_float(q[hq][w].x); v[1] += __uint_as_float(q[hq][w].y);
+            v[2] += __uint_as_float(q[hq][w].z); v[3] += __uint_as_float(q[hq][w].w);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // tokens S .. 63 too (rows of the SMAX-row buffer nobody reads): no branches
+            const u32x2_t g = {__float_as_uint(v[u]), tag};
+            __builtin_amdgcn_raw_buffer_store_b64(g, X.rs, (int)(obase + ((size_t)(t0 + r0 + u) * ldo + row0 + rho) * 8), 0, SC1);
+        }
     }
     __syncthreads();   // the LDS region is the next job's DMA target
 }
@@ -347,8 +362,9 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         }
     };
     auto next_job = [&]() { advance(); issue(); };
-    // a slot workgroup issues the next job's weights after its next slot step (whose loads then go first), at the latest
-    // when that job starts
+    // a slot workgroup issues the next job's weights after its next attention (the polls of the norm and attention steps
+    // before it then do not queue behind 128 KB of weight DMA; O and the final norm follow with no slot work of this
+    // workgroup), at the latest when that job starts
     bool pending = false;
     auto after_job = [&]() { if (slot) pending = true; else next_job(); };
     auto after_rn = [&]() { if (pending) { next_job(); pending = false; } };
@@ -398,7 +414,6 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                     if (pass == 0 && l == 0) x = ldf4(p.x_in + (size_t)b * H + 4 * t);
                     else fold(SL.sld, X.tag(ph_of(pass, l - 1, K_DN)));
                     norm_pub(Lw.attn_norm, SL.xna, K_RNA, X.tag(ph_of(pass, l, K_RNA)));
-                    after_rn();
                 }
                 // ---- QKV: rows 64 rp .. +63 of tile tt -> granules
                 if (hq) {
@@ -445,7 +460,11 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 }
                 uint16_t *const ab = reinterpret_cast<uint16_t *>(p.state + SL.attn);
                 attn_small_compute<true>(kv, xs, aux, g, pos, p.eps, p.kc + hoff, p.vc + hoff,
-                                         [&](int e) { return ab + fragoff(NH * D / 8, b, e) / 2; }, S.att[wave]);
+                                         [&](int e) { return ab + fragoff(NH * D / 8, b, e) / 2; }, S.att[wave]
+#ifdef CPB_ATT_STAMPS   // development: stamps inside the attention, phases (pass, 5, 1 + l), column k
+                                         , [&](int k) { CPROF(pass * 48 + 41 + l, k); }
+#endif
+                );
                 CPROF(ph_of(pass, l, K_ATT), 3);
                 if (!(pass == 0 && l == NLC - 1)) publish(X, K_ATT, sw, X.tag(ph_of(pass, l, K_ATT)));
                 else __syncthreads();
@@ -470,7 +489,6 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
             if (rn) {
                 fold(SL.slo, X.tag(ph_of(pass, l, K_O)));
                 norm_pub(Lw.ffn_norm, SL.xnf, K_RNF, X.tag(ph_of(pass, l, K_RNF)));
-                after_rn();
             }
             // ---- GU: 32 SwiGLU units (rows 64 rp .. +63, gate/up interleaved in 16-row blocks), tile tt
             if (hg) {
@@ -519,7 +537,6 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         if (rn) {
             fold(SL.sld, X.tag(ph_of(pass, NLC - 1, K_DN)));
             norm_pub(p.out_norm, SL.xna, K_RNA, X.tag(ph_of(pass, NLC, K_RNA)));
-            after_rn();
         }
         if (hh) {
             after_rn();
@@ -591,7 +608,6 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                 if (b == 0 && t == 0)   // every workgroup has read seq: each one's first job fed this last selection
                     __hip_atomic_store(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            after_rn();
         }
     }
 }

@@ -82,25 +82,29 @@ __device__ __forceinline__ void g_wait(const uint64_t *base, uint32_t tag, uint3
 
 // ---------------------------------------------------------------- 16-byte poll loads
 // Two granules per global_load_dwordx4 sc1 (each 8-byte half was written by ONE 8-byte sc1 store and is checked against
-// its own tag, so a pair torn between its halves only costs another poll).  The compiler does not model these inline
-// asm loads: every load is issued, then ONE s_waitcnt vmcnt(0) that names all destinations as in-out operands, so no
-// destination register is read or reused before the wait.  (Q3T_POLL16=0: the 8-byte atomic loads of g_wait.)
+// its own tag, so a pair torn between its halves only costs another poll).  The M loads of one poll and their
+// s_waitcnt vmcnt(0) are ONE asm statement: the compiler cannot place a read or a copy of a destination register between
+// a load and its wait, whatever the register pressure.  (Q3T_POLL16=0: the 8-byte atomic loads of g_wait.)
 #ifndef Q3T_POLL16
 #define Q3T_POLL16 1
 #endif
-__device__ __forceinline__ void ld16_sc1_issue(const uint64_t *p, u32x4_t &r) {
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=&v"(r) : "v"(p) : "memory");
-}
 template <int M>
-__device__ __forceinline__ void ld16_sc1_wait(u32x4_t (&r)[M]) {
-    if constexpr (M == 1) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]) : : "memory");
-    else if constexpr (M == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]) : : "memory");
-    else if constexpr (M == 3) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]) : : "memory");
-    else if constexpr (M == 4) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]) : : "memory");
-    else if constexpr (M == 5) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]) : : "memory");
-    else if constexpr (M == 6) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]) : : "memory");
-    else if constexpr (M == 8) asm volatile("s_waitcnt vmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) : : "memory");
-    else static_assert(M == 0, "ld16_sc1_wait: unsupported count");
+__device__ __forceinline__ void ld16_sc1_batch(const uint64_t *const (&a)[M], u32x4_t (&r)[M]) {
+    if constexpr (M == 1)
+        asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]) : "v"(a[0]) : "memory");
+    else if constexpr (M == 2)
+        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\tglobal_load_dwordx4 %1, %3, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]) : "v"(a[0]), "v"(a[1]) : "memory");
+    else if constexpr (M == 3)
+        asm volatile("global_load_dwordx4 %0, %3, off sc1\n\tglobal_load_dwordx4 %1, %4, off sc1\n\tglobal_load_dwordx4 %2, %5, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]) : "v"(a[0]), "v"(a[1]), "v"(a[2]) : "memory");
+    else if constexpr (M == 4)
+        asm volatile("global_load_dwordx4 %0, %4, off sc1\n\tglobal_load_dwordx4 %1, %5, off sc1\n\tglobal_load_dwordx4 %2, %6, off sc1\n\tglobal_load_dwordx4 %3, %7, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]) : "memory");
+    else if constexpr (M == 5)
+        asm volatile("global_load_dwordx4 %0, %5, off sc1\n\tglobal_load_dwordx4 %1, %6, off sc1\n\tglobal_load_dwordx4 %2, %7, off sc1\n\tglobal_load_dwordx4 %3, %8, off sc1\n\tglobal_load_dwordx4 %4, %9, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]) : "memory");
+    else if constexpr (M == 6)
+        asm volatile("global_load_dwordx4 %0, %6, off sc1\n\tglobal_load_dwordx4 %1, %7, off sc1\n\tglobal_load_dwordx4 %2, %8, off sc1\n\tglobal_load_dwordx4 %3, %9, off sc1\n\tglobal_load_dwordx4 %4, %10, off sc1\n\tglobal_load_dwordx4 %5, %11, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]) : "memory");
+    else if constexpr (M == 8)
+        asm volatile("global_load_dwordx4 %0, %8, off sc1\n\tglobal_load_dwordx4 %1, %9, off sc1\n\tglobal_load_dwordx4 %2, %10, off sc1\n\tglobal_load_dwordx4 %3, %11, off sc1\n\tglobal_load_dwordx4 %4, %12, off sc1\n\tglobal_load_dwordx4 %5, %13, off sc1\n\tglobal_load_dwordx4 %6, %14, off sc1\n\tglobal_load_dwordx4 %7, %15, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]) : "memory");
+    else static_assert(M == 0, "ld16_sc1_batch: unsupported count");
 }
 // g_wait over RUNS runs of RUN contiguous granules (RUN even, 16-B aligned), run k at base + k * STRIDE
 template <int RUNS, int RUN, int STRIDE = 0>
@@ -110,11 +114,12 @@ __device__ __forceinline__ void g_wait16(const uint64_t *base, uint32_t tag, uin
     u32x4_t r[M];
     unsigned it = 0;
     while (true) {
+        const uint64_t *a[M];
 #pragma unroll
         for (int k = 0; k < RUNS; ++k)
 #pragma unroll
-            for (int j = 0; j < RUN / 2; ++j) ld16_sc1_issue(base + k * STRIDE + 2 * j, r[k * (RUN / 2) + j]);
-        ld16_sc1_wait<M>(r);
+            for (int j = 0; j < RUN / 2; ++j) a[k * (RUN / 2) + j] = base + k * STRIDE + 2 * j;
+        ld16_sc1_batch<M>(a, r);
         bool ok = true;
 #pragma unroll
         for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;
@@ -144,11 +149,12 @@ __device__ __forceinline__ void g_wait16_pair(const uint64_t *a, const uint64_t 
     u32x4_t r[M];
     unsigned it = 0;
     while (true) {
+        const uint64_t *ad[M];
 #pragma unroll
-        for (int j = 0; j < N / 2; ++j) ld16_sc1_issue(a + 2 * j, r[j]);
+        for (int j = 0; j < N / 2; ++j) ad[j] = a + 2 * j;
 #pragma unroll
-        for (int j = 0; j < M2 / 2; ++j) ld16_sc1_issue(b + 2 * j, r[N / 2 + j]);
-        ld16_sc1_wait<M>(r);
+        for (int j = 0; j < M2 / 2; ++j) ad[N / 2 + j] = b + 2 * j;
+        ld16_sc1_batch<M>(ad, r);
         bool ok = true;
 #pragma unroll
         for (int m = 0; m < M; ++m) ok &= r[m].y == tag && r[m].w == tag;

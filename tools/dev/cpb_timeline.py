@@ -90,3 +90,17 @@ if len(sys.argv) > 2:
             q = np.percentile(v[ok], [0, 10, 50, 90, 100])
             slow = np.argsort(np.where(ok, v, -1e9))[-6:][::-1]
             print(f"{NAMES[k]:5s} {lab:8s} n={ok.sum():3d}  min {q[0]:6.2f} p10 {q[1]:6.2f} p50 {q[2]:6.2f} p90 {q[3]:6.2f} max {q[4]:6.2f}  slowest wg {list(slow)}")
+# attention detail (variant build with -DCPB_ATT_STAMPS): wave 0 of every slot workgroup, per layer l >= 1, deltas between
+# the QKV data ready, the stamps inside attn_small_compute (0: before the 1st LDS fence, 1: after it, 2: before the 2nd,
+# 3: after it) and computed
+if os.environ.get("Q3T_DEV_LIB", "1") != "1":
+    d = {k: [] for k in ("ready->s0", "s0->s1", "s1->s2", "s2->s3", "s3->computed")}
+    for p in range(1, 16):
+        for l in range(1, 5):
+            rdy = T[128:, ph(p, l, 1), 1]
+            st = [T[128:, p * 48 + 41 + l, k] for k in range(4)]
+            cmp_ = T[128:, ph(p, l, 2), 3]
+            seq = [rdy] + st + [cmp_]
+            for (k, a, b_) in zip(d.keys(), seq[:-1], seq[1:]):
+                d[k].append(np.nanmedian(b_ - a))
+    print("attention (slot workgroups, median):", "  ".join(f"{k} {np.nanmean(v):.2f}" for k, v in d.items()), "us")
