@@ -10,6 +10,7 @@
 // add; the last adder loads the partials with sc1 loads) -- no combine launch, no release/acquire cache flushes.
 #include "kernels.h"
 #include "attn_small.h"
+#include "attn_seq.h"
 
 #include <type_traits>
 
@@ -320,179 +321,22 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 #endif
 template <int D, int R>
 __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnParams p) {
-    constexpr int LPP = D / 8, NP = 4;       // 16 lanes per position, 4 passes of 16 positions per 64-chunk
-    static_assert(LPP == 16, "D = 128");
-    const int slot = blockIdx.x, g = blockIdx.y;
+    static_assert(D == 128 && R == 2, "talker heads: D 128, 2 q heads per kv head (attn_seq.h)");
+    __shared__ AttnSeqLds L;
+    const int slot = blockIdx.x, g = blockIdx.y, lane = threadIdx.x & 63;
     const int pos = p.pos[slot];
-    const int nch = pos / 64 + 1;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
-    __shared__ float q_s[R][D];
-    __shared__ __attribute__((aligned(16))) uint16_t kh_s[D], vh_s[D];
-    __shared__ float wm[4][R], wl[4][R];
-    __shared__ float wa[4][R][D];
-
     const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
-    uint4 ka[NP], va[NP], kb[NP], vb[NP];
-    auto issue = [&](int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            const int j = min(c * 64 + pi * 16 + pg, pos);
-            kr[pi] = ldg16(p.kc + head_off + (size_t)j * D + li * 8);
-            vr[pi] = ldg16(p.vc + head_off + (size_t)j * D + li * 8);
-        }
-    };
-    issue(0, ka, va);
-
-    // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded
-    const int QKV = (p.nH + 2 * p.nKV) * D;
-    const float *qkv = p.qkv + (size_t)slot * QKV;
-    const float *rope = p.rope + (size_t)pos * D;
-    for (int v = wave; v < R + 2; v += 4) {
-        if (v == R + 1) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) vh_s[lane + 64 * e] = f2h(qkv[(size_t)(p.nH + p.nKV + g) * D + lane + 64 * e]);
-            continue;
-        }
-        const bool isk = v == R;
-        const float *src = isk ? qkv + (size_t)(p.nH + g) * D : qkv + (size_t)(g * R + v) * D;
-        const float *w = isk ? p.kn : p.qn;
-        float x[2];
-        double ss = 0.0;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) { x[e] = src[lane + 64 * e]; ss += (double)__fmul_rn(x[e], x[e]); }
-        ss = wave_sum_d(ss);
-        const float scale = 1.0f / sqrtf((float)(ss / D) + p.eps);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
-        const float c = rope[2 * lane], s = rope[2 * lane + 1];
-        const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
-        const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
-        if (isk) {
-            kh_s[lane] = f2h(y0);
-            kh_s[lane + 64] = f2h(y1);
-        } else {
-            q_s[v][lane] = f16r(y0);
-            q_s[v][lane + 64] = f16r(y1);
-        }
-    }
-    __syncthreads();
-    for (int e = t; e < D; e += 256) {   // KV append at pos
-        p.kc[head_off + (size_t)pos * D + e] = kh_s[e];
-        p.vc[head_off + (size_t)pos * D + e] = vh_s[e];
-    }
-    const float kq_scale = 1.0f / sqrtf((float)D);
-    // q is f16-exact (f16r above): the scores are v_dot2_f32_f16 over f16 pairs straight from the K registers (no
-    // per-element conversion; f16 products are exact in f32)
-    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-    h2_t q2[R][4];
-#pragma unroll
-    for (int h = 0; h < R; ++h)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            q2[h][e].x = (_Float16)q_s[h][li * 8 + 2 * e];
-            q2[h][e].y = (_Float16)q_s[h][li * 8 + 2 * e + 1];
-        }
-
-    float m[R], l[R], acc[R][8];
-#pragma unroll
-    for (int h = 0; h < R; ++h) {
-        m[h] = -INFINITY;
-        l[h] = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
-    }
-    // one chunk; LAST: positions past pos masked, a wave may hold no live position yet
-    auto chunk = [&](auto last_tag, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
-        constexpr bool LAST = decltype(last_tag)::value;
-        float sc[NP][R];
-        bool ok[NP];
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            ok[pi] = !LAST || c * 64 + pi * 16 + pg <= pos;
-            const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
-#pragma unroll
-            for (int h = 0; h < R; ++h) {
-                float s = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kw[e]), q2[h][e], s, false);
-                s = group_sum<LPP>(s);
-                sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
-            }
-        }
-#pragma unroll
-        for (int h = 0; h < R; ++h) {
-            float mc = sc[0][h];
-#pragma unroll
-            for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
-            mc = rows_max(mc);                      // this wave's 16 positions of the chunk
-            const float mn = fmaxf(m[h], mc);
-            if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
-            const float alpha = __expf(__fsub_rn(m[h], mn));
-            l[h] *= alpha;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[h][e] *= alpha;
-            m[h] = mn;
-        }
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            float v8[8];
-            unpack8_cvt(vr[pi], v8);
-#pragma unroll
-            for (int h = 0; h < R; ++h) {
-                const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
-                l[h] += pr;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, acc[h][e]);
-            }
-        }
-    };
-    // the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
-    auto patch = [&](uint4 (&kr)[NP], uint4 (&vr)[NP]) {
-        if (pg == (pos & 15)) {
-            const uint4 kn = *reinterpret_cast<const uint4 *>(&kh_s[li * 8]);
-            const uint4 vn = *reinterpret_cast<const uint4 *>(&vh_s[li * 8]);
-#pragma unroll
-            for (int pi = 0; pi < NP; ++pi)
-                if (pi == ((pos & 63) >> 4)) { kr[pi] = kn; vr[pi] = vn; }
-        }
-    };
-    using whole = std::integral_constant<bool, false>;
-    using last = std::integral_constant<bool, true>;
-    for (int c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) issue(c + 1, kb, vb);
-        if (c + 1 < nch) chunk(whole{}, c, ka, va);
-        else { patch(ka, va); chunk(last{}, c, ka, va); }
-        if (c + 1 < nch) {
-            if (c + 2 < nch) issue(c + 2, ka, va);
-            if (c + 2 < nch) chunk(whole{}, c + 1, kb, vb);
-            else { patch(kb, vb); chunk(last{}, c + 1, kb, vb); }
-        }
-    }
-    // merge the four waves
-#pragma unroll
-    for (int h = 0; h < R; ++h) {
-        const float ls = rows_sum(l[h]);
-        if (lane == 0) { wm[wave][h] = m[h]; wl[wave][h] = ls; }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float a = rows_sum(acc[h][e]);
-            if (lane < 16) wa[wave][h][li * 8 + e] = a;
-        }
-    }
-    __syncthreads();
-    for (int o = t; o < R * D; o += 256) {
-        const int h = o / D, d = o % D;
-        const float M = fmaxf(fmaxf(wm[0][h], wm[1][h]), fmaxf(wm[2][h], wm[3][h]));
-        float num = 0.0f, den = 0.0f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            if (wm[w][h] == -INFINITY) continue;
-            const float f = expf(__fsub_rn(wm[w][h], M));
-            num = __fmaf_rn(wa[w][h][d], f, num);
-            den = __fmaf_rn(wl[w][h], f, den);
-        }
-        p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(num / den);
-    }
+    const float *qkv = p.qkv + (size_t)slot * (p.nH + 2 * p.nKV) * D;
+    attn_seq_wg<false>(
+        pos, p.kc + head_off, p.vc + head_off, p.rope + (size_t)pos * D, p.qn, p.kn, p.eps,
+        [&](int v, float (&x)[2]) {
+            const float *src = v == R + 1 ? qkv + (size_t)(p.nH + p.nKV + g) * D
+                             : v == R     ? qkv + (size_t)(p.nH + g) * D
+                                          : qkv + (size_t)(g * R + v) * D;
+            x[0] = src[lane];
+            x[1] = src[lane + 64];
+        },
+        [&](int h, int d, float y) { p.out[(size_t)slot * p.nH * D + (size_t)(g * R + h) * D + d] = f2h(y); }, L);
 }
 
 

@@ -1,0 +1,228 @@
+// attn_seq.h — decode attention of ONE (slot, kv head) on ONE 256-thread workgroup walking the whole context
+// (src/tts_transformer.cpp:1410-1475: head RMSNorm over 128 lanes, NEOX RoPE at pos, F16 KV append, softmax with scale
+// 1/sqrt(D), GQA: 2 q heads per kv head).  Shared source of k_attn_seq (attn.hip, one launch per layer at >= 16 slots)
+// and the persistent batched talker step (persist_tkb.hip), so both compute the same bits.
+//
+// The workgroup walks its context in 64-position chunks with the next chunk's K/V loads in flight (register double
+// buffer); each wave keeps its own online-softmax state (max, sum, 8-dim accumulator per head) over its 16 positions of
+// every chunk, so no barrier is taken per chunk; the four waves merge once at the end.  Scores are v_dot2_f32_f16 on the
+// packed K registers against the f16-exact q, exponentials v_exp_f32 (__expf); every chunk but the last is whole (all
+// 64 positions <= pos: no masks), and the new K/V row (pos) is patched into the last chunk's registers from LDS.
+//
+// The caller supplies the raw QKV values (qkv_of: wave v < 2 q head 2g + v, v = 2 the new k, v = 3 the new v; lanes
+// lane and lane + 64) -- K/V chunk 0 is in flight before it is called -- and the output store (out: one value, or with
+// VEC4 four consecutive dims of threads 0..63; the per-dim arithmetic does not depend on the thread that runs it).
+#pragma once
+#include "kernels.h"
+
+#include <type_traits>
+
+#pragma clang fp contract(off)   // every rounding as written (both includers compile with contraction off too)
+
+namespace q3t {
+
+struct AttnSeqLds {
+    float q_s[2][128];
+    alignas(16) uint16_t kh_s[128];
+    alignas(16) uint16_t vh_s[128];
+    float wm[4][2], wl[4][2];
+    float wa[4][2][128];
+};
+
+namespace aseq {
+typedef unsigned int u32x4_s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(const uint16_t *p) {
+    typedef const __attribute__((address_space(1))) u32x4_s gv;
+    const u32x4_s v = *(gv *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// each converted value materialised: the consumer FMA may not absorb the conversion into a v_fma_mix_f32 (whose f16
+// operands do not go through v_cvt_f32_f16: whole chunks then differed from the masked last chunk)
+__device__ __forceinline__ void unpack8_cvt(const uint4 u, float (&f)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { f[2 * e] = opaque(h2f(w[e] & 0xffff)); f[2 * e + 1] = opaque(h2f(w[e] >> 16)); }
+}
+}  // namespace aseq
+
+//   kc/vc: this (layer, slot, kv head)'s cache [n_ctx][128] f16 (row pos is written here); rope_row: rope + pos * 128
+template <bool VEC4, class QkvOf, class Out>
+__device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc, const float *rope_row, const float *qn,
+                                            const float *kn, float eps, QkvOf qkv_of, Out out, AttnSeqLds &L) {
+    using namespace aseq;
+    constexpr int D = 128, R = 2, LPP = D / 8, NP = 4;   // 16 lanes per position, 4 passes of 16 positions per 64-chunk
+    const int nch = pos / 64 + 1;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
+
+    uint4 ka[NP], va[NP], kb[NP], vb[NP];
+    auto issue = [&](int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            const int j = min(c * 64 + pi * 16 + pg, pos);
+            kr[pi] = ld16(kc + (size_t)j * D + li * 8);
+            vr[pi] = ld16(vc + (size_t)j * D + li * 8);
+        }
+    };
+    issue(0, ka, va);
+
+    // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded
+    {
+        const int v = wave;
+        float x[2];
+        qkv_of(v, x);
+        if (v == R + 1) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) L.vh_s[lane + 64 * e] = f2h(x[e]);
+        } else {
+            const bool isk = v == R;
+            const float *w = isk ? kn : qn;
+            double ss = 0.0;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) ss += (double)__fmul_rn(x[e], x[e]);
+            ss = wave_sum_d(ss);
+            const float scale = 1.0f / sqrtf((float)(ss / D) + eps);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+            const float c = rope_row[2 * lane], s = rope_row[2 * lane + 1];
+            const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
+            const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
+            if (isk) {
+                L.kh_s[lane] = f2h(y0);
+                L.kh_s[lane + 64] = f2h(y1);
+            } else {
+                L.q_s[v][lane] = f16r(y0);
+                L.q_s[v][lane + 64] = f16r(y1);
+            }
+        }
+    }
+    __syncthreads();
+    if (t < D) {   // KV append at pos
+        kc[(size_t)pos * D + t] = L.kh_s[t];
+        vc[(size_t)pos * D + t] = L.vh_s[t];
+    }
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    // q is f16-exact (f16r above): the scores are v_dot2_f32_f16 over f16 pairs straight from the K registers (no
+    // per-element conversion; f16 products are exact in f32)
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    h2_t q2[R][4];
+#pragma unroll
+    for (int h = 0; h < R; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            q2[h][e].x = (_Float16)L.q_s[h][li * 8 + 2 * e];
+            q2[h][e].y = (_Float16)L.q_s[h][li * 8 + 2 * e + 1];
+        }
+
+    float m[R], l[R], acc[R][8];
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        m[h] = -INFINITY;
+        l[h] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
+    }
+    // one chunk; LAST: positions past pos masked, a wave may hold no live position yet
+    auto chunk = [&](auto last_tag, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
+        constexpr bool LAST = decltype(last_tag)::value;
+        float sc[NP][R];
+        bool ok[NP];
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            ok[pi] = !LAST || c * 64 + pi * 16 + pg <= pos;
+            const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                float s = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kw[e]), q2[h][e], s, false);
+                s = group_sum<LPP>(s);
+                sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            float mc = sc[0][h];
+#pragma unroll
+            for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
+            mc = rows_max(mc);                      // this wave's 16 positions of the chunk
+            const float mn = fmaxf(m[h], mc);
+            if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
+            const float alpha = __expf(__fsub_rn(m[h], mn));
+            l[h] *= alpha;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[h][e] *= alpha;
+            m[h] = mn;
+        }
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) {
+            float v8[8];
+            unpack8_cvt(vr[pi], v8);
+#pragma unroll
+            for (int h = 0; h < R; ++h) {
+                const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
+                l[h] += pr;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, acc[h][e]);
+            }
+        }
+    };
+    // the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
+    auto patch = [&](uint4 (&kr)[NP], uint4 (&vr)[NP]) {
+        if (pg == (pos & 15)) {
+            const uint4 kn4 = *reinterpret_cast<const uint4 *>(&L.kh_s[li * 8]);
+            const uint4 vn4 = *reinterpret_cast<const uint4 *>(&L.vh_s[li * 8]);
+#pragma unroll
+            for (int pi = 0; pi < NP; ++pi)
+                if (pi == ((pos & 63) >> 4)) { kr[pi] = kn4; vr[pi] = vn4; }
+        }
+    };
+    using whole = std::integral_constant<bool, false>;
+    using last = std::integral_constant<bool, true>;
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) issue(c + 1, kb, vb);
+        if (c + 1 < nch) chunk(whole{}, c, ka, va);
+        else { patch(ka, va); chunk(last{}, c, ka, va); }
+        if (c + 1 < nch) {
+            if (c + 2 < nch) issue(c + 2, ka, va);
+            if (c + 2 < nch) chunk(whole{}, c + 1, kb, vb);
+            else { patch(kb, vb); chunk(last{}, c + 1, kb, vb); }
+        }
+    }
+    // merge the four waves
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const float ls = rows_sum(l[h]);
+        if (lane == 0) { L.wm[wave][h] = m[h]; L.wl[wave][h] = ls; }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float a = rows_sum(acc[h][e]);
+            if (lane < 16) L.wa[wave][h][li * 8 + e] = a;
+        }
+    }
+    __syncthreads();
+    auto merged = [&](int h, int d) {
+        const float M = fmaxf(fmaxf(L.wm[0][h], L.wm[1][h]), fmaxf(L.wm[2][h], L.wm[3][h]));
+        float num = 0.0f, den = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            if (L.wm[w][h] == -INFINITY) continue;
+            const float f = expf(__fsub_rn(L.wm[w][h], M));
+            num = __fmaf_rn(L.wa[w][h][d], f, num);
+            den = __fmaf_rn(L.wl[w][h], f, den);
+        }
+        return num / den;
+    };
+    if constexpr (VEC4) {
+        if (t < 64) {
+            const int h = t >> 5, d0 = (t & 31) * 4;
+            float y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = merged(h, d0 + e);
+            out(h, d0, y);
+        }
+    } else {
+        for (int o = t; o < R * D; o += 256) out(o / D, o % D, merged(o / D, o % D));
+    }
+}
+
+}  // namespace q3t

@@ -95,6 +95,7 @@ Options Options::from_env() {
     o.fold_advance = env_flag("Q3T_FOLD_ADVANCE", true);
     o.tk_roles = env_flag("Q3T_TK_ROLES", true);
     o.cpb = env_flag("Q3T_PERSIST_CPB", true);
+    o.tkb = env_flag("Q3T_PERSIST_TKB", true);
     o.fused_select = env_flag("Q3T_FUSED_SELECT", true);
     o.defer_cp_select = env_flag("Q3T_CP_DEFER_SELECT", true);
     o.attn_split = env_flag("Q3T_ATTN_SPLIT", false);
@@ -256,6 +257,7 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
 #endif
     if (!setup_persist()) return false;
     if (!setup_cpb()) return false;
+    if (!setup_tkb()) return false;
     if (!tok_gguf.empty()) {
         voc_.reset(new Vocoder());
         if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
@@ -558,6 +560,37 @@ bool Engine::setup_cpb() {
     }
     return true;
 }
+// the batched talker step (persist_tkb.hip): the 0.6B talker shapes on the matrix-core family, on a device that holds its
+// 256 workgroups at one per CU
+bool Engine::setup_tkb() {
+    int n_cu = 0;
+    Q3T_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device_));
+    tkb_ = opt_.tkb && mm_ok_ && max_slots_ > 1 && !c_.has_mtp && c_.n_layers == 28 && c_.hidden == 1024 &&
+           c_.n_heads == 16 && c_.n_kv == 8 && c_.head_dim == 128 && c_.inter == 3072 && c_.codec_vocab == 3072 &&
+           n_cu >= 256 && tkb_resident(device_);
+    if (!tkb_) return true;
+    tkb_state_ = dalloc<uint8_t>(tkb_state_bytes());
+    if (!tkb_state_) { set_error("device allocation failed"); return false; }
+#ifdef Q3T_DEV
+    if (std::getenv("Q3T_PERSIST_PROF") && !pprof_) pprof_ = dalloc<uint64_t>((size_t)PROF_WG * PROF_PH * 4);
+#endif
+    if (!pl_dev_) {
+        std::vector<PLayerW> pl(L_.size());
+        for (size_t i = 0; i < L_.size(); ++i)
+            pl[i] = PLayerW{L_[i].qkv, L_[i].o, L_[i].gu, L_[i].down, L_[i].attn_norm, L_[i].ffn_norm, L_[i].qn, L_[i].kn};
+        pl_dev_ = dalloc<PLayerW>(pl.size());
+        if (!pl_dev_) { set_error("device allocation failed"); return false; }
+        Q3T_HIP(hipMemcpyAsync(pl_dev_, pl.data(), pl.size() * sizeof(PLayerW), hipMemcpyHostToDevice, stream_));
+        Q3T_HIP(hipStreamSynchronize(stream_));
+    }
+    return true;
+}
+// the slot counts the step serves: the per-op family it reproduces (decoder_stack_mm with k_attn_seq: >= 16 policy
+// slots, no forced split attention; split-K 4 for every S_main of these shapes)
+bool Engine::use_tkb(int S) const {
+    const int S_main = policy_slots_ > 0 ? policy_slots_ : S;
+    return tkb_ && use_mm(S) && S <= 64 && S_main >= 16 && S_main <= 64 && !opt_.attn_split;
+}
 // the slot counts the frame serves: the matrix-core family (decoder_stack_mm) with the split-K of <= 64 slots
 bool Engine::use_cpb(int S) const {
     const int S_main = policy_slots_ > 0 ? policy_slots_ : S;
@@ -751,12 +784,13 @@ bool Engine::persist_recover() {
                     "falling back to the launch-per-op graphs for this context\n", device_);
     if (pstate_) Q3T_HIP(hipMemsetAsync(pstate_, 0, persist_state_bytes(), stream_));   // ordered before the re-run on stream_
     if (cpb_state_ && !cpb_clear(cpb_state_, stream_)) return false;
+    if (tkb_state_ && !tkb_clear(tkb_state_, stream_)) return false;
     Q3T_HIP(hipStreamSynchronize(stream_));
     for (auto &kv : g_talker_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_frame_) hipGraphExecDestroy(kv.second);
     for (auto &kv : g_cp_) hipGraphExecDestroy(kv.second);
     g_talker_.clear(); g_frame_.clear(); g_cp_.clear();
-    persist_ = persist_cp_ = cp_roles_ = tk_roles_ = cpb_ = false;
+    persist_ = persist_cp_ = cp_roles_ = tk_roles_ = cpb_ = tkb_ = false;
     // the tables (serving only the persistent frame) stay allocated until the context is destroyed: a hipFree here
     // would synchronise the device and invalidate graph captures other contexts' threads have in progress
     // the per-op code predictor with its attention as its own launch reproduces the persistent frame bit for bit
@@ -815,6 +849,10 @@ bool Engine::persist_error() {
     if (cpb_ && cpb_state_) {
         bool e = false;
         if (!cpb_error(cpb_state_, stream_, &e) || e) return true;
+    }
+    if (tkb_ && tkb_state_) {
+        bool e = false;
+        if (!tkb_error(tkb_state_, stream_, &e) || e) return true;
     }
     if (!(persist_ || persist_cp_) || !pstate_) return false;
     PersistParams p;
@@ -1088,6 +1126,18 @@ bool Engine::enqueue_talker(int S, hipStream_t s, bool gather_input, bool select
         in0.prenormed = prenormed;
     }
     const bool mm = use_mm(S);   // batched: one selection workgroup per slot after the head
+    if (use_tkb(S)) {   // batched: the whole step as one persistent launch (persist_tkb.hip)
+        if (gather_input && !prenormed && !gather_sum(in0.gs, 16, S, H, x_, H, s)) return false;
+        TkbParams p;
+        p.L = pl_dev_; p.n_layers = c_.n_layers; p.head = codec_head_; p.out_norm = out_norm_;
+        p.x_in = x_; p.hidden = hidden_; p.logits = logits_;
+        p.rope = rope_; p.pos = pos_; p.kc = kc_; p.vc = vc_; p.kv_layer = kv_layer; p.n_ctx = max_ctx_;
+        if (select_next) { p.select = 1; p.sel = select_spec(SEL_CB0, gp_, 1, 0); }
+        p.S = S; p.eps = c_.eps;
+        p.state = tkb_state_;
+        p.prof = pprof_;
+        return persist_talker_batched(p, s);
+    }
     if (mm) {
         if (!decoder_stack_mm(c_, opt_.attn_split, L_, S, x_, xn_, parts_, qkv_, attn_, hmlp_, kc_, vc_, kv_layer, max_ctx_, max_splits, pos_,
                               rope_, part_, ticket_, s, gather_input ? &in0 : nullptr, out_norm_, hidden_, policy_slots_))

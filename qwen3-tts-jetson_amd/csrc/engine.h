@@ -53,6 +53,7 @@ struct PLayerW;
 //   Q3T_PERSIST=0          single-slot talker step as launch-per-phase graphs instead of the persistent kernel
 //   Q3T_PERSIST_CP=0       single-slot code-predictor frame as per-op launches
 //   Q3T_PERSIST_CPB=0      batched (matrix-core) code-predictor frame as per-op launches (persist_cpb.hip otherwise)
+//   Q3T_PERSIST_TKB=0      batched (matrix-core) talker step as per-op launches (persist_tkb.hip otherwise)
 //   Q3T_CP_FUSED_ATTN=0    code-predictor attention as its own launch (the arithmetic the persistent frame reproduces)
 //   Q3T_FUSED_SELECT=0     token selection as standalone launches
 //   Q3T_CP_DEFER_SELECT=0  code-predictor tokens selected in the head launch
@@ -67,6 +68,7 @@ struct Options {
     bool fold_advance = true;   // Q3T_FOLD_ADVANCE: the single-slot role talker kernel advances pos / frame (no k_advance)
     bool tk_roles = true;       // Q3T_TK_ROLES: the 1-slot talker step on role-specialised workgroups (persist_tk.hip)
     bool cpb = true;            // Q3T_PERSIST_CPB: the batched (2..64-slot) code-predictor frame as one persistent launch
+    bool tkb = true;            // Q3T_PERSIST_TKB: the batched (16..64-policy-slot) talker step as one persistent launch
     bool attn_split = false;
     unsigned persist_fault_at = 0;
     int poll_every = 16;   // frames between done-flag polls
@@ -140,13 +142,13 @@ public:
     bool persist_fault_hook(int S, int n_launches);   // Q3T_PERSIST_FAULT_AT test hook (host side)
     unsigned persist_launches_ = 0;
     bool persist_error();
-    bool persist_enabled() const { return persist_ || persist_cp_ || cpb_; }
+    bool persist_enabled() const { return persist_ || persist_cp_ || cpb_ || tkb_; }
     int persist_kernels() const {   // q3t_persist_kernels
-        return (persist_ ? (tk_roles_ ? 1 : 2) : 0) | (persist_cp_ ? (cp_roles_ && cp_qkvtab_ ? 4 : 8) : 0) | (cpb_ ? 16 : 0);
+        return (persist_ ? (tk_roles_ ? 1 : 2) : 0) | (persist_cp_ ? (cp_roles_ && cp_qkvtab_ ? 4 : 8) : 0) | (cpb_ ? 16 : 0) | (tkb_ ? 32 : 0);
     }
     // runs with S slots launch a persistent grid (the 1-slot kernels, or the batched code-predictor frame): they hold the
     // device lock exclusively (devlock.h)
-    bool persist_exclusive(int S) const { return ((persist_ || persist_cp_) && S == 1) || (cpb_ && S > 1); }
+    bool persist_exclusive(int S) const { return ((persist_ || persist_cp_) && S == 1) || ((cpb_ || tkb_) && S > 1); }
     bool persist_fell_back() const { return persist_fallback_; }
 #ifdef Q3T_DEV
     // development hook: copy a device state buffer to the host (0 K cache, 1 V cache, 2 qkv, 3 attention output)
@@ -289,6 +291,10 @@ private:
     uint8_t *cpb_state_ = nullptr;
     bool setup_cpb();
     bool use_cpb(int S) const;
+    bool tkb_ = false;         // the batched talker step runs persist_tkb.hip (use_tkb)
+    uint8_t *tkb_state_ = nullptr;
+    bool setup_tkb();
+    bool use_tkb(int S) const;
     uint8_t *pstate_ = nullptr;
     int *table_iota_ = nullptr;   // 0..codec_vocab-1: the table builds' token ids
     uint64_t *pprof_ = nullptr;   // Q3T_DEV + Q3T_PERSIST_PROF: persistent-step timeline

@@ -132,4 +132,34 @@ bool persist_cp_batched(const CpbParams &p, hipStream_t s);
 bool cpb_error(const uint8_t *state, hipStream_t s, bool *err);   // a hand-off wait gave up
 bool cpb_clear(uint8_t *state, hipStream_t s);   // zero the flags and the error word
 
+// ------------------------------------------------------------------ the batched talker step (persist_tkb.hip)
+// 2..64 slots, 0.6B talker shapes (28 layers), the launch-per-op matrix-core family of >= 16 policy slots (split-K 4,
+// k_attn_seq): the whole step of every slot -- 28 layers, final norm, codec head, CB0 selection -- as one persistent
+// launch, bit-identical to enqueue_talker's decoder_stack_mm + head GEMM + select_tokens
+struct TkbParams {
+    const PLayerW *L = nullptr;                  // device array [28]
+    int n_layers = 0;
+    const uint16_t *head = nullptr;              // codec head [3072][1024]
+    const float *out_norm = nullptr;
+    const float *x_in = nullptr;                 // [S][1024] the step's input rows (the residual stream's start)
+    float *hidden = nullptr;                     // [S][1024] side output: the final-normalised hidden state (f32)
+    float *logits = nullptr;                     // [S][3072] (optional) the head's logits
+    const float *rope = nullptr;
+    const int *pos = nullptr;                    // [S]
+    uint16_t *kc = nullptr, *vc = nullptr;       // [28][slot][8][n_ctx][128] f16
+    size_t kv_layer = 0;
+    int n_ctx = 0;
+    int select = 0;                              // 1: CB0 of the next frame (sel: SEL_CB0, frame_offset 1)
+    SelectSpec sel;
+    int S = 0;
+    float eps = 1e-6f;
+    uint8_t *state = nullptr;                    // tkb_state_bytes(), zeroed once
+    uint64_t *prof = nullptr;                    // development timeline [256][768][4] (null = off)
+};
+size_t tkb_state_bytes();
+bool tkb_resident(int device);                   // both instantiations fit one workgroup per CU, >= 256 CUs
+bool persist_talker_batched(const TkbParams &p, hipStream_t s);
+bool tkb_error(const uint8_t *state, hipStream_t s, bool *err);   // a hand-off wait gave up
+bool tkb_clear(uint8_t *state, hipStream_t s);   // zero the flags and the error word
+
 }  // namespace q3t
