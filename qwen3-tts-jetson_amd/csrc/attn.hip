@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
     const int pos = p.pos[slot];
     const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
     const float *qkv = p.qkv + (size_t)slot * (p.nH + 2 * p.nKV) * D;
-    attn_seq_wg<false>(
+    attn_seq_wg<false, 2>(
         pos, p.kc + head_off, p.vc + head_off, p.rope + (size_t)pos * D, p.qn, p.kn, p.eps,
         [&](int v, float (&x)[2]) {
             const float *src = v == R + 1 ? qkv + (size_t)(p.nH + p.nKV + g) * D

@@ -3,8 +3,9 @@
 // 1/sqrt(D), GQA: 2 q heads per kv head).  Shared source of k_attn_seq (attn.hip, one launch per layer at >= 16 slots)
 // and the persistent batched talker step (persist_tkb.hip), so both compute the same bits.
 //
-// The workgroup walks its context in 64-position chunks with the next chunk's K/V loads in flight (register double
-// buffer); each wave keeps its own online-softmax state (max, sum, 8-dim accumulator per head) over its 16 positions of
+// The workgroup walks its context in 64-position chunks with the next NB - 1 chunks' K/V loads in flight (a register
+// ring of NB chunks: k_attn_seq, two workgroups per CU, NB = 2; the persistent step, one per CU, a deeper ring -- one
+// chunk in flight per CU bounded it at ~20 GB/s per CU); each wave keeps its own online-softmax state (max, sum, 8-dim accumulator per head) over its 16 positions of
 // every chunk, so no barrier is taken per chunk; the four waves merge once at the end.  Scores are v_dot2_f32_f16 on the
 // packed K registers against the f16-exact q, exponentials v_exp_f32 (__expf); every chunk but the last is whole (all
 // 64 positions <= pos: no masks), and the new K/V row (pos) is patched into the last chunk's registers from LDS.
@@ -46,7 +47,7 @@ __device__ __forceinline__ void unpack8_cvt(const uint4 u, float (&f)[8]) {
 }  // namespace aseq
 
 //   kc/vc: this (layer, slot, kv head)'s cache [n_ctx][128] f16 (row pos is written here); rope_row: rope + pos * 128
-template <bool VEC4, class QkvOf, class Out>
+template <bool VEC4, int NB, class QkvOf, class Out>
 __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc, const float *rope_row, const float *qn,
                                             const float *kn, float eps, QkvOf qkv_of, Out out, AttnSeqLds &L) {
     using namespace aseq;
@@ -54,7 +55,8 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
     const int nch = pos / 64 + 1;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
 
-    uint4 ka[NP], va[NP], kb[NP], vb[NP];
+    static_assert(NB >= 2 && NB <= 4, "ring depth");
+    uint4 kq[NB][NP], vq[NB][NP];
     auto issue = [&](int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
 #pragma unroll
         for (int pi = 0; pi < NP; ++pi) {
@@ -63,7 +65,9 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
             vr[pi] = ld16(vc + (size_t)j * D + li * 8);
         }
     };
-    issue(0, ka, va);
+#pragma unroll
+    for (int c = 0; c < NB - 1; ++c)
+        if (c < nch) issue(c, kq[c], vq[c]);
 
     // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded
     {
@@ -178,14 +182,15 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
     };
     using whole = std::integral_constant<bool, false>;
     using last = std::integral_constant<bool, true>;
-    for (int c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) issue(c + 1, kb, vb);
-        if (c + 1 < nch) chunk(whole{}, c, ka, va);
-        else { patch(ka, va); chunk(last{}, c, ka, va); }
-        if (c + 1 < nch) {
-            if (c + 2 < nch) issue(c + 2, ka, va);
-            if (c + 2 < nch) chunk(whole{}, c + 1, kb, vb);
-            else { patch(kb, vb); chunk(last{}, c + 1, kb, vb); }
+    for (int c0 = 0; c0 < nch; c0 += NB) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk c0 + k in slot k
+            const int c = c0 + k;
+            if (c < nch) {
+                if (c + NB - 1 < nch) issue(c + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
+                if (c + 1 < nch) chunk(whole{}, c, kq[k], vq[k]);
+                else { patch(kq[k], vq[k]); chunk(last{}, c, kq[k], vq[k]); }
+            }
         }
     }
     // merge the four waves

@@ -35,6 +35,9 @@ namespace {
 using namespace pmm;
 
 constexpr int NL = 28, SW0 = 128, VPT = VOC / 256;
+#ifndef TKB_NB
+#define TKB_NB 4   // attention K/V ring depth (chunks of 32 KB per workgroup)
+#endif
 
 enum Kind { K_RNA = 0, K_QKV = 1, K_ATT = 2, K_O = 3, K_RNF = 4, K_GU = 5, K_DN = 6, K_HEAD = 7 };
 __device__ __forceinline__ int ph_of(int l, int k) { return l * 8 + k; }   // l = NL: the final norm / head
@@ -183,7 +186,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             const size_t hoff = (size_t)l * p.kv_layer + ((size_t)ub * NKV + g) * p.n_ctx * D;
             const uint32_t tq = X.tag(ph_of(l, K_QKV));
             if (u == w) TPROF(ph_of(l, K_QKV), 0);
-            attn_seq_wg<true>(
+            attn_seq_wg<true, TKB_NB>(
                 pos, p.kc + hoff, p.vc + hoff, p.rope + (size_t)pos * D, Lw.qn, Lw.kn, p.eps,
                 [&](int v, float (&xv)[2]) {   // wave v: q head 2g + v (v < 2), k (2), v (3) of slot ub: 2 granules per lane
                     const int row = v < 2 ? (2 * g + v) * D : v == 2 ? (NH + g) * D : (NH + NKV + g) * D;
@@ -194,6 +197,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
                         const u32x2_t c = __builtin_amdgcn_raw_buffer_load_b64(X.rs, (int)(o + 64 * 8), 0, SC1V);
                         r[0] = u32x4_t{a.x, a.y, c.x, c.y};
                     });
+                    if (u == w && v == 0) TPROF(ph_of(l, K_QKV), 1);
                     xv[0] = __uint_as_float(gq[0].x);
                     xv[1] = __uint_as_float(gq[0].z);
                 },
