@@ -353,14 +353,18 @@ def main():
                 "x_realtime": round(args.frames * FRAME_SEC * batched * world / b_el, 1),
                 "steps": b_steps, "breakdown_ms_per_step": {k: round(v / b_steps, 1) for k, v in stats.items()},
                 "talker_step_ms": round(bt, 4), "cp_frame_ms": round(bc, 4),
-                "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots "
-                                                       "(MFMA f16 GEMMs on hoisted norms, split-K slabs, k_attn_seq: one "
-                                                       "workgroup per (slot, kv head) streaming the whole context: 7 "
-                                                       "launches per layer)",
+                "roofline": {"bound": "hbm", "kernel": f"talker decode step at KV position {p_mid}, {batched} slots " + (
+                                 "(ONE persistent launch, k_tkb, persist_tkb.hip: 28 layers + codec head + CB0 selection; "
+                                 "MFMA tile jobs with LDS-DMA weights, granule / flag hand-offs, attention one workgroup "
+                                 "per (slot, kv head) streaming the whole context)" if pk & 32 else
+                                 "(MFMA f16 GEMMs on hoisted norms, split-K slabs, k_attn_seq: one workgroup per (slot, kv "
+                                 "head) streaming the whole context: 7 launches per layer)"),
                              "achieved": round(b_bytes / (bt * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(b_bytes / (bt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "traffic": pmc_traffic(batched)[0], "traffic_source": pmc_traffic(batched)[1],
                              "bytes_per_launch": b_bytes, "launch_ms": round(bt, 4)},
+                "cp_kernel": ("16-pass code-predictor frame of every slot, ONE persistent launch (k_cpb, persist_cpb.hip)"
+                              if pk & 16 else "16-pass code-predictor frame, launch-per-op graph (decoder_stack_mm)"),
                 "vocoder_roofline": voc_roofline(stats["vocoder_ms"], batched, b_steps),
                 "mfma_pmc": pmc_file("talker_b64"), "mfma_pmc_cp": pmc_file("cp_b64")}
 
