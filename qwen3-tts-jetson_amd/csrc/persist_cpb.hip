@@ -13,7 +13,7 @@
 //   QKV              128 x NT         [0, 128 NT)       32 rows x 32 tokens, K 1024 (xnA 64 KB)    qkv f32
 //   ATT              1 per slot       192 + b           8 kv groups (2 per wave), <= 16 positions  attn f16 [b]
 //   O                32 x 4 x NT      [0, 128 NT)       32 rows x 32 tokens x K slice 512          slabO f32 [z]
-//   GU               192              [0, 192)          32 rows (16 SwiGLU units) x 32 NT tokens   h f16
+//   GU               96 x NT          gj: [0, 128), odd slot wgs  64 rows (32 SwiGLU units) x 32 tokens  h f16
 //   DN               32 x 4 x NT      [0, 128 NT)       32 rows x 32 tokens x K slice 768          slabD f32 [z]
 //   HEAD (p >= 1)    64 x NT          [0, 64 NT)        32 rows x 32 tokens, K 1024 (final xnA)    logits f32
 //   SEL  (p >= 1)    1 per slot       192 + b           top-k / argmax of the slot's row, commit; next pass's x[b]
@@ -92,7 +92,10 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
     const bool slot = sw >= 0 && sw < 2 * p.S;
     const int b = sw >> 1, hf = sw & 1;
     const bool rn = slot && hf == 0;
-    const bool hq = w < NQJ, hg = w < NGJ, hh = w < NHJ;
+    // gate/up job gj: workgroups [0, 128), then the odd slot workgroups 129, 131, ...: the residual rows' workgroups
+    // (even) run the norm right before gate/up, so a gate/up job there started ~2 us after the others
+    const int gj = w < SW0 ? w : (w & 1) ? SW0 + (w - SW0 - 1) / 2 : -1;
+    const bool hq = w < NQJ, hg = gj >= 0 && gj < NGJ, hh = w < NHJ;
     if (t < NLC) S.layers[t] = p.L[t];
     if (t < 15) S.heads[t] = p.heads[t];
     if (t < 16) S.tabs[t] = p.tabs[t];
@@ -120,7 +123,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         switch (ck) {
             case K_QKV: load_w<4>(S.wl, Lw.qkv, H, 64 * (w % 64), 0); break;
             case K_O: load_w<2>(S.wl, Lw.o, NH * D, 64 * (w % 16), 512 * ((w / 16) % 4)); break;
-            case K_GU: load_w<4>(S.wl, Lw.gu, H, 64 * (w % 96), 0); break;
+            case K_GU: load_w<4>(S.wl, Lw.gu, H, 64 * (gj % 96), 0); break;
             case K_DN: load_w<3>(S.wl, Lw.down, INTER, 64 * (w % 16), 768 * ((w / 16) % 4)); break;
             default: load_w<4>(S.wl, S.heads[cp - 1], H, 64 * (w % 32), 0); break;
         }
@@ -257,7 +260,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
             // ---- GU: 32 SwiGLU units (rows 64 rp .. +63, gate/up interleaved in 16-row blocks), tile tt
             if (hg) {
                 after_rn();
-                const int rp = w % 96, tt = w / 96;
+                const int rp = gj % 96, tt = gj / 96;
                 const int nv = min(32, p.S - 32 * tt);
                 wait_flags_wg(X, K_RNF, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(pass, l, K_RNF)));
                 mm_tile<4>(X, SL.xnf, H / 8, 0, 32 * tt);
@@ -275,7 +278,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                         __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.h + fragoff(INTER / 8, tok, unit), 0, SC1);
                     }
                 }
-                publish(X, K_GU, w, X.tag(ph_of(pass, l, K_GU)));
+                publish(X, K_GU, gj, X.tag(ph_of(pass, l, K_GU)));
                 after_job();
             }
             // ---- DN: split-K slab z of rows 64 rp .. +63, tile tt; wave w reads units [768 z + 192 w, +192)

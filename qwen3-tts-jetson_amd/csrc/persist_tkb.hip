@@ -13,7 +13,7 @@
 //   QKV              64 x NT          [0, 64 NT)        64 rows x 32 tokens, K 1024                  qkv granules
 //   ATT              8 per slot       u % 256, u = 8b+g (slot b, kv head g): the whole context          attn f16
 //   O                16 x 4 x NT      [0, 64 NT)        64 rows x 32 tokens x K slice 512            slabO granules
-//   GU               96 x NT          [0, 96 NT)        32 SwiGLU units x 32 tokens                  h f16
+//   GU               96 x NT          gj: [0, 128), odd slot wgs  32 SwiGLU units x 32 tokens           h f16
 //   DN               16 x 4 x NT      [0, 64 NT)        64 rows x 32 tokens x K slice 768            slabD granules
 //   HEAD             48 x NT          [0, 48 NT)        64 rows x 32 tokens, K 1024 (final xnA)      logits granules
 //   SEL              1 per slot       128 + 2b          CB0 selection of the slot (+ logits row, commit)
@@ -89,7 +89,10 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
     const bool rn = sw >= 0 && sw < 2 * p.S && (sw & 1) == 0;   // slot b's residual row, norms and selection
     const bool slot = sw >= 0 && sw < 2 * p.S;
     const int b = sw >> 1;
-    const bool hq = w < NQJ, hg = w < NGJ, hh = w < NHJ;
+    // gate/up job gj: workgroups [0, 128), then the odd slot workgroups 129, 131, ...: the residual rows' workgroups
+    // (even) run the norm right before gate/up, so a gate/up job there started ~2 us after the others
+    const int gj = w < SW0 ? w : (w & 1) ? SW0 + (w - SW0 - 1) / 2 : -1;
+    const bool hq = w < NQJ, hg = gj >= 0 && gj < NGJ, hh = w < NHJ;
     const int nunits = NKV * p.S;
     for (int i = t; i < NL; i += 256) S.layers[i] = p.L[i];
     __syncthreads();
@@ -113,7 +116,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
         switch (ck) {
             case K_QKV: load_w<4>(S.wl, Lw.qkv, H, 64 * (w % 64), 0); break;
             case K_O: load_w<2>(S.wl, Lw.o, NH * D, 64 * (w % 16), 512 * ((w / 16) % 4)); break;
-            case K_GU: load_w<4>(S.wl, Lw.gu, H, 64 * (w % 96), 0); break;
+            case K_GU: load_w<4>(S.wl, Lw.gu, H, 64 * (gj % 96), 0); break;
             case K_DN: load_w<3>(S.wl, Lw.down, INTER, 64 * (w % 16), 768 * ((w / 16) % 4)); break;
             default: load_w<4>(S.wl, p.head, H, 64 * (w % 48), 0); break;
         }
@@ -229,7 +232,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
         // ---- GU: 32 SwiGLU units (rows 64 rp .. +63, gate/up interleaved in 16-row blocks), tile tt
         if (hg) {
             flush();
-            const int rp = w % 96, tt = w / 96;
+            const int rp = gj % 96, tt = gj / 96;
             const int nv = min(32, p.S - 32 * tt);
             wait_flags_wg(X, K_RNF, nv, [&](int i) { return 32 * tt + i; }, X.tag(ph_of(l, K_RNF)));
             mm_tile<4>(X, SL.xnf, H / 8, 0, 32 * tt);
@@ -247,7 +250,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
                     __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.h + fragoff(INTER / 8, tok, unit), 0, SC1);
                 }
             }
-            publish(X, K_GU, w, X.tag(ph_of(l, K_GU)));
+            publish(X, K_GU, gj, X.tag(ph_of(l, K_GU)));
             after_job();
         }
         // ---- DN: split-K slab z of rows 64 rp .. +63, tile tt; wave w reads units [768 z + 192 w, +192)
