@@ -80,6 +80,11 @@ void q3t_ctx_destroy(q3t_ctx *ctx);
 int q3t_comm_unique_id(uint8_t *id /* [Q3T_COMM_ID_BYTES] */);
 int q3t_ctx_create_shared(const char *tts_gguf, const char *tokenizer_gguf, int device, int max_slots, int max_ctx,
                           int rank, int world, const uint8_t *id, q3t_ctx **out);
+/* host-only weight layout of a model file (no device touched): the byte offset of every allocation of the talker blob
+ * in order (n_alloc of them; offsets may be NULL to query n_alloc, else max_n entries) and the bytes used -- what every
+ * rank of q3t_ctx_create_shared computes from the GGUF headers before the broadcast (whose size check compares
+ * `used` across ranks) */
+int q3t_plan_weight_layout(const char *tts_gguf, uint64_t *offsets, int max_n, int *n_alloc, uint64_t *used);
 /* a second context whose weight blobs are copied device-to-device from src's (same or peer device, no file reads) */
 int q3t_ctx_create_replica(q3t_ctx *src, int device, int max_slots, int max_ctx, q3t_ctx **out);
 /* element-wise max over the ranks of a shared context (n <= 64 host doubles; also a barrier); no-op otherwise */

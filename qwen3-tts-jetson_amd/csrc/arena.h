@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstddef>
 #include <string>
+#include <vector>
 
 #include "q3t_common.h"
 
@@ -17,6 +18,8 @@ namespace q3t {
 
 struct WeightArena {
     bool recv = false;      // true: shapes only, the bytes arrive later (broadcast / device copy)
+    bool plan = false;      // true: host-only layout (no device memory; implies recv): the offsets every rank computes
+    std::vector<size_t> *trace = nullptr;   // plan: the offset of every allocation, in order
     char *base = nullptr;
     size_t cap = 0, used = 0;
 
@@ -24,10 +27,14 @@ struct WeightArena {
     WeightArena(const WeightArena &) = delete;
     WeightArena &operator=(const WeightArena &) = delete;
     ~WeightArena() {
-        if (base) hipFree(base);
+        if (base && !plan) hipFree(base);
     }
     bool reserve(size_t bytes) {
         cap = (bytes + 255) & ~(size_t)255;
+        if (plan) {   // an address that is never dereferenced: only offsets from it are recorded
+            base = reinterpret_cast<char *>((size_t)1 << 44);
+            return true;
+        }
         if (hipMalloc(&base, cap) != hipSuccess) {
             base = nullptr;
             set_error("weight arena: hipMalloc of " + std::to_string(cap) + " B failed");
@@ -43,12 +50,13 @@ struct WeightArena {
             return nullptr;
         }
         T *p = reinterpret_cast<T *>(base + used);
+        if (trace) trace->push_back(used);
         used += bytes;
         return p;
     }
     // host -> arena copy; a no-op on receiving ranks (their bytes come from the broadcast)
     bool put(void *dst, const void *src, size_t bytes) {
-        if (recv || bytes == 0) return true;
+        if (recv || plan || bytes == 0) return true;
         if (hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) {
             set_error("weight arena: upload failed");
             return false;

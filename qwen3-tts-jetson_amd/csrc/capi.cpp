@@ -109,6 +109,23 @@ int q3t_ctx_create_shared(const char *tts_gguf, const char *tokenizer_gguf, int 
     GUARD_END
 }
 
+int q3t_plan_weight_layout(const char *tts_gguf, uint64_t *offsets, int max_n, int *n_alloc, uint64_t *used) {
+    GUARD_BEGIN
+    if (!tts_gguf || !n_alloc || !used) { q3t::set_error("null argument"); return Q3T_ERR; }
+    std::vector<size_t> off;
+    size_t u = 0;
+    {
+        q3t::Engine e;
+        if (!e.plan_layout(tts_gguf, off, u)) return Q3T_ERR;
+    }
+    *n_alloc = (int)off.size();
+    *used = u;
+    if (offsets)
+        for (int i = 0; i < std::min<int>(max_n, (int)off.size()); ++i) offsets[i] = off[i];
+    return Q3T_OK;
+    GUARD_END
+}
+
 int q3t_ctx_create_replica(q3t_ctx *src, int device, int max_slots, int max_ctx, q3t_ctx **out) {
     GUARD_BEGIN
     if (!out || !src) { q3t::set_error("null argument"); return Q3T_ERR; }

@@ -172,36 +172,9 @@ bool check_shape(const GgufTensor *t, const char *name, int64_t cols, int64_t ro
 }
 }  // namespace
 
-bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
-                  bool recv_weights) {
-    DeviceLock lk(false, device);   // allocation zeroing / weight upload run kernels and copies on this device
-    device_ = device;
-    tts_path_ = tts_gguf;
-    tok_path_ = tok_gguf;
-    wa_.recv = recv_weights;
-    opt_ = Options::from_env();
-    cp_fused_attn_ = opt_.cp_fused_attn;
-    defer_cp_select_ = opt_.defer_cp_select;
-    fused_select_ = opt_.fused_select;
-    persist_ = opt_.persist;
-    poll_every_ = opt_.poll_every;
-    max_slots_ = std::max(1, max_slots);
-    max_ctx_ = std::max(32, max_ctx);
-    if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
-    Q3T_HIP(hipSetDevice(device));
-    Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    if (tts_gguf.empty()) {
-        // vocoder-only context (AudioTokenizerDecoder / TRTVocoderDecoder load without a talker model)
-        if (tok_gguf.empty()) { set_error("no model file given"); return false; }
-        talker_ = false;
-        voc_.reset(new Vocoder());
-        if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
-        Q3T_HIP(hipStreamSynchronize(stream_));
-        return true;
-    }
-    Gguf g;
-    if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
-    // parse_config key aliases / defaults: src/tts_transformer.cpp:288-442
+// parse_config key aliases / defaults: src/tts_transformer.cpp:288-442 (GGUF header keys only: every rank, and the
+// host-only layout plan, compute the same config)
+bool Engine::parse_config(const Gguf &g) {
     c_.text_vocab = (int)g.get_int({"qwen3-tts.text.vocab_size", "qwen3-tts.text_vocab_size"}, 151936);
     c_.text_dim = (int)g.get_int({"qwen3-tts.text.embedding_dim", "qwen3-tts.text_hidden_size"}, 2048);
     c_.hidden = (int)g.get_int({"qwen3-tts.talker.embedding_length", "qwen3-tts.embedding_length"}, 1024);
@@ -247,6 +220,39 @@ bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int 
     if (c_.n_codebooks != 16) { set_error("n_codebooks must be 16"); return false; }
     // the fused code-predictor attention prologue is specialised to the 0.6B head layout (16 q / 8 kv heads x 128)
     cp_fused_attn_ = cp_fused_attn_ && c_.cp_heads == 16 && c_.cp_kv == 8 && c_.head_dim == 128 && c_.cp_hidden == 1024;
+    return true;
+}
+
+bool Engine::load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
+                  bool recv_weights) {
+    DeviceLock lk(false, device);   // allocation zeroing / weight upload run kernels and copies on this device
+    device_ = device;
+    tts_path_ = tts_gguf;
+    tok_path_ = tok_gguf;
+    wa_.recv = recv_weights;
+    opt_ = Options::from_env();
+    cp_fused_attn_ = opt_.cp_fused_attn;
+    defer_cp_select_ = opt_.defer_cp_select;
+    fused_select_ = opt_.fused_select;
+    persist_ = opt_.persist;
+    poll_every_ = opt_.poll_every;
+    max_slots_ = std::max(1, max_slots);
+    max_ctx_ = std::max(32, max_ctx);
+    if (max_ctx_ > ATTN_CHUNK * ATTN_MAX_SPLITS) { set_error("max_ctx exceeds " + std::to_string(ATTN_CHUNK * ATTN_MAX_SPLITS)); return false; }
+    Q3T_HIP(hipSetDevice(device));
+    Q3T_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (tts_gguf.empty()) {
+        // vocoder-only context (AudioTokenizerDecoder / TRTVocoderDecoder load without a talker model)
+        if (tok_gguf.empty()) { set_error("no model file given"); return false; }
+        talker_ = false;
+        voc_.reset(new Vocoder());
+        if (!voc_->load(tok_gguf, stream_, recv_weights)) return false;
+        Q3T_HIP(hipStreamSynchronize(stream_));
+        return true;
+    }
+    Gguf g;
+    if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
+    if (!parse_config(g)) return false;
     if (!upload_weights(g)) return false;
     if (!alloc_state()) return false;
 #ifdef Q3T_DEV
@@ -292,7 +298,10 @@ std::vector<WeightArena *> Engine::weight_arenas() {
     return v;
 }
 
-bool Engine::upload_weights(const Gguf &g) {
+bool Engine::upload_weights(const Gguf &g) { return layout_weights(g) && upload_weights_rest(); }
+
+// every weight tensor into the arena, in a fixed order that depends on the GGUF shapes alone
+bool Engine::layout_weights(const Gguf &g) {
     const int H = c_.hidden, D = c_.head_dim;
     // every weight goes into the arena (one blob: the unit of the RCCL broadcast); receiving ranks touch only the
     // GGUF headers, never the tensor bytes
@@ -381,6 +390,26 @@ bool Engine::upload_weights(const Gguf &g) {
         spk_.reset(new SpeakerEncoder());
         if (!spk_->load(g, wa_, stream_)) return false;
     }
+    return true;
+}
+
+// the weight arena of a model file laid out on the host only (WeightArena::plan): the offsets of every allocation in
+// order and the bytes used -- what every rank of a shared start-up computes from the GGUF headers before the RCCL
+// broadcast (comm_bcast_arenas checks the sizes; tests/test_dist_cpu.py compares whole layouts across gloo ranks)
+bool Engine::plan_layout(const std::string &tts_gguf, std::vector<size_t> &offsets, size_t &used) {
+    Gguf g;
+    if (!g.open(tts_gguf)) { set_error(g.error()); return false; }
+    if (!parse_config(g)) return false;
+    wa_.plan = wa_.recv = true;
+    wa_.trace = &offsets;
+    const bool ok = layout_weights(g);
+    wa_.trace = nullptr;
+    used = wa_.used;
+    return ok;
+}
+
+bool Engine::upload_weights_rest() {
+    const int D = c_.head_dim;
     // the 16 tables of the step embedding: codec_embd (code 0) + code_pred.codec_embd[0..14] (codes 1..15)
     std::vector<uint16_t *> tabs16(16);
     tabs16[0] = codec_embd_;

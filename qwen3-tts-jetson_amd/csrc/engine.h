@@ -81,6 +81,8 @@ public:
     ~Engine();
     // recv_weights: lay out the weight arenas from the GGUF headers only; the bytes are filled afterwards by
     // copy_weights_from() or an RCCL broadcast of weight_arenas()
+    // host-only weight layout of a model file (no device): allocation offsets in order, bytes used
+    bool plan_layout(const std::string &tts_gguf, std::vector<size_t> &offsets, size_t &used);
     bool load(const std::string &tts_gguf, const std::string &tok_gguf, int device, int max_slots, int max_ctx,
               bool recv_weights = false);
     // the packed weight blobs (talker + code predictor + embeddings; vocoder), in broadcast order
@@ -160,6 +162,9 @@ public:
 
 private:
     bool upload_weights(const Gguf &g);
+    bool parse_config(const Gguf &g);
+    bool layout_weights(const Gguf &g);
+    bool upload_weights_rest();
     bool alloc_state();
     bool setup_persist();
     // after a persistent launch flagged a fault: drain the stream, clear the hand-off state, drop the captured graphs

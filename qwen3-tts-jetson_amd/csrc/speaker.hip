@@ -215,6 +215,7 @@ bool SpeakerEncoder::load(const Gguf &g, WeightArena &wa, hipStream_t s) {
     if (!conv("mfa", mfa_, MFA, MFA, 1) || !conv("asp.tdnn", asp_tdnn_, 3 * MFA, 128, 1) ||
         !conv("asp.conv", asp_conv_, 128, MFA, 1) || !conv("fc", fc_, 2 * MFA, dim_, 1))
         return false;
+    if (wa.plan) return true;   // host-only layout: the arena part is all a plan records
     // front-end constants with the reference's own expressions (computed per rank, outside the weight blob)
     std::vector<float> basis((size_t)NFFT * 2 * NBIN), win(NFFT, 0.0f), fbT((size_t)NBIN * NMEL, 0.0f);
     for (int k = 0; k < NBIN; ++k)

@@ -61,6 +61,7 @@ COMM_ID_BYTES = 128
 _lib.q3t_comm_unique_id.argtypes = [C.c_char_p]
 _lib.q3t_ctx_create_shared.argtypes = [C.c_char_p, C.c_char_p, _I, _I, _I, _I, _I, C.c_char_p, C.POINTER(_P)]
 _lib.q3t_ctx_create_replica.argtypes = [_P, _I, _I, _I, C.POINTER(_P)]
+_lib.q3t_plan_weight_layout.argtypes = [C.c_char_p, _P, _I, C.POINTER(_I), C.POINTER(C.c_uint64)]
 _lib.q3t_comm_allreduce_max.argtypes = [_P, np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"), _I]
 _lib.q3t_set_mfma_min_batch.argtypes = [_I]
 _lib.q3t_synchronize.argtypes = [_P]
@@ -99,7 +100,7 @@ _lib.q3t_prefill_embd.argtypes = [_P, _ip, _I, _P, _I, _fp, C.POINTER(C.c_int32)
 # names the C ABI must export (checked by tests without a GPU)
 EXPORTS = ["q3t_last_error", "q3t_default_params", "q3t_ctx_create", "q3t_ctx_destroy", "q3t_get_config",
            "q3t_generate", "q3t_generate_stream", "q3t_generate_queue", "q3t_comm_unique_id", "q3t_ctx_create_shared",
-           "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_persist_kernels", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
+           "q3t_plan_weight_layout", "q3t_ctx_create_replica", "q3t_comm_allreduce_max", "q3t_set_mfma_min_batch", "q3t_synchronize", "q3t_last_timing", "q3t_time_stage", "q3t_persist_status", "q3t_persist_kernels", "q3t_vocoder_num_samples", "q3t_vocoder_flops", "q3t_vocoder_decode",
            "q3t_vocoder_decode_chunked", "q3t_vocoder_decode_batch", "q3t_vocoder_set_batch_frames", "q3t_speaker_dim", "q3t_ctx_create_speaker", "q3t_speaker_encode", "q3t_speaker_mel",
            "q3t_tokenizer_load", "q3t_tokenizer_free", "q3t_tokenizer_info", "q3t_tokenizer_encode",
            "q3t_tokenizer_decode", "q3t_talker_forward", "q3t_talker_prefill",
@@ -138,6 +139,17 @@ def comm_unique_id():
     buf = C.create_string_buffer(COMM_ID_BYTES)
     _check(_lib.q3t_comm_unique_id(buf))
     return buf.raw
+
+
+def plan_weight_layout(tts_gguf):
+    """Host-only weight layout of a model file (no device): (byte offset of every allocation of the talker blob in
+    order, bytes used) -- what each rank of a shared start-up computes from the GGUF headers before the broadcast."""
+    n = C.c_int(0)
+    used = C.c_uint64(0)
+    _check(_lib.q3t_plan_weight_layout(str(tts_gguf).encode(), None, 0, C.byref(n), C.byref(used)))
+    off = np.zeros(max(n.value, 1), np.uint64)
+    _check(_lib.q3t_plan_weight_layout(str(tts_gguf).encode(), _addr(off), n.value, C.byref(n), C.byref(used)))
+    return off[:n.value], int(used.value)
 
 
 class Tokenizer:
