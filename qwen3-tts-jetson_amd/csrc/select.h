@@ -1,11 +1,22 @@
 // select.h — token selection of the decode path on one 256-thread workgroup (device code, included by the kernel
 // translation units).  Thread t owns the contiguous indices [t*vpt, t*vpt + vpt), vpt = ceil(V / 256) <= 16, in
-// registers, so the inverse-CDF scan runs in index order exactly like the reference's sequential loop.
+// registers.
 //
 //   argmax         first maximum (strict '>' scan, src/tts_transformer.cpp:2051-2061)
-//   top-k sampling /T -> k-th largest by 3-pass radix select on order-preserving keys (11/11/10-bit digits),
-//                  `< thr -> -inf` so ties survive (:2456-2464), optional kept id restored (EOS, :2466-2470),
-//                  exp(v - max), inverse CDF with u * total (:2474-2495; CP: trt_cuda_kernels.cu:120-183)
+//   top-k sampling /T -> top-k with `< thr -> -inf` so ties survive (:2456-2464), the kept id restored (EOS,
+//                  :2466-2470), exp(v - max), inverse CDF with u * total (:2474-2495; CP: trt_cuda_kernels.cu:120-183).
+//                  Default: sel_topk_fast -- three workgroup barriers (row max / min, a 256-bin range histogram, the
+//                  <= 128 entries at or above the boundary bin gathered in index order); the boundary-bin entries are
+//                  ranked among themselves, so the survivors are exactly {v >= k-th largest} (+ the kept id).  Its CDF
+//                  total adds the survivors' exponentials two per lane and scans across one wave, in index order: the
+//                  same set and order as the reference's sequential loop, but not the same f32 rounding of the running
+//                  sum as the general path (per-thread sums in index order, then the waves), so a row whose u * total
+//                  falls within an ulp-level distance of a CDF boundary can pick a neighbouring token on the two paths
+//                  (checked against the reference semantics within 1e-4 of the CDF: tests/test_gpu_select.py,
+//                  test_gpu_parity.py::test_cb0_select_kept_eos).  Degenerate rows (no finite range, fewer than k finite
+//                  values, more than 128 entries at or above the boundary bin) take the general path: k-th largest by a
+//                  range histogram + candidate ranking, or a 3-pass radix select on order-preserving keys (11/11/10-bit
+//                  digits), then the thread-order inverse-CDF scan.
 //   CB0 processing control-range mask, repetition penalty over the seen set, EOS ramp, bench EOS mask
 //                  (src/tts_transformer.cpp:2416-2445)
 #pragma once

@@ -177,6 +177,53 @@ def test_cb0_select_matches_oracle(pair):
             assert got[s] == exp, (trial, s)
 
 
+def test_cb0_select_kept_eos(pair):
+    """the kept id (EOS) of the CB0 top-k on the fast selection path (select.h sel_topk_fast): EOS in the boundary bin
+    (tied with the k-th largest, just below it), boosted by the EOS ramp, or -inf; with and without the bench EOS mask.
+    Each token must lie in the reference's inverse-CDF interval (keep_id restored after the top-k) of the oracle's
+    processed logits (tolerance 1e-4 of the CDF), and a -inf EOS is never picked."""
+    cfg, eng, orc = pair
+    V = eng.cfg["codec_vocab"]
+    EOS = 2150 if V > 2150 else V - 1
+    rng = np.random.default_rng(5)
+    n = n_tol = 0
+    for case in ("tie", "below", "ramp", "neg_inf", "tie_bin", "masked"):
+        for trial in range(6):
+            lg = (rng.standard_normal((2, V)) * 3).astype(np.float32)
+            lg[:, V - 1024:] = np.where(np.arange(V - 1024, V) == EOS, lg[:, V - 1024:], -5.0)   # (masked anyway)
+            seen = np.zeros((2, V), np.uint8)
+            frame, force = 5, 0
+            for s in range(2):
+                kth = np.sort(lg[s][: V - 1024])[::-1][49]
+                if case == "tie":
+                    lg[s, EOS] = kth
+                elif case == "below":
+                    lg[s, EOS] = np.nextafter(kth, -np.inf, dtype=np.float32)
+                elif case == "ramp":
+                    frame = 70
+                    lg[s, EOS] = kth - 1.0
+                elif case == "neg_inf":
+                    lg[s, EOS] = -np.inf
+                elif case == "tie_bin":   # many exact ties around the cut, EOS among them
+                    lg[s] = np.round(lg[s] * 2) / 2
+                    lg[s, EOS] = np.round(kth * 2) / 2
+                else:                     # bench EOS mask: EOS is not kept
+                    force = 100
+                    lg[s, EOS] = kth
+            got = eng.cb0_select(lg, seen, frame, 16, temperature=0.9, top_k=50, seed=31 + trial,
+                                 repetition_penalty=1.0, force_frames=force)
+            for s in range(2):
+                u = uniform(31 + trial, s, frame, 0)
+                exp, proc = orc.cb0_select(lg[s], seen[s], frame, 16, rep=1.0, temperature=0.9, top_k=50, u=u,
+                                           eos_mask=int(frame < force))
+                keep = -1 if frame < force else EOS
+                if case == "neg_inf" or frame < force:
+                    assert got[s] != EOS, (case, trial, s)
+                n_tol += check_token(proc, int(got[s]), 0.9, 50, float(u), keep, tol_cdf=1e-4)
+                n += 1
+    assert n_tol <= 2, (n_tol, n)
+
+
 def test_project_text_and_prefill_match_oracle(pair):
     cfg, eng, orc = pair
     toks = prompt(cfg)
