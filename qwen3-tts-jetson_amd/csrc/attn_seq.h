@@ -13,6 +13,8 @@
 // The caller supplies the raw QKV values (qkv_of: wave v < 2 q head 2g + v, v = 2 the new k, v = 3 the new v; lanes
 // lane and lane + 64) -- K/V chunk 0 is in flight before it is called -- and the output store (out: one value, or with
 // VEC4 four consecutive dims of threads 0..63; the per-dim arithmetic does not depend on the thread that runs it).
+// (Measured and rejected: two units per workgroup with their whole chunks interleaved -- two dependency chains per wave
+// -- spilled 340 B per lane inside the persistent step and ran 20 us per layer against 15 us for the two in turn.)
 #pragma once
 #include "kernels.h"
 
@@ -46,161 +48,154 @@ __device__ __forceinline__ void unpack8_cvt(const uint4 u, float (&f)[8]) {
 }
 }  // namespace aseq
 
-//   kc/vc: this (layer, slot, kv head)'s cache [n_ctx][128] f16 (row pos is written here); rope_row: rope + pos * 128
-template <bool VEC4, int NB, class QkvOf, class Out>
-__device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc, const float *rope_row, const float *qn,
-                                            const float *kn, float eps, QkvOf qkv_of, Out out, AttnSeqLds &L) {
-    using namespace aseq;
-    constexpr int D = 128, R = 2, LPP = D / 8, NP = 4;   // 16 lanes per position, 4 passes of 16 positions per 64-chunk
-    const int nch = pos / 64 + 1;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, pg = t / LPP, li = t % LPP;
-
-    static_assert(NB >= 2 && NB <= 4, "ring depth");
-    uint4 kq[NB][NP], vq[NB][NP];
-    auto issue = [&](int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            const int j = min(c * 64 + pi * 16 + pg, pos);
-            kr[pi] = ld16(kc + (size_t)j * D + li * 8);
-            vr[pi] = ld16(vc + (size_t)j * D + li * 8);
-        }
-    };
-#pragma unroll
-    for (int c = 0; c < NB - 1; ++c)
-        if (c < nch) issue(c, kq[c], vq[c]);
-
-    // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded
-    {
-        const int v = wave;
-        float x[2];
-        qkv_of(v, x);
-        if (v == R + 1) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) L.vh_s[lane + 64 * e] = f2h(x[e]);
-        } else {
-            const bool isk = v == R;
-            const float *w = isk ? kn : qn;
-            double ss = 0.0;
-#pragma unroll
-            for (int e = 0; e < 2; ++e) ss += (double)__fmul_rn(x[e], x[e]);
-            ss = wave_sum_d(ss);
-            const float scale = 1.0f / sqrtf((float)(ss / D) + eps);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
-            const float c = rope_row[2 * lane], s = rope_row[2 * lane + 1];
-            const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
-            const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
-            if (isk) {
-                L.kh_s[lane] = f2h(y0);
-                L.kh_s[lane + 64] = f2h(y1);
-            } else {
-                L.q_s[v][lane] = f16r(y0);
-                L.q_s[v][lane + 64] = f16r(y1);
-            }
-        }
-    }
-    __syncthreads();
-    if (t < D) {   // KV append at pos
-        kc[(size_t)pos * D + t] = L.kh_s[t];
-        vc[(size_t)pos * D + t] = L.vh_s[t];
-    }
-    const float kq_scale = 1.0f / sqrtf((float)D);
-    // q is f16-exact (f16r above): the scores are v_dot2_f32_f16 over f16 pairs straight from the K registers (no
-    // per-element conversion; f16 products are exact in f32)
-    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+namespace aseq {
+constexpr int D = 128, R = 2, LPP = D / 8, NP = 4;   // 16 lanes per position, 4 passes of 16 positions per 64-chunk
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+struct Unit {   // one (slot, kv head): its cache, position and online-softmax state (this thread's share)
+    int pos, nch;
+    uint16_t *kc, *vc;
     h2_t q2[R][4];
+    float m[R], l[R], acc[R][8];
+};
+__device__ __forceinline__ void unit_init(Unit &U, int pos, uint16_t *kc, uint16_t *vc) {
+    U.pos = pos;
+    U.nch = pos / 64 + 1;
+    U.kc = kc;
+    U.vc = vc;
+}
+__device__ __forceinline__ void issue(const Unit &U, int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
+    const int t = threadIdx.x, pg = t / LPP, li = t % LPP;
+#pragma unroll
+    for (int pi = 0; pi < NP; ++pi) {
+        const int j = min(c * 64 + pi * 16 + pg, U.pos);
+        kr[pi] = ld16(U.kc + (size_t)j * D + li * 8);
+        vr[pi] = ld16(U.vc + (size_t)j * D + li * 8);
+    }
+}
+// head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded (wave v: vector v)
+template <class QkvOf>
+__device__ __forceinline__ void prologue(const float *rope_row, const float *qn, const float *kn, float eps, QkvOf qkv_of,
+                                         AttnSeqLds &L) {
+    const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+    float x[2];
+    qkv_of(v, x);
+    if (v == R + 1) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) L.vh_s[lane + 64 * e] = f2h(x[e]);
+    } else {
+        const bool isk = v == R;
+        const float *w = isk ? kn : qn;
+        double ss = 0.0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) ss += (double)__fmul_rn(x[e], x[e]);
+        ss = wave_sum_d(ss);
+        const float scale = 1.0f / sqrtf((float)(ss / D) + eps);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) x[e] = (x[e] * scale) * w[lane + 64 * e];
+        const float c = rope_row[2 * lane], s = rope_row[2 * lane + 1];
+        const float y0 = opaque(opaque(x[0] * c) - opaque(x[1] * s));
+        const float y1 = opaque(opaque(x[0] * s) + opaque(x[1] * c));
+        if (isk) {
+            L.kh_s[lane] = f2h(y0);
+            L.kh_s[lane + 64] = f2h(y1);
+        } else {
+            L.q_s[v][lane] = f16r(y0);
+            L.q_s[v][lane + 64] = f16r(y1);
+        }
+    }
+}
+// after the barrier that follows prologue(): the KV append at pos, q as f16 pairs (f16-exact: the scores are
+// v_dot2_f32_f16 straight from the K registers), the state zeroed
+__device__ __forceinline__ void start(Unit &U, const AttnSeqLds &L) {
+    const int t = threadIdx.x, li = t % LPP;
+    if (t < D) {
+        U.kc[(size_t)U.pos * D + t] = L.kh_s[t];
+        U.vc[(size_t)U.pos * D + t] = L.vh_s[t];
+    }
 #pragma unroll
     for (int h = 0; h < R; ++h)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            q2[h][e].x = (_Float16)L.q_s[h][li * 8 + 2 * e];
-            q2[h][e].y = (_Float16)L.q_s[h][li * 8 + 2 * e + 1];
+            U.q2[h][e].x = (_Float16)L.q_s[h][li * 8 + 2 * e];
+            U.q2[h][e].y = (_Float16)L.q_s[h][li * 8 + 2 * e + 1];
         }
-
-    float m[R], l[R], acc[R][8];
 #pragma unroll
     for (int h = 0; h < R; ++h) {
-        m[h] = -INFINITY;
-        l[h] = 0.0f;
+        U.m[h] = -INFINITY;
+        U.l[h] = 0.0f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[h][e] = 0.0f;
+        for (int e = 0; e < 8; ++e) U.acc[h][e] = 0.0f;
     }
-    // one chunk; LAST: positions past pos masked, a wave may hold no live position yet
-    auto chunk = [&](auto last_tag, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
-        constexpr bool LAST = decltype(last_tag)::value;
-        float sc[NP][R];
-        bool ok[NP];
+}
+// one chunk; LAST: positions past pos masked, a wave may hold no live position yet
+template <bool LAST>
+__device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
+    const int pg = threadIdx.x / LPP;
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    float sc[NP][R];
+    bool ok[NP];
 #pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            ok[pi] = !LAST || c * 64 + pi * 16 + pg <= pos;
-            const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
-#pragma unroll
-            for (int h = 0; h < R; ++h) {
-                float s = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kw[e]), q2[h][e], s, false);
-                s = group_sum<LPP>(s);
-                sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
-            }
-        }
+    for (int pi = 0; pi < NP; ++pi) {
+        ok[pi] = !LAST || c * 64 + pi * 16 + pg <= U.pos;
+        const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
 #pragma unroll
         for (int h = 0; h < R; ++h) {
-            float mc = sc[0][h];
+            float s = 0.0f;
 #pragma unroll
-            for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
-            mc = rows_max(mc);                      // this wave's 16 positions of the chunk
-            const float mn = fmaxf(m[h], mc);
-            if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
-            const float alpha = __expf(__fsub_rn(m[h], mn));
-            l[h] *= alpha;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[h][e] *= alpha;
-            m[h] = mn;
-        }
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) {
-            float v8[8];
-            unpack8_cvt(vr[pi], v8);
-#pragma unroll
-            for (int h = 0; h < R; ++h) {
-                const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], m[h])) : 0.0f;
-                l[h] += pr;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, acc[h][e]);
-            }
-        }
-    };
-    // the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
-    auto patch = [&](uint4 (&kr)[NP], uint4 (&vr)[NP]) {
-        if (pg == (pos & 15)) {
-            const uint4 kn4 = *reinterpret_cast<const uint4 *>(&L.kh_s[li * 8]);
-            const uint4 vn4 = *reinterpret_cast<const uint4 *>(&L.vh_s[li * 8]);
-#pragma unroll
-            for (int pi = 0; pi < NP; ++pi)
-                if (pi == ((pos & 63) >> 4)) { kr[pi] = kn4; vr[pi] = vn4; }
-        }
-    };
-    using whole = std::integral_constant<bool, false>;
-    using last = std::integral_constant<bool, true>;
-    for (int c0 = 0; c0 < nch; c0 += NB) {
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk c0 + k in slot k
-            const int c = c0 + k;
-            if (c < nch) {
-                if (c + NB - 1 < nch) issue(c + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
-                if (c + 1 < nch) chunk(whole{}, c, kq[k], vq[k]);
-                else { patch(kq[k], vq[k]); chunk(last{}, c, kq[k], vq[k]); }
-            }
+            for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, kw[e]), U.q2[h][e], s, false);
+            s = group_sum<LPP>(s);
+            sc[pi][h] = ok[pi] ? __fmul_rn(s, kq_scale) : -INFINITY;
         }
     }
-    // merge the four waves
 #pragma unroll
     for (int h = 0; h < R; ++h) {
-        const float ls = rows_sum(l[h]);
-        if (lane == 0) { L.wm[wave][h] = m[h]; L.wl[wave][h] = ls; }
+        float mc = sc[0][h];
+#pragma unroll
+        for (int pi = 1; pi < NP; ++pi) mc = fmaxf(mc, sc[pi][h]);
+        mc = rows_max(mc);                      // this wave's 16 positions of the chunk
+        const float mn = fmaxf(U.m[h], mc);
+        if (LAST && mn == -INFINITY) continue;  // no live position in this wave yet
+        const float alpha = __expf(__fsub_rn(U.m[h], mn));
+        U.l[h] *= alpha;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) U.acc[h][e] *= alpha;
+        U.m[h] = mn;
+    }
+#pragma unroll
+    for (int pi = 0; pi < NP; ++pi) {
+        float v8[8];
+        unpack8_cvt(vr[pi], v8);
+#pragma unroll
+        for (int h = 0; h < R; ++h) {
+            const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], U.m[h])) : 0.0f;
+            U.l[h] += pr;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) U.acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, U.acc[h][e]);
+        }
+    }
+}
+// the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
+__device__ __forceinline__ void patch(const Unit &U, uint4 (&kr)[NP], uint4 (&vr)[NP], const AttnSeqLds &L) {
+    const int t = threadIdx.x, pg = t / LPP, li = t % LPP;
+    if (pg == (U.pos & 15)) {
+        const uint4 kn4 = *reinterpret_cast<const uint4 *>(&L.kh_s[li * 8]);
+        const uint4 vn4 = *reinterpret_cast<const uint4 *>(&L.vh_s[li * 8]);
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi)
+            if (pi == ((U.pos & 63) >> 4)) { kr[pi] = kn4; vr[pi] = vn4; }
+    }
+}
+// merge the four waves' states (LDS), then the outputs
+template <bool VEC4, class Out>
+__device__ __forceinline__ void finish(const Unit &U, Out out, AttnSeqLds &L) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, li = t % LPP;
+#pragma unroll
+    for (int h = 0; h < R; ++h) {
+        const float ls = rows_sum(U.l[h]);
+        if (lane == 0) { L.wm[wave][h] = U.m[h]; L.wl[wave][h] = ls; }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const float a = rows_sum(acc[h][e]);
+            const float a = rows_sum(U.acc[h][e]);
             if (lane < 16) L.wa[wave][h][li * 8 + e] = a;
         }
     }
@@ -228,6 +223,36 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
     } else {
         for (int o = t; o < R * D; o += 256) out(o / D, o % D, merged(o / D, o % D));
     }
+}
+}  // namespace aseq
+
+//   kc/vc: this (layer, slot, kv head)'s cache [n_ctx][128] f16 (row pos is written here); rope_row: rope + pos * 128
+template <bool VEC4, int NB, class QkvOf, class Out>
+__device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc, const float *rope_row, const float *qn,
+                                            const float *kn, float eps, QkvOf qkv_of, Out out, AttnSeqLds &L) {
+    using namespace aseq;
+    static_assert(NB >= 2 && NB <= 4, "ring depth");
+    Unit U;
+    unit_init(U, pos, kc, vc);
+    uint4 kq[NB][NP], vq[NB][NP];
+#pragma unroll
+    for (int c = 0; c < NB - 1; ++c)
+        if (c < U.nch) issue(U, c, kq[c], vq[c]);
+    prologue(rope_row, qn, kn, eps, qkv_of, L);
+    __syncthreads();
+    start(U, L);
+    for (int c0 = 0; c0 < U.nch; c0 += NB) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk c0 + k in slot k
+            const int c = c0 + k;
+            if (c < U.nch) {
+                if (c + NB - 1 < U.nch) issue(U, c + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
+                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k]);
+                else { patch(U, kq[k], vq[k], L); chunk<true>(U, c, kq[k], vq[k]); }
+            }
+        }
+    }
+    finish<VEC4>(U, out, L);
 }
 
 }  // namespace q3t

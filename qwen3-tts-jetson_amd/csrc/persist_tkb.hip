@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             TPROF(ph_of(l, K_QKV), 2);
             after_job();
         }
-        // ---- ATT: units u = w, w + 256, ... (slot u / 8, kv head u % 8), the whole context of each
+        // ---- ATT: units u = w, w + 256 (slot u / 8, kv head u % 8), the whole context of each, in turn
         for (int u = w; u < nunits; u += G) {
             const int ub = u >> 3, g = u & 7;
             const int pos = p.pos[ub];
