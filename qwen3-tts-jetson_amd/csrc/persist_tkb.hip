@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             TPROF(ph_of(l, K_QKV), 3);
             epi_gran(X, SL.qkv, QKVN, 64 * rp, 32 * tt, X.tag(ph_of(l, K_QKV)));
             TPROF(ph_of(l, K_QKV), 2);
-            after_job();
+            pending = true;   // the O weights after the attention units: their polls and K/V streams go first
         }
         // ---- ATT: units u = w, w + 256 (slot u / 8, kv head u % 8), the whole context of each, in turn
         for (int u = w; u < nunits; u += G) {
