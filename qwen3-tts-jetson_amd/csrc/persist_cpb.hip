@@ -285,7 +285,9 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
             if (hq) {
                 after_rn();
                 const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
-                wait_flags_wg(X, K_GU, 24, [&](int i) { return 24 * z + i + 96 * tt; }, X.tag(ph_of(pass, l, K_GU)));
+                // each wave waits for the 6 gate/up jobs of its own K quarter only (units [768 z + 192 w, +192)): no barrier,
+                // no wave held by another quarter's late producer
+                wait_flags(X, K_GU, 6, [&](int i) { return 24 * z + 6 * wave + i + 96 * tt; }, X.tag(ph_of(pass, l, K_GU)));
                 mm_tile<3>(X, SL.h, INTER / 8, 768 * z, 32 * tt);
                 CPROF(ph_of(pass, l, K_DN), 3);
                 epi_gran(X, SL.sld + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(pass, l, K_DN)));

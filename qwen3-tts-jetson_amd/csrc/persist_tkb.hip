@@ -217,7 +217,8 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
         if (hq) {
             const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
             const int nv = min(32, p.S - 32 * tt);
-            wait_flags_wg(X, K_ATT, 2 * nv, [&](int i) { return (32 * tt + (i >> 1)) * NKV + 2 * z + (i & 1); }, X.tag(ph_of(l, K_ATT)));
+            // wave w multiplies head 4 z + w: the units of kv head 2 z + w / 2 of the tile's slots (its own wait, no barrier)
+            wait_flags(X, K_ATT, nv, [&](int i) { return (32 * tt + i) * NKV + 2 * z + (wave >> 1); }, X.tag(ph_of(l, K_ATT)));
             mm_tile<2>(X, SL.attn, NH * D / 8, 512 * z, 32 * tt);
             TPROF(ph_of(l, K_O), 3);
             epi_gran(X, SL.slo + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(l, K_O)));
@@ -257,7 +258,9 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
         if (hq) {
             flush();
             const int rp = w % 16, z = (w / 16) % 4, tt = w / 64;
-            wait_flags_wg(X, K_GU, 24, [&](int i) { return 24 * z + i + 96 * tt; }, X.tag(ph_of(l, K_GU)));
+            // each wave waits for the 6 gate/up jobs of its own K quarter only (units [768 z + 192 w, +192)): no barrier,
+                // no wave held by another quarter's late producer
+                wait_flags(X, K_GU, 6, [&](int i) { return 24 * z + 6 * wave + i + 96 * tt; }, X.tag(ph_of(l, K_GU)));
             mm_tile<3>(X, SL.h, INTER / 8, 768 * z, 32 * tt);
             TPROF(ph_of(l, K_DN), 3);
             epi_gran(X, SL.sld + (size_t)z * SMAX * H * 8, H, 64 * rp, 32 * tt, X.tag(ph_of(l, K_DN)));
