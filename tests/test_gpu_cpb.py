@@ -101,3 +101,20 @@ def test_cpb_stage_time(engines):
     tg = eg.time_stage(1, 64, 0, 5)
     assert ep.persist_status() == 0
     print(f"64-slot CP frame: persistent {tp:.3f} ms, per-op {tg:.3f} ms")
+
+
+def test_cpb_slot_invariance(engines):
+    """a slot's codes do not depend on how many slots the frame runs: the first 8 slots of a 64-slot frame equal an
+    8-slot frame on the same inputs (one token tile vs two; the MFMA columns, split-K slices and norms are per token)"""
+    ep, _ = engines
+    H = ep.cfg["hidden"]
+    rng = np.random.default_rng(77)
+    hid = (rng.standard_normal((64, H)) * 1.5).astype(np.float32)
+    cb0 = rng.integers(0, 2048, 64).astype(np.int32)
+    for temperature in (0.0, 0.9):
+        c64 = ep.codepred_frame(hid, cb0, temperature=temperature, top_k=50, seed=9, frame=3)
+        c8 = ep.codepred_frame(hid[:8], cb0[:8], temperature=temperature, top_k=50, seed=9, frame=3)
+        c33 = ep.codepred_frame(hid[:33], cb0[:33], temperature=temperature, top_k=50, seed=9, frame=3)
+        assert np.array_equal(c64[:8], c8), temperature
+        assert np.array_equal(c64[:33], c33), temperature
+    assert ep.persist_status() == 0

@@ -100,3 +100,18 @@ def test_tkb_stage_time(engines):
     tg = eg.time_stage(0, 64, 140, 5)
     assert ep.persist_status() == 0
     print(f"64-slot talker step at position 140: persistent {tp:.3f} ms, per-op {tg:.3f} ms")
+
+
+def test_tkb_slot_invariance(engines):
+    """a slot's hidden state and logits do not depend on how many slots the step runs: the first 16 (and 33) slots of
+    a 64-slot step equal a 16-slot (33-slot) step on the same inputs and positions"""
+    ep, _ = engines
+    H = ep.cfg["hidden"]
+    rng = np.random.default_rng(78)
+    pos = (np.arange(64) % 9 + 40).astype(np.int32)
+    x = (rng.standard_normal((64, H)) * 0.5).astype(np.float32)
+    h64, l64 = ep.talker_forward(x, pos)
+    for n in (16, 33):
+        hn, ln = ep.talker_forward(x[:n], pos[:n])   # the same K/V rows rewritten with the same values
+        assert np.array_equal(h64[:n], hn) and np.array_equal(l64[:n], ln), n
+    assert ep.persist_status() == 0
