@@ -321,6 +321,10 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
         if (slot) {   // both halves select (the same token); the even one commits it
             const uint32_t tg = X.tag(ph_of(pass, NLC, K_HEAD));
             CPROF(ph_of(pass, NLC, K_HEAD), 0);
+            SelectSpec sp = p.sel;
+            sp.step = pass - 1;
+            SelPre pre;   // the selection's per-slot inputs (done, frame, seed, utterance) before the poll, off the chain
+            sel_prefetch<SEL_CP>(sp, b, pre);
             u32x4_t lr[4];   // thread t: logits 8t .. 8t+7 (select_token's exact-width ownership, V = 2048)
             poll_gran<4>(X, tg, lr, [&](u32x4_t (&r)[4]) {
 #pragma unroll
@@ -333,9 +337,7 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
             for (int k = 0; k < 4; ++k) { v[2 * k] = __uint_as_float(lr[k].x); v[2 * k + 1] = __uint_as_float(lr[k].z); }
 #pragma unroll
             for (int e = 8; e < SEL_VPT_MAX; ++e) v[e] = -INFINITY;
-            SelectSpec sp = p.sel;
-            sp.step = pass - 1;
-            const int tok = select_token_regs<SEL_CP>(sp, v, b, S.sel);   // -1: slot done
+            const int tok = select_token_pre<SEL_CP>(sp, pre, v, S.sel);   // -1: slot done
             if (t == 0 && tok >= 0) {
                 if (rn) select_commit(sp, b, tok);
                 S.toks[pass] = tok;

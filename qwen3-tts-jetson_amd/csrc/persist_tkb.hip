@@ -286,6 +286,8 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
     if (rn) {
         const uint32_t tg = X.tag(ph_of(NL, K_HEAD));
         TPROF(ph_of(NL, K_HEAD), 0);
+        SelPre pre;   // the selection's per-slot inputs (done, frame, seed, seen bytes) before the poll, off the chain
+        if (p.select) sel_prefetch<SEL_CB0>(p.sel, b, pre);
         u32x4_t lr[VPT / 2];   // thread t: logits VPT t .. VPT t + VPT - 1 (select_token's exact-width ownership, V = 3072)
         poll_gran<VPT / 2>(X, tg, lr, [&](u32x4_t (&r)[VPT / 2]) {
 #pragma unroll
@@ -304,7 +306,7 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             for (int k = 0; k < VPT / 4; ++k) *reinterpret_cast<float4 *>(row + 4 * k) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
         }
         if (p.select) {
-            const int tok = select_token_regs<SEL_CB0>(p.sel, v, b, S.sel);   // -1: slot done
+            const int tok = select_token_pre<SEL_CB0>(p.sel, pre, v, S.sel);   // -1: slot done
             if (t == 0 && tok >= 0) select_commit(p.sel, b, tok);
         }
         TPROF(ph_of(NL, K_HEAD), 3);
