@@ -132,11 +132,19 @@ template <bool LAST>
 __device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
     const int pg = threadIdx.x / LPP;
     const float kq_scale = 1.0f / sqrtf((float)D);
+    // the last chunk's passes past pos hold no live position for any lane: they are skipped (exactly: their scores
+    // are -inf, their exponentials 0, and adding 0 leaves l and acc -- never -0 -- unchanged)
+    const int npi = LAST ? ((U.pos & 63) >> 4) + 1 : NP;
     float sc[NP][R];
     bool ok[NP];
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
         ok[pi] = !LAST || c * 64 + pi * 16 + pg <= U.pos;
+        if (LAST && pi >= npi) {
+#pragma unroll
+            for (int h = 0; h < R; ++h) sc[pi][h] = -INFINITY;
+            continue;
+        }
         const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
 #pragma unroll
         for (int h = 0; h < R; ++h) {
@@ -163,6 +171,7 @@ __device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], con
     }
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
+        if (LAST && pi >= npi) continue;
         float v8[8];
         unpack8_cvt(vr[pi], v8);
 #pragma unroll
