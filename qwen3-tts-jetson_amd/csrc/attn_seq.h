@@ -264,4 +264,60 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
     finish<VEC4>(U, out, L);
 }
 
+// nu (1 or 2) units of one workgroup in turn as ONE chunk stream through the NB register ring: the second unit's first
+// chunks are issued during the first unit's last chunks, so they land while it merges and publishes.  Each unit's
+// arithmetic is attn_seq_wg's.  unit(k, pos, kc, vc, rope_row) describes unit k; qkv_of(k, v, x) / out(k, h, d0, y)
+// as attn_seq_wg's (VEC4 stores); done(k) runs on the whole workgroup after unit k's outputs (its publish).
+template <int NB, class UnitOf, class QkvOf, class Out, class Done>
+__device__ __forceinline__ void attn_seq_stream(int nu, UnitOf unit_of, const float *qn, const float *kn, float eps,
+                                                QkvOf qkv_of, Out out, Done done, AttnSeqLds &L) {
+    using namespace aseq;
+    static_assert(NB >= 2 && NB <= 4, "ring depth");
+    Unit Ud[2];   // descriptors (pos, nch, caches) of both units; the softmax state lives in U
+    const float *rope[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        int pos = 0;
+        uint16_t *kc = nullptr, *vc = nullptr;
+        rope[k] = nullptr;
+        if (k < nu) unit_of(k, pos, kc, vc, rope[k]);
+        unit_init(Ud[k], pos, kc, vc);
+    }
+    const int n0 = Ud[0].nch, total = n0 + (nu > 1 ? Ud[1].nch : 0);
+    auto issue_g = [&](int g, uint4 (&kr)[NP], uint4 (&vr)[NP]) {   // chunk g of the stream
+        if (g < n0) issue(Ud[0], g, kr, vr);
+        else issue(Ud[1], g - n0, kr, vr);
+    };
+    uint4 kq[NB][NP], vq[NB][NP];
+#pragma unroll
+    for (int g = 0; g < NB - 1; ++g)
+        if (g < total) issue_g(g, kq[g], vq[g]);
+    Unit U = Ud[0];
+    prologue(rope[0], qn, kn, eps, [&](int v, float (&x)[2]) { qkv_of(0, v, x); }, L);
+    __syncthreads();
+    start(U, L);
+    for (int g0 = 0; g0 < total; g0 += NB) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk g0 + k in slot k
+            const int g = g0 + k;
+            if (g < total) {
+                if (g + NB - 1 < total) issue_g(g + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
+                if (g == n0) {   // unit boundary: the first unit's merge, outputs and publish, the second's prologue
+                    finish<true>(U, [&](int h, int d0, const float (&y)[4]) { out(0, h, d0, y); }, L);
+                    done(0);
+                    U = Ud[1];
+                    prologue(rope[1], qn, kn, eps, [&](int v, float (&x)[2]) { qkv_of(1, v, x); }, L);
+                    __syncthreads();
+                    start(U, L);
+                }
+                const int c = g < n0 ? g : g - n0;
+                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k]);
+                else { patch(U, kq[k], vq[k], L); chunk<true>(U, c, kq[k], vq[k]); }
+            }
+        }
+    }
+    finish<true>(U, [&](int h, int d0, const float (&y)[4]) { out(nu - 1, h, d0, y); }, L);
+    done(nu - 1);
+}
+
 }  // namespace q3t

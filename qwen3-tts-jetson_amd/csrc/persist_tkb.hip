@@ -182,35 +182,45 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             TPROF(ph_of(l, K_QKV), 2);
             pending = true;   // the O weights after the attention units: their polls and K/V streams go first
         }
-        // ---- ATT: units u = w, w + 256 (slot u / 8, kv head u % 8), the whole context of each, in turn
-        for (int u = w; u < nunits; u += G) {
-            const int ub = u >> 3, g = u & 7;
-            const int pos = p.pos[ub];
-            const size_t hoff = (size_t)l * p.kv_layer + ((size_t)ub * NKV + g) * p.n_ctx * D;
+        // ---- ATT: units u = w, w + 256 (slot u / 8, kv head u % 8), the whole context of each, in turn as one chunk
+        // stream (the second unit's first chunks in flight during the first unit's tail)
+        if (w < nunits) {
             const uint32_t tq = X.tag(ph_of(l, K_QKV));
-            if (u == w) TPROF(ph_of(l, K_QKV), 0);
-            attn_seq_wg<true, TKB_NB>(
-                pos, p.kc + hoff, p.vc + hoff, p.rope + (size_t)pos * D, Lw.qn, Lw.kn, p.eps,
-                [&](int v, float (&xv)[2]) {   // wave v: q head 2g + v (v < 2), k (2), v (3) of slot ub: 2 granules per lane
+            const int nu = w + G < nunits ? 2 : 1, g = w & 7;
+            const int ub[2] = {w >> 3, (w + G) >> 3};
+            TPROF(ph_of(l, K_QKV), 0);
+            attn_seq_stream<TKB_NB>(
+                nu,
+                [&](int k, int &pos, uint16_t *&kc, uint16_t *&vc, const float *&rope_row) {
+                    pos = p.pos[ub[k]];
+                    const size_t hoff = (size_t)l * p.kv_layer + ((size_t)ub[k] * NKV + g) * p.n_ctx * D;
+                    kc = p.kc + hoff;
+                    vc = p.vc + hoff;
+                    rope_row = p.rope + (size_t)pos * D;
+                },
+                Lw.qn, Lw.kn, p.eps,
+                [&](int k, int v, float (&xv)[2]) {   // wave v: q head 2g + v (v < 2), k (2), v (3) of slot ub[k]
                     const int row = v < 2 ? (2 * g + v) * D : v == 2 ? (NH + g) * D : (NH + NKV + g) * D;
                     u32x4_t gq[1];
                     poll_gran<1>(X, tq, gq, [&](u32x4_t (&r)[1]) {
-                        const size_t o = SL.qkv + ((size_t)ub * QKVN + row + lane) * 8;
+                        const size_t o = SL.qkv + ((size_t)ub[k] * QKVN + row + lane) * 8;
                         const u32x2_t a = __builtin_amdgcn_raw_buffer_load_b64(X.rs, (int)o, 0, SC1V);
                         const u32x2_t c = __builtin_amdgcn_raw_buffer_load_b64(X.rs, (int)(o + 64 * 8), 0, SC1V);
                         r[0] = u32x4_t{a.x, a.y, c.x, c.y};
                     });
-                    if (u == w && v == 0) TPROF(ph_of(l, K_QKV), 1);
+                    if (k == 0 && v == 0) TPROF(ph_of(l, K_QKV), 1);
                     xv[0] = __uint_as_float(gq[0].x);
                     xv[1] = __uint_as_float(gq[0].z);
                 },
-                [&](int hd, int d0, const float (&y)[4]) {   // 4 halves of the slot's attention row, fragment order
+                [&](int k, int hd, int d0, const float (&y)[4]) {   // 4 halves of the slot's attention row, fragment order
                     const u32x2_t o = {(uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16), (uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16)};
-                    __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.attn + fragoff(NH * D / 8, ub, (2 * g + hd) * D + d0), 0, SC1);
+                    __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.attn + fragoff(NH * D / 8, ub[k], (2 * g + hd) * D + d0), 0, SC1);
+                },
+                [&](int k) {
+                    if (k == 0) TPROF(ph_of(l, K_ATT), 3);
+                    publish(X, K_ATT, w + k * G, X.tag(ph_of(l, K_ATT)));
                 },
                 S.att);
-            if (u == w) TPROF(ph_of(l, K_ATT), 3);
-            publish(X, K_ATT, u, X.tag(ph_of(l, K_ATT)));
         }
         flush();
         // ---- O: split-K slab z of rows 64 rp .. +63, tile tt: heads 4z .. 4z+3 = kv heads 2z, 2z+1 of the tile's slots
