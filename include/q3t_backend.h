@@ -126,7 +126,8 @@ int q3t_synchronize(q3t_ctx *ctx);
 int q3t_last_timing(const q3t_ctx *ctx, double *prefill_ms, double *frames_ms);
 
 /* replay the captured stage graph (0 = talker decode step, 1 = 16-pass code-predictor frame) `iters` times at
- * KV position `pos` for n_slots slots; *ms = mean device time per replay (HIP events on the context stream) */
+ * KV position `pos` for n_slots slots; *ms = mean device time per replay (an event pair around each replay on the
+ * context stream: the replay's own duration, not the host-side gap between two graph launches) */
 int q3t_time_stage(q3t_ctx *ctx, int stage, int n_slots, int pos, int iters, double *ms);
 /* the single-slot talker step and code-predictor frame as persistent launches (persist.hip, no reference
  * counterpart: they replace the per-op graphs of TTSTransformer::forward_step / TRTCodePredictor at batch 1):

@@ -2127,18 +2127,24 @@ bool Engine::time_stage(int stage, int S, int pos, int iters, double *ms) {
     if (stage == 0) { if (!graph_for(g_talker_, S, &Engine::enqueue_talker_step)) return false; g = g_talker_[S]; }
     else { if (!graph_for(g_cp_, S, &Engine::enqueue_cp_only)) return false; g = g_cp_[S]; }
     Q3T_HIP(hipGraphLaunch(g, stream_));   // warm
-    hipEvent_t a, b;
-    Q3T_HIP(hipEventCreate(&a));
-    Q3T_HIP(hipEventCreate(&b));
-    Q3T_HIP(hipEventRecord(a, stream_));
-    for (int i = 0; i < iters; ++i) Q3T_HIP(hipGraphLaunch(g, stream_));
-    Q3T_HIP(hipEventRecord(b, stream_));
-    Q3T_HIP(hipEventSynchronize(b));
-    float t = 0;
-    hipEventElapsedTime(&t, a, b);
-    hipEventDestroy(a);
-    hipEventDestroy(b);
-    *ms = t / iters;
+    // one event pair around EACH replay, on the stream the kernels run on: the mean is the replay's own duration (for
+    // the persistent stages, the one kernel's), without the host-side gap between two graph launches
+    std::vector<hipEvent_t> ev(2 * (size_t)iters, nullptr);
+    for (hipEvent_t &e : ev) Q3T_HIP(hipEventCreate(&e));
+    for (int i = 0; i < iters; ++i) {
+        Q3T_HIP(hipEventRecord(ev[2 * i], stream_));
+        Q3T_HIP(hipGraphLaunch(g, stream_));
+        Q3T_HIP(hipEventRecord(ev[2 * i + 1], stream_));
+    }
+    Q3T_HIP(hipEventSynchronize(ev.back()));
+    double sum = 0.0;
+    for (int i = 0; i < iters; ++i) {
+        float t = 0;
+        hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]);
+        sum += t;
+    }
+    for (hipEvent_t e : ev) hipEventDestroy(e);
+    *ms = sum / iters;
     if (persist_error()) {   // time the launch-per-op fallback instead of a faulted persistent launch
         if (!persist_recover()) return false;
         return time_stage(stage, S, pos, iters, ms);
