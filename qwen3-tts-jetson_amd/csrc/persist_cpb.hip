@@ -376,11 +376,10 @@ __global__ void __launch_bounds__(256, 1) k_cpb(const CpbParams p) {
                     hh2.y = (uint32_t)f2h(y2) | ((uint32_t)f2h(y3) << 16);
                     *reinterpret_cast<uint2 *>(p.txn + (size_t)b * H + 4 * t) = hh2;
                 }
-                if (b == 0 && t == 0)   // every workgroup has read seq: each one's first job fed this last selection
-                    __hip_atomic_store(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
+    exit_ticket(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq);
 }
 
 size_t cpb_lds() { return std::max(sizeof(BLds), (size_t)96 * 1024); }   // > 80 KB: one workgroup per CU
@@ -411,6 +410,7 @@ bool cpb_clear(uint8_t *state, hipStream_t s) {   // after a fault: zero the fla
     const StateLayout L;
     Q3T_HIP(hipMemsetAsync(state + L.flags, 0, L.ctr - L.flags, s));
     Q3T_HIP(hipMemsetAsync(state + L.ctr + 32 * 4, 0, 4, s));
+    Q3T_HIP(hipMemsetAsync(state + L.ctr + 48 * 4, 0, 4, s));   // the exit ticket
     return true;
 }
 

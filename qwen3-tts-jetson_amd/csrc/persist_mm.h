@@ -102,6 +102,19 @@ __device__ __forceinline__ void publish(Ctx &X, int kind, int j, uint32_t tag) {
     CPROF((int)((tag - 1u) & 1023u), 2);
 }
 
+// the launch's LAST workgroup to finish bumps seq (ctr[0]; an exit ticket in ctr[48]): every workgroup has read seq by
+// then, whatever order the workgroups were dispatched in.  Every workgroup runs it, idle ones included
+__device__ __forceinline__ void exit_ticket(unsigned *ctr, unsigned seq) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned *done = ctr + 48;
+        if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // spin until every granule a lane loads (issue(r) fills r) carries `tag` (bounded, as wait_flags)
 template <int M, class Issue>
 __device__ __forceinline__ void poll_gran(Ctx &X, uint32_t tag, u32x4_t (&r)[M], Issue issue) {

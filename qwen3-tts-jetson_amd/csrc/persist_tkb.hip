@@ -320,11 +320,8 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
             if (t == 0 && tok >= 0) select_commit(p.sel, b, tok);
         }
         TPROF(ph_of(NL, K_HEAD), 3);
-        if (b == 0) {   // every workgroup has read seq: each one's first job fed this slot's logits
-            __syncthreads();
-            if (t == 0) __hip_atomic_store(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
+    exit_ticket(reinterpret_cast<unsigned *>(p.state + SL.ctr), X.seq);
 }
 
 size_t tkb_lds() { return std::max(sizeof(BLds), (size_t)96 * 1024); }   // > 80 KB: one workgroup per CU
@@ -355,6 +352,7 @@ bool tkb_clear(uint8_t *state, hipStream_t s) {   // after a fault: zero the fla
     const StateLayout L;
     Q3T_HIP(hipMemsetAsync(state + L.flags, 0, L.ctr - L.flags, s));
     Q3T_HIP(hipMemsetAsync(state + L.ctr + 32 * 4, 0, 4, s));
+    Q3T_HIP(hipMemsetAsync(state + L.ctr + 48 * 4, 0, 4, s));   // the exit ticket
     return true;
 }
 
