@@ -8,7 +8,7 @@
 // chunk in flight per CU bounded it at ~20 GB/s per CU); each wave keeps its own online-softmax state (max, sum, 8-dim accumulator per head) over its 16 positions of
 // every chunk, so no barrier is taken per chunk; the four waves merge once at the end.  Scores are v_dot2_f32_f16 on the
 // packed K registers against the f16-exact q, exponentials v_exp_f32 (__expf); every chunk but the last is whole (all
-// 64 positions <= pos: no masks), and the new K/V row (pos) is patched into the last chunk's registers from LDS.
+// 64 positions <= pos: no masks), and the new K/V row (pos) is read from LDS in place of the last chunk's loaded one.
 //
 // The caller supplies the raw QKV values (qkv_of: wave v < 2 q head 2g + v, v = 2 the new k, v = 3 the new v; lanes
 // lane and lane + 64) -- K/V chunk 0 is in flight before it is called -- and the output store (out: one value, or with
@@ -63,13 +63,16 @@ __device__ __forceinline__ void unit_init(Unit &U, int pos, uint16_t *kc, uint16
     U.kc = kc;
     U.vc = vc;
 }
+// chunk c >= U.nch: a placeholder issue (the ring's steps past the end) -- the same load instructions, every lane on the
+// cache's first 16 bytes (one line per instruction), the registers never read
 __device__ __forceinline__ void issue(const Unit &U, int c, uint4 (&kr)[NP], uint4 (&vr)[NP]) {
     const int t = threadIdx.x, pg = t / LPP, li = t % LPP;
+    const bool live = c < U.nch;
 #pragma unroll
     for (int pi = 0; pi < NP; ++pi) {
-        const int j = min(c * 64 + pi * 16 + pg, U.pos);
-        kr[pi] = ld16(U.kc + (size_t)j * D + li * 8);
-        vr[pi] = ld16(U.vc + (size_t)j * D + li * 8);
+        const int o = live ? min(c * 64 + pi * 16 + pg, U.pos) * D + li * 8 : 0;
+        kr[pi] = ld16(U.kc + o);
+        vr[pi] = ld16(U.vc + o);
     }
 }
 // head RMSNorm + NEOX RoPE of the R q heads and the new k (k_attn arithmetic); the new v f16-rounded (wave v: vector v)
@@ -128,9 +131,17 @@ __device__ __forceinline__ void start(Unit &U, const AttnSeqLds &L) {
     }
 }
 // one chunk; LAST: positions past pos masked, a wave may hold no live position yet
+// The new row (pos, in LDS since start()) stands in for the last chunk's loaded one at its use: pass (pos % 64) / 16,
+// position group pos % 16 (the ring registers are only read, so the compiler keeps no copies of them)
 template <bool LAST>
-__device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP]) {
-    const int pg = threadIdx.x / LPP;
+__device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], const uint4 (&vr)[NP], const AttnSeqLds &L) {
+    const int pg = threadIdx.x / LPP, li = threadIdx.x % LPP;
+    uint4 kn4, vn4;
+    if constexpr (LAST) {
+        kn4 = *reinterpret_cast<const uint4 *>(&L.kh_s[li * 8]);
+        vn4 = *reinterpret_cast<const uint4 *>(&L.vh_s[li * 8]);
+    }
+    auto isnew = [&](int pi) { return LAST && pi == ((U.pos & 63) >> 4) && pg == (U.pos & 15); };
     const float kq_scale = 1.0f / sqrtf((float)D);
     // the last chunk's passes past pos hold no live position for any lane: they are skipped (exactly: their scores
     // are -inf, their exponentials 0, and adding 0 leaves l and acc -- never -0 -- unchanged)
@@ -145,7 +156,8 @@ __device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], con
             for (int h = 0; h < R; ++h) sc[pi][h] = -INFINITY;
             continue;
         }
-        const uint32_t kw[4] = {kr[pi].x, kr[pi].y, kr[pi].z, kr[pi].w};
+        const uint4 kv = isnew(pi) ? kn4 : kr[pi];
+        const uint32_t kw[4] = {kv.x, kv.y, kv.z, kv.w};
 #pragma unroll
         for (int h = 0; h < R; ++h) {
             float s = 0.0f;
@@ -173,7 +185,7 @@ __device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], con
     for (int pi = 0; pi < NP; ++pi) {
         if (LAST && pi >= npi) continue;
         float v8[8];
-        unpack8_cvt(vr[pi], v8);
+        unpack8_cvt(isnew(pi) ? vn4 : vr[pi], v8);
 #pragma unroll
         for (int h = 0; h < R; ++h) {
             const float pr = ok[pi] ? __expf(__fsub_rn(sc[pi][h], U.m[h])) : 0.0f;
@@ -181,17 +193,6 @@ __device__ __forceinline__ void chunk(Unit &U, int c, const uint4 (&kr)[NP], con
 #pragma unroll
             for (int e = 0; e < 8; ++e) U.acc[h][e] = __fmaf_rn(pr, ok[pi] ? v8[e] : 0.0f, U.acc[h][e]);
         }
-    }
-}
-// the new row into the last chunk's registers (pass (pos % 64) / 16, position group pos % 16)
-__device__ __forceinline__ void patch(const Unit &U, uint4 (&kr)[NP], uint4 (&vr)[NP], const AttnSeqLds &L) {
-    const int t = threadIdx.x, pg = t / LPP, li = t % LPP;
-    if (pg == (U.pos & 15)) {
-        const uint4 kn4 = *reinterpret_cast<const uint4 *>(&L.kh_s[li * 8]);
-        const uint4 vn4 = *reinterpret_cast<const uint4 *>(&L.vh_s[li * 8]);
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi)
-            if (pi == ((U.pos & 63) >> 4)) { kr[pi] = kn4; vr[pi] = vn4; }
     }
 }
 // merge the four waves' states (LDS), then the outputs
@@ -244,9 +245,12 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
     Unit U;
     unit_init(U, pos, kc, vc);
     uint4 kq[NB][NP], vq[NB][NP];
+    // every ring step issues one chunk, unconditionally (past the end: a placeholder, see issue), so every path
+    // to a chunk's first use has the same NB - 1 chunks issued after it and the compiler's wait is vmcnt(8 (NB - 1)),
+    // not vmcnt(0) (a conditional issue made the path without it the wait's worst case: every chunk then waited for
+    // the chunks issued after it, and the ring held one chunk in flight)
 #pragma unroll
-    for (int c = 0; c < NB - 1; ++c)
-        if (c < U.nch) issue(U, c, kq[c], vq[c]);
+    for (int c = 0; c < NB - 1; ++c) issue(U, c, kq[c], vq[c]);
     prologue(rope_row, qn, kn, eps, qkv_of, L);
     __syncthreads();
     start(U, L);
@@ -254,10 +258,10 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
 #pragma unroll
         for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk c0 + k in slot k
             const int c = c0 + k;
+            issue(U, c + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
             if (c < U.nch) {
-                if (c + NB - 1 < U.nch) issue(U, c + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
-                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k]);
-                else { patch(U, kq[k], vq[k], L); chunk<true>(U, c, kq[k], vq[k]); }
+                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k], L);
+                else chunk<true>(U, c, kq[k], vq[k], L);
             }
         }
     }
@@ -266,8 +270,8 @@ __device__ __forceinline__ void attn_seq_wg(int pos, uint16_t *kc, uint16_t *vc,
 
 // nu (1 or 2) units of one workgroup in turn as ONE chunk stream through the NB register ring: the second unit's first
 // chunks are issued during the first unit's last chunks, so they land while it merges and publishes.  Each unit's
-// arithmetic is attn_seq_wg's.  unit(k, pos, kc, vc, rope_row) describes unit k; qkv_of(k, v, x) / out(k, h, d0, y)
-// as attn_seq_wg's (VEC4 stores); done(k) runs on the whole workgroup after unit k's outputs (its publish).
+// arithmetic is attn_seq_wg's.  unit(k, pos, kc, vc, rope_row) describes unit k; qkv_of(k, v, x) / out(k, h, d, y)
+// as attn_seq_wg's (one output dimension per thread: the merge on all four waves); done(k) runs on the whole workgroup after unit k's outputs (its publish).
 template <int NB, class UnitOf, class QkvOf, class Out, class Done>
 __device__ __forceinline__ void attn_seq_stream(int nu, UnitOf unit_of, const float *qn, const float *kn, float eps,
                                                 QkvOf qkv_of, Out out, Done done, AttnSeqLds &L) {
@@ -284,14 +288,15 @@ __device__ __forceinline__ void attn_seq_stream(int nu, UnitOf unit_of, const fl
         unit_init(Ud[k], pos, kc, vc);
     }
     const int n0 = Ud[0].nch, total = n0 + (nu > 1 ? Ud[1].nch : 0);
-    auto issue_g = [&](int g, uint4 (&kr)[NP], uint4 (&vr)[NP]) {   // chunk g of the stream
-        if (g < n0) issue(Ud[0], g, kr, vr);
+    auto issue_g = [&](int g, uint4 (&kr)[NP], uint4 (&vr)[NP]) {   // chunk g of the stream (g >= total: placeholder)
+        if (g < n0 || g >= total) issue(Ud[0], g < n0 ? g : n0, kr, vr);
         else issue(Ud[1], g - n0, kr, vr);
     };
     uint4 kq[NB][NP], vq[NB][NP];
+    // unconditional issues (placeholders past the stream's end): the compiler's waits count NB - 1 chunks in flight
+    // (attn_seq_wg)
 #pragma unroll
-    for (int g = 0; g < NB - 1; ++g)
-        if (g < total) issue_g(g, kq[g], vq[g]);
+    for (int g = 0; g < NB - 1; ++g) issue_g(g, kq[g], vq[g]);
     Unit U = Ud[0];
     prologue(rope[0], qn, kn, eps, [&](int v, float (&x)[2]) { qkv_of(0, v, x); }, L);
     __syncthreads();
@@ -300,10 +305,10 @@ __device__ __forceinline__ void attn_seq_stream(int nu, UnitOf unit_of, const fl
 #pragma unroll
         for (int k = 0; k < NB; ++k) {   // ring slots are compile-time: chunk g0 + k in slot k
             const int g = g0 + k;
+            issue_g(g + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
             if (g < total) {
-                if (g + NB - 1 < total) issue_g(g + NB - 1, kq[(k + NB - 1) % NB], vq[(k + NB - 1) % NB]);
                 if (g == n0) {   // unit boundary: the first unit's merge, outputs and publish, the second's prologue
-                    finish<true>(U, [&](int h, int d0, const float (&y)[4]) { out(0, h, d0, y); }, L);
+                    finish<false>(U, [&](int h, int d, float y) { out(0, h, d, y); }, L);
                     done(0);
                     U = Ud[1];
                     prologue(rope[1], qn, kn, eps, [&](int v, float (&x)[2]) { qkv_of(1, v, x); }, L);
@@ -311,12 +316,12 @@ __device__ __forceinline__ void attn_seq_stream(int nu, UnitOf unit_of, const fl
                     start(U, L);
                 }
                 const int c = g < n0 ? g : g - n0;
-                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k]);
-                else { patch(U, kq[k], vq[k], L); chunk<true>(U, c, kq[k], vq[k]); }
+                if (c + 1 < U.nch) chunk<false>(U, c, kq[k], vq[k], L);
+                else chunk<true>(U, c, kq[k], vq[k], L);
             }
         }
     }
-    finish<true>(U, [&](int h, int d0, const float (&y)[4]) { out(nu - 1, h, d0, y); }, L);
+    finish<false>(U, [&](int h, int d, float y) { out(nu - 1, h, d, y); }, L);
     done(nu - 1);
 }
 

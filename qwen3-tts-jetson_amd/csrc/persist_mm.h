@@ -29,7 +29,7 @@ constexpr int FLAGS_PER_KIND = 512;   // flag words per hand-off kind
 // K / 8.  A consumer wave's load instruction for chunk column (c, j) then reads two runs of 32 consecutive chunks (whole
 // 64-byte sectors) instead of one 16-byte piece of 64 different sectors: sc1 loads are not merged in L1, so the
 // row-major order moved every activation byte four times over the CU's L2 path.
-__device__ __forceinline__ int fragoff(int kch, int tok, int k) {   // byte offset of half k (k % 4 == 0) of token tok
+__device__ __forceinline__ int fragoff(int kch, int tok, int k) {   // byte offset of half k of token tok (8-byte stores: k % 4 == 0)
     return (((tok >> 5) * kch + (k >> 3)) * 32 + (tok & 31)) * 16 + (k & 7) * 2;
 }
 

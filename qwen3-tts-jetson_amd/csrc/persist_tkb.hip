@@ -212,9 +212,8 @@ __global__ void __launch_bounds__(256, 1) k_tkb(const TkbParams p) {
                     xv[0] = __uint_as_float(gq[0].x);
                     xv[1] = __uint_as_float(gq[0].z);
                 },
-                [&](int k, int hd, int d0, const float (&y)[4]) {   // 4 halves of the slot's attention row, fragment order
-                    const u32x2_t o = {(uint32_t)f2h(y[0]) | ((uint32_t)f2h(y[1]) << 16), (uint32_t)f2h(y[2]) | ((uint32_t)f2h(y[3]) << 16)};
-                    __builtin_amdgcn_raw_buffer_store_b64(o, X.rs, (int)SL.attn + fragoff(NH * D / 8, ub[k], (2 * g + hd) * D + d0), 0, SC1);
+                [&](int k, int hd, int d, float y) {   // one half of the slot's attention row, fragment order
+                    __builtin_amdgcn_raw_buffer_store_b16(f2h(y), X.rs, (int)SL.attn + fragoff(NH * D / 8, ub[k], (2 * g + hd) * D + d), 0, SC1);
                 },
                 [&](int k) {
                     if (k == 0) TPROF(ph_of(l, K_ATT), 3);
