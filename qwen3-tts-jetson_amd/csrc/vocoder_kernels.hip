@@ -388,6 +388,235 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     }
 }
 
+// ======================================================================================= pipelined multi-tap conv
+// k_conv_mt's 256-row x NT-channel tile of a stride-1 multi-tap conv (the residual units' dilated 7-tap convs of the
+// wide decoder blocks), the same MFMA fragments in the same (K chunk, tap, k) order -- so the same bits -- with its
+// K-chunk staging moved off the critical path: the input window and the chunk's weights of every tap go straight to
+// LDS by buffer-load-to-LDS DMA (no registers, no synchronous weight load: k_conv_mt's 7-tap tile loaded its weights
+// at the top of each chunk and waited for them, since registering them one chunk ahead spilled), into two stages, so
+// chunk c + 1 lands while chunk c multiplies.  One workgroup per CU (2 x 64 KB of stages).
+//   stage: window rows [320][4 x 16 B] (rows past the window, before the sequence or past T_in: zeros from the
+//   buffer's range check), weights [tap][NT][4 x 16 B] padded to 44 KB; 16-byte slot q of row r sits at slot
+//   q ^ ((r >> 2) & 3) (conflict-free ds_read_b128 fragment reads without row padding: a DMA fills 1 KB contiguously)
+// Every thread issues exactly 16 DMA instructions per stage (5 window, 11 weight; placeholders out of range), so the
+// wait for the previous stage is vmcnt(16).
+template <int RB> struct PdGeom {   // stage geometry of k_conv_pd<RB>: window rows 128 RB + 64, weights 44 KB
+    static constexpr int XROWS = 128 * RB + 64, XSLOTS = XROWS * 4, WSLOTS = 44 * 64, STAGE = (XSLOTS + WSLOTS) * 16;
+    static constexpr int XI = XSLOTS / 256, WI = WSLOTS / 256;   // DMA instructions per thread and stage
+    static_assert(XSLOTS % 256 == 0 && 2 * STAGE <= 160 * 1024, "stages");
+};
+constexpr unsigned PD_OOB = 0x7ffffff0u;   // a buffer offset past every range: the DMA writes zeros
+
+template <int RB, int NT, int ACT>
+__global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
+    constexpr int MT = 128 * RB, CB = NT / 32;
+    using Gm = PdGeom<RB>;
+    constexpr int PD_XSLOTS = Gm::XSLOTS, PD_STAGE = Gm::STAGE, PD_XI = Gm::XI, PD_WI = Gm::WI;
+    static_assert(CONV_MAX_TAPS * NT * 4 <= Gm::WSLOTS, "weight stage");
+    extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_taps = p.n_taps, dmin = p.dmin, M = p.M;
+    const size_t ub = blockIdx.z;
+    const int ldy = p.ldy ? p.ldy : p.C_out;
+    const uint16_t *pxh = p.xh + ub * p.xbs * p.C_in;
+    float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
+    const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
+    uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
+    const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
+    if (m0 >= M) return;   // (uniform per workgroup)
+    const int win = MT + p.dmax - dmin;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(pxh), 0,
+                                                                        (int)((size_t)p.T_in * p.C_in * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.taps[0].w), 0,
+                                                                        (int)((size_t)n_taps * p.C_out * p.C_in * 2), 0x00020000);
+    typedef __attribute__((address_space(3))) void lds_t;
+    // this thread's DMA sources of the tile at K chunk 0 (instruction k of wave w fills slots [(4k + w) * 64, +64) of
+    // its region; lane l slot (4k + w) * 64 + l); a chunk adds 2 c0 bytes through the scalar offset, so a DMA costs no
+    // vector instruction.  Out of range (rows outside the window / sequence, taps past n_taps): PD_OOB, the buffer's
+    // range check writes zeros (it holds with the scalar offset added too: PD_OOB + 2 c0 < 2^32)
+    constexpr int ND = PD_XI + PD_WI;
+    unsigned voff[ND];
+#pragma unroll
+    for (int k = 0; k < PD_XI; ++k) {
+        const int P = (4 * k + wave) * 64 + lane, row = P >> 2, q = (P & 3) ^ ((row >> 2) & 3);
+        const int i = m0 + dmin + row;
+        voff[k] = row < win && i >= 0 && i < p.T_in ? (unsigned)(((size_t)i * p.C_in + 8 * q) * 2) : PD_OOB;
+    }
+#pragma unroll
+    for (int k = 0; k < PD_WI; ++k) {
+        const int P = (4 * k + wave) * 64 + lane, j = P / (NT * 4), rem = P - j * (NT * 4), co = rem >> 2;
+        const int q = (rem & 3) ^ ((co >> 2) & 3);
+        voff[PD_XI + k] = j < n_taps ? (unsigned)((((size_t)j * p.C_out + co0 + co) * p.C_in + 8 * q) * 2) : PD_OOB;
+    }
+// (the voffset argument as int: an unsigned one made the host pass drop the kernel stubs without a diagnostic)
+#define PD_DMA(k, st, c0)                                                                                              \
+    do {                                                                                                              \
+        uint8_t *base_ = reinterpret_cast<uint8_t *>(sm) + (st) * PD_STAGE;                                           \
+        if ((k) < PD_XI)                                                                                              \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_t *)(base_ + (4 * (k) + wave) * 1024), 16, (int)voff[k], 2 * (c0), 0, 0); \
+        else                                                                                                          \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_t *)(base_ + PD_XSLOTS * 16 + (4 * ((k) - PD_XI) + wave) * 1024), \
+                                                     16, (int)voff[k], 2 * (c0), 0, 0);                                    \
+    } while (0)
+    const int r = lane & 31, h = lane >> 5;
+    f32x16_t acc[RB][CB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+    int dj[CONV_MAX_TAPS];
+#pragma unroll
+    for (int j = 0; j < CONV_MAX_TAPS; ++j) dj[j] = p.taps[j].dj;   // (compile-time index: scalar kernel-argument loads)
+    const int nch = p.C_in / MT_KC;
+#pragma unroll
+    for (int k = 0; k < ND; ++k) PD_DMA(k, 0, 0);
+    for (int c = 0; c < nch; ++c) {
+        // chunk c's DMAs (issued during chunk c - 1's MFMAs) have landed for every thread; a bare barrier
+        // (__syncthreads' fence adds nothing here)
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        const bool nxt = c + 1 < nch;
+        const uint8_t *xs = reinterpret_cast<const uint8_t *>(sm) + (c & 1) * PD_STAGE;
+        const uint8_t *ws = xs + PD_XSLOTS * 16;
+        // the 7 taps x 2 k-steps as one straight-line sequence, each step's fragments read one step ahead into the
+        // other register set (one wave per SIMD cannot hide an LDS round trip per step otherwise); the MFMA order is
+        // k_conv_mt's (tap, k-step, row tile, channel tile)
+        constexpr int NSTEP = 2 * CONV_MAX_TAPS;
+        half8_t a[2][RB], b[2][CB];
+        auto frag = [&](int st, half8_t (&av)[RB], half8_t (&bv)[CB]) {
+            const int j = st >> 1, q = h + 2 * (st & 1);
+            const int arow = wave * 32 * RB + r + (dj[j] - dmin);
+#pragma unroll
+            for (int i = 0; i < RB; ++i) {
+                const int row = arow + 32 * i;
+                av[i] = *reinterpret_cast<const half8_t *>(xs + row * 64 + ((q ^ ((row >> 2) & 3)) * 16));
+            }
+#pragma unroll
+            for (int cc = 0; cc < CB; ++cc) {
+                const int co = cc * 32 + r;
+                bv[cc] = *reinterpret_cast<const half8_t *>(ws + (j * NT + co) * 64 + ((q ^ ((co >> 2) & 3)) * 16));
+            }
+        };
+        frag(0, a[0], b[0]);
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) {
+            if (st + 1 < NSTEP) frag(st + 1, a[(st + 1) & 1], b[(st + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);   // the reads stay ahead of this step's MFMAs (the scheduler sank them)
+            // chunk c + 1's DMAs into the other stage (read by chunk c - 1, released by its trailing barrier), four
+            // per step among the first steps' MFMAs: their issue hides in the MFMA shadow and they land long before
+            // chunk c ends
+            if (nxt) {
+#pragma unroll
+                for (int k = 4 * st; k < 4 * st + 4; ++k)
+                    if (k < ND) PD_DMA(k, (c + 1) & 1, (c + 1) * MT_KC);
+            }
+#pragma unroll
+            for (int i = 0; i < RB; ++i)
+#pragma unroll
+                for (int cc = 0; cc < CB; ++cc)
+                    acc[i][cc] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[st & 1][i], b[st & 1][cc], acc[i][cc], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage c & 1 is chunk c + 2's DMA target
+    }
+    // ---- epilogue: k_conv_mt's (transposed slices through LDS, 4 channels per lane)
+    constexpr int ELD = NT + 4, Q = NT / 4, EK = 32 * Q / 64;
+    float *es = reinterpret_cast<float *>(sm) + wave * 32 * ELD;
+    float *prm = reinterpret_cast<float *>(sm) + 4 * 32 * ELD;
+    if (tid < NT) {
+        const int co = co0 + tid;
+        prm[tid] = p.bias ? p.bias[co] : 0.0f;
+        prm[NT + tid] = p.scale ? p.scale[co] : 1.0f;
+        prm[2 * NT + tid] = p.y16_a ? p.y16_a[co] : 0.0f;
+        prm[3 * NT + tid] = p.y16_a ? p.y16_ib[co] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+#pragma unroll
+        for (int cc = 0; cc < CB; ++cc)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg)
+                es[((reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)) * ELD + cc * 32 + (lane & 31)] = acc[i][cc][reg];
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+        for (int k = 0; k < EK; ++k) {
+            const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
+            const int m = m0 + wave * 32 * RB + i * 32 + row;
+            if (m >= M) continue;
+            const size_t t = (size_t)m, o = t * ldy + co0 + q4;
+            const size_t o16 = t * p.C_out + co0 + q4;
+            const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
+            float v[4] = {a.x, a.y, a.z, a.w};
+            if (p.bias) {
+                const float4 b = *reinterpret_cast<const float4 *>(prm + q4);
+                v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+            }
+            if (p.scale) {
+                const float4 g = *reinterpret_cast<const float4 *>(prm + NT + q4);
+                v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
+            }
+            if (pres) {
+                const float4 rr = *reinterpret_cast<const float4 *>(pres + o);
+                v[0] = rr.x + v[0]; v[1] = rr.y + v[1]; v[2] = rr.z + v[2]; v[3] = rr.w + v[3];
+            }
+            if constexpr (ACT != 0) {
+                if (p.act) {
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) v[qq] = conv_act(v[qq], p.act);
+                }
+            }
+            if (py) *reinterpret_cast<float4 *>(py + o) = make_float4(v[0], v[1], v[2], v[3]);
+            if (py16) {
+                float z[4] = {v[0], v[1], v[2], v[3]};
+                if (p.y16_a) {
+                    const float4 sa = *reinterpret_cast<const float4 *>(prm + 2 * NT + q4);
+                    const float4 sb = *reinterpret_cast<const float4 *>(prm + 3 * NT + q4);
+                    const float av[4] = {sa.x, sa.y, sa.z, sa.w}, bv[4] = {sb.x, sb.y, sb.z, sb.w};
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) z[qq] = snake_apply(z[qq], av[qq], bv[qq]);
+                }
+                uint2 hv;
+                hv.x = (uint32_t)f2h(z[0]) | ((uint32_t)f2h(z[1]) << 16);
+                hv.y = (uint32_t)f2h(z[2]) | ((uint32_t)f2h(z[3]) << 16);
+                *reinterpret_cast<uint2 *>(py16 + o16) = hv;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Q3T_CONV_PD=0 keeps the multi-tap convs on k_conv_mt (A/B and the bit-exactness test; read at every launch)
+static int conv_pd_mode() {   // 0 off, 1 256-row tiles, 2 512-row tiles
+    const char *e = std::getenv("Q3T_CONV_PD");
+    return e ? std::atoi(e) : 2;
+}
+// k_conv_pd's preconditions: a stride-1 7-tap conv whose taps are consecutive [tap][C_out][C_in] blocks, and 32-bit buffer
+// offsets below the out-of-range marker
+static bool pd_ok(const ConvParams &p) {
+    if (p.so != 1 || p.ob != 0 || p.n_taps != CONV_MAX_TAPS || p.dmax - p.dmin > 64) return false;
+    for (int j = 1; j < p.n_taps; ++j)
+        if (p.taps[j].w != p.taps[0].w + (size_t)j * p.C_out * p.C_in) return false;
+    return (size_t)p.T_in * p.C_in * 2 < PD_OOB && (size_t)p.n_taps * p.C_out * p.C_in * 2 < PD_OOB;
+}
+
+template <int RB, int NT>
+static bool launch_pd(const ConvParams &p, hipStream_t s) {
+    constexpr int lds = 2 * PdGeom<RB>::STAGE;
+    static bool attr = false;
+    if (!attr) {
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, -1>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = true;
+    }
+    const dim3 grid((p.M + 128 * RB - 1) / (128 * RB), p.C_out / NT, p.nb);
+    if (p.act) hipLaunchKernelGGL((k_conv_pd<RB, NT, -1>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((k_conv_pd<RB, NT, 0>), grid, dim3(256), lds, s, p);
+    Q3T_HIP(hipGetLastError());
+    return true;
+}
+
 template <int RB, int NT, int MINB, int TW, int ACT>
 static bool launch_mt2(const ConvParams &p, hipStream_t s) {
     constexpr int MT = 128 * RB;
@@ -479,6 +708,13 @@ bool conv(const ConvParams &pin, hipStream_t s) {
                 case 4: return NT == 96 ? launch_mt1<4, 96, 1, 7>(p, s) : launch_mt1<4, 64, 1, 7>(p, s);
                 default: break;
             }
+        }
+        // the pipelined kernel for the wide blocks' 7-tap convs (512 frames, per launch: C_in 768 191 -> 125 us, 384
+        // 278 -> 207 us, 192 301 -> 256 us with 512-row tiles; 256-row tiles: 135 / 202 us, and no gain at 192)
+        const int pm = conv_pd_mode();
+        if (big && p.n_taps > 3 && p.C_in >= 192 && pd_ok(p)) {
+            if (pm == 1) return NT == 96 ? launch_pd<2, 96>(p, s) : launch_pd<2, 64>(p, s);
+            if (pm == 2) return NT == 96 ? launch_pd<4, 96>(p, s) : launch_pd<4, 64>(p, s);
         }
         if (NT == 96) return big ? launch_mt<2, 96>(p, s) : launch_mt<1, 96>(p, s);
         return big ? launch_mt<2, 64>(p, s) : launch_mt<1, 64>(p, s);

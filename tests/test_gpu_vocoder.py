@@ -133,3 +133,32 @@ def test_fused_residual_unit_bit_exact(F, nutt):
     finally:
         fused.close()
         ref.close()
+
+
+@pytest.mark.parametrize("lens", [(512,), (280, 300, 271)])
+def test_pipelined_conv_bit_exact(lens):
+    """the wide blocks' dilated 7-tap convs on k_conv_pd (LDS-DMA double-buffered K chunks; 256- and 512-row tiles)
+    against k_conv_mt (Q3T_CONV_PD=0, read at every launch): bit-identical PCM.  512 frames put the 768-, 384- and
+    192-channel blocks' convs on the pipelined kernel (the 768-channel block needs >= 512 frames), the 3-utterance
+    batch the 384- and 192-channel blocks with grid z"""
+    import q3t
+    tts, tok = synth_dir("full")
+    eng = q3t.Engine(None, tok, device=0)
+    old = os.environ.get("Q3T_CONV_PD")
+    try:
+        cl = [_codes(F, 300 + F) for F in lens]
+        run = (lambda: [eng.vocoder(cl[0], 0)]) if len(cl) == 1 else (lambda: eng.vocoder_batch(cl, 0))
+        os.environ["Q3T_CONV_PD"] = "0"
+        ref = run()
+        for mode in ("1", "2"):   # 256- and 512-row tiles
+            os.environ["Q3T_CONV_PD"] = mode
+            got = run()
+            for x, y in zip(got, ref):
+                assert x.shape == y.shape
+                assert np.array_equal(x, y), (mode, float(np.abs(x - y).max()))
+    finally:
+        if old is None:
+            os.environ.pop("Q3T_CONV_PD", None)
+        else:
+            os.environ["Q3T_CONV_PD"] = old
+        eng.close()
