@@ -400,35 +400,60 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
 //   q ^ ((r >> 2) & 3) (conflict-free ds_read_b128 fragment reads without row padding: a DMA fills 1 KB contiguously)
 // Every thread issues exactly 16 DMA instructions per stage (5 window, 11 weight; placeholders out of range), so the
 // wait for the previous stage is vmcnt(16).
-template <int RB> struct PdGeom {   // stage geometry of k_conv_pd<RB>: window rows 128 RB + 64, weights 44 KB
-    static constexpr int XROWS = 128 * RB + 64, XSLOTS = XROWS * 4, WSLOTS = 44 * 64, STAGE = (XSLOTS + WSLOTS) * 16;
+// stage geometry of k_conv_pd<RB, NT, TAPS>: window rows 128 RB + 64, weights TAPS x NT rows, both in 1 KB DMA pieces
+// spread over the 4 waves (7 taps x 96 channels: 44 KB)
+template <int RB, int NT, int TAPS> struct PdGeom {
+    static constexpr int XROWS = 128 * RB + 64, XSLOTS = XROWS * 4, WSLOTS = (TAPS * NT * 4 + 255) / 256 * 256;
+    static constexpr int STAGE = (XSLOTS + WSLOTS) * 16;
     static constexpr int XI = XSLOTS / 256, WI = WSLOTS / 256;   // DMA instructions per thread and stage
     static_assert(XSLOTS % 256 == 0 && 2 * STAGE <= 160 * 1024, "stages");
 };
 constexpr unsigned PD_OOB = 0x7ffffff0u;   // a buffer offset past every range: the DMA writes zeros
 
-template <int RB, int NT, int ACT>
+// TAPS = 7: a stride-1 conv (taps [tap][C_out][C_in] consecutive); TAPS = 2: one launch over every output phase of a
+// transposed conv (grid z = utterance x phase, k_conv_mt's ct_* geometry: phase phi's taps k = k0 + j st, input rows
+// m + (phi + trim - k) / st, output rows st m + phi)
+template <int RB, int NT, int TAPS, int ACT>
 __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     constexpr int MT = 128 * RB, CB = NT / 32;
-    using Gm = PdGeom<RB>;
+    using Gm = PdGeom<RB, NT, TAPS>;
     constexpr int PD_XSLOTS = Gm::XSLOTS, PD_STAGE = Gm::STAGE, PD_XI = Gm::XI, PD_WI = Gm::WI;
-    static_assert(CONV_MAX_TAPS * NT * 4 <= Gm::WSLOTS, "weight stage");
     extern __shared__ __attribute__((aligned(16))) uint16_t sm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n_taps = p.n_taps, dmin = p.dmin, M = p.M;
-    const size_t ub = blockIdx.z;
+    int n_taps = p.n_taps, dmin = p.dmin, dmax = p.dmax, M = p.M, so = 1, ob = 0;
+    int dj[TAPS];
+    size_t wofs[TAPS];   // tap j's weight block, elements past the buffer base
+    const uint16_t *wbase = p.taps[0].w;
+    size_t wbytes = (size_t)n_taps * p.C_out * p.C_in * 2;
+    const int nz = TAPS == 2 ? p.ct_st : 1;
+    const size_t ub = blockIdx.z / nz;
+    if constexpr (TAPS == 2) {
+        const int phi = blockIdx.z - (int)ub * nz, st = p.ct_st, k0 = (phi + p.ct_trim) % st, d0 = (phi + p.ct_trim - k0) / st;
+        n_taps = min(TAPS, (p.ct_k - k0 + st - 1) / st);
+#pragma unroll
+        for (int j = 0; j < TAPS; ++j) { dj[j] = d0 - j; wofs[j] = (size_t)(k0 + j * st) * p.C_out * p.C_in; }
+        dmin = d0 - (n_taps - 1);
+        dmax = d0;
+        M = (p.T_out - phi + st - 1) / st;
+        so = st;
+        ob = phi;
+        wbase = p.ct_w;
+        wbytes = (size_t)p.ct_k * p.C_out * p.C_in * 2;
+    } else {
+#pragma unroll
+        for (int j = 0; j < TAPS; ++j) { dj[j] = p.taps[j].dj; wofs[j] = (size_t)j * p.C_out * p.C_in; }
+    }
     const int ldy = p.ldy ? p.ldy : p.C_out;
     const uint16_t *pxh = p.xh + ub * p.xbs * p.C_in;
     float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
     const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
     uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
     const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
-    if (m0 >= M) return;   // (uniform per workgroup)
-    const int win = MT + p.dmax - dmin;
+    if (m0 >= M || n_taps <= 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
+    const int win = MT + dmax - dmin;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(pxh), 0,
                                                                         (int)((size_t)p.T_in * p.C_in * 2), 0x00020000);
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(p.taps[0].w), 0,
-                                                                        (int)((size_t)n_taps * p.C_out * p.C_in * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(wbase), 0, (int)wbytes, 0x00020000);
     typedef __attribute__((address_space(3))) void lds_t;
     // this thread's DMA sources of the tile at K chunk 0 (instruction k of wave w fills slots [(4k + w) * 64, +64) of
     // its region; lane l slot (4k + w) * 64 + l); a chunk adds 2 c0 bytes through the scalar offset, so a DMA costs no
@@ -446,7 +471,10 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     for (int k = 0; k < PD_WI; ++k) {
         const int P = (4 * k + wave) * 64 + lane, j = P / (NT * 4), rem = P - j * (NT * 4), co = rem >> 2;
         const int q = (rem & 3) ^ ((co >> 2) & 3);
-        voff[PD_XI + k] = j < n_taps ? (unsigned)((((size_t)j * p.C_out + co0 + co) * p.C_in + 8 * q) * 2) : PD_OOB;
+        size_t wj = 0;
+#pragma unroll
+        for (int jj = 0; jj < TAPS; ++jj) wj = jj == j ? wofs[jj] : wj;
+        voff[PD_XI + k] = j < n_taps ? (unsigned)((wj + (size_t)(co0 + co) * p.C_in + 8 * q) * 2) : PD_OOB;
     }
 // (the voffset argument as int: an unsigned one made the host pass drop the kernel stubs without a diagnostic)
 #define PD_DMA(k, st, c0)                                                                                              \
@@ -466,9 +494,6 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
         for (int j = 0; j < CB; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-    int dj[CONV_MAX_TAPS];
-#pragma unroll
-    for (int j = 0; j < CONV_MAX_TAPS; ++j) dj[j] = p.taps[j].dj;   // (compile-time index: scalar kernel-argument loads)
     const int nch = p.C_in / MT_KC;
 #pragma unroll
     for (int k = 0; k < ND; ++k) PD_DMA(k, 0, 0);
@@ -482,7 +507,7 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
         // the 7 taps x 2 k-steps as one straight-line sequence, each step's fragments read one step ahead into the
         // other register set (one wave per SIMD cannot hide an LDS round trip per step otherwise); the MFMA order is
         // k_conv_mt's (tap, k-step, row tile, channel tile)
-        constexpr int NSTEP = 2 * CONV_MAX_TAPS;
+        constexpr int NSTEP = 2 * TAPS;   // (every phase has TAPS taps: pd_ok)
         half8_t a[2][RB], b[2][CB];
         auto frag = [&](int st, half8_t (&av)[RB], half8_t (&bv)[CB]) {
             const int j = st >> 1, q = h + 2 * (st & 1);
@@ -545,7 +570,7 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
             const int e = lane + 64 * k, row = e / Q, q4 = (e % Q) * 4;
             const int m = m0 + wave * 32 * RB + i * 32 + row;
             if (m >= M) continue;
-            const size_t t = (size_t)m, o = t * ldy + co0 + q4;
+            const size_t t = (size_t)m * so + ob, o = t * ldy + co0 + q4;
             const size_t o16 = t * p.C_out + co0 + q4;
             const float4 a = *reinterpret_cast<const float4 *>(es + row * ELD + q4);
             float v[4] = {a.x, a.y, a.z, a.w};
@@ -588,6 +613,10 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
 }
 
 // Q3T_CONV_PD=0 keeps the multi-tap convs on k_conv_mt (A/B and the bit-exactness test; read at every launch)
+static bool conv_pd_ct() {   // Q3T_CONV_PD_CT=0 keeps the transposed convs on k_conv_mt (A/B)
+    const char *e = std::getenv("Q3T_CONV_PD_CT");
+    return !e || std::atoi(e) != 0;
+}
 static int conv_pd_mode() {   // 0 off, 1 256-row tiles, 2 512-row tiles
     const char *e = std::getenv("Q3T_CONV_PD");
     return e ? std::atoi(e) : 2;
@@ -595,24 +624,27 @@ static int conv_pd_mode() {   // 0 off, 1 256-row tiles, 2 512-row tiles
 // k_conv_pd's preconditions: a stride-1 7-tap conv whose taps are consecutive [tap][C_out][C_in] blocks, and 32-bit buffer
 // offsets below the out-of-range marker
 static bool pd_ok(const ConvParams &p) {
+    if (p.ct_st)   // transposed: kernel 2 st, so every output phase has exactly 2 taps
+        return p.ct_k == 2 * p.ct_st && p.C_in % MT_KC == 0 && (size_t)p.T_in * p.C_in * 2 < PD_OOB &&
+               (size_t)p.ct_k * p.C_out * p.C_in * 2 < PD_OOB;
     if (p.so != 1 || p.ob != 0 || p.n_taps != CONV_MAX_TAPS || p.dmax - p.dmin > 64) return false;
     for (int j = 1; j < p.n_taps; ++j)
         if (p.taps[j].w != p.taps[0].w + (size_t)j * p.C_out * p.C_in) return false;
     return (size_t)p.T_in * p.C_in * 2 < PD_OOB && (size_t)p.n_taps * p.C_out * p.C_in * 2 < PD_OOB;
 }
 
-template <int RB, int NT>
+template <int RB, int NT, int TAPS = CONV_MAX_TAPS>
 static bool launch_pd(const ConvParams &p, hipStream_t s) {
-    constexpr int lds = 2 * PdGeom<RB>::STAGE;
+    constexpr int lds = 2 * PdGeom<RB, NT, TAPS>::STAGE;
     static bool attr = false;
     if (!attr) {
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, -1>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, TAPS, 0>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        Q3T_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conv_pd<RB, NT, TAPS, -1>), hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         attr = true;
     }
-    const dim3 grid((p.M + 128 * RB - 1) / (128 * RB), p.C_out / NT, p.nb);
-    if (p.act) hipLaunchKernelGGL((k_conv_pd<RB, NT, -1>), grid, dim3(256), lds, s, p);
-    else hipLaunchKernelGGL((k_conv_pd<RB, NT, 0>), grid, dim3(256), lds, s, p);
+    const dim3 grid((p.M + 128 * RB - 1) / (128 * RB), p.C_out / NT, (p.ct_st ? p.ct_st : 1) * p.nb);
+    if (p.act) hipLaunchKernelGGL((k_conv_pd<RB, NT, TAPS, -1>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((k_conv_pd<RB, NT, TAPS, 0>), grid, dim3(256), lds, s, p);
     Q3T_HIP(hipGetLastError());
     return true;
 }
@@ -683,6 +715,10 @@ bool conv(const ConvParams &pin, hipStream_t s) {
         q.dmax = q.n_taps - 1;                      // taps of one phase are consecutive input rows
         if (q.M <= 0) return true;
         const long tiles256 = (long)((q.M + 255) / 256) * (p.C_out / NT) * p.ct_st * p.nb;
+        // the pipelined kernel (512-row tiles, both taps of a phase per K chunk) where a tile has 24+ K chunks (per launch
+        // at 512 frames: C_in 1536 116 -> 94 us, 768 162 -> 157; 384 209 -> 201; 192 275 -> 288 us)
+        if (tiles256 >= 512 && p.C_in >= 768 && conv_pd_mode() == 2 && pd_ok(q) && conv_pd_ct())
+            return NT == 96 ? launch_pd<4, 96, 2>(q, s) : launch_pd<4, 64, 2>(q, s);
         if (NT == 96) return tiles256 >= 512 ? launch_mt<2, 96>(q, s) : launch_mt<1, 96>(q, s);
         return tiles256 >= 512 ? launch_mt<2, 64>(q, s) : launch_mt<1, 64>(q, s);
     }
