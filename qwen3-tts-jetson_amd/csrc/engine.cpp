@@ -22,44 +22,6 @@ namespace q3t {
 Engine::Engine() = default;
 
 namespace {
-// writer-preferring reader/writer lock: once an exclusive holder waits, no new shared hold is granted for up to
-// kReaderYield, so a single-slot generate is not starved by overlapping shared holds (vocoder + batched contexts in a
-// serving loop; glibc's std::shared_mutex prefers readers).  The preference is bounded: a frame callback runs under
-// its generate's shared hold and may wait for another thread that needs a shared hold on the same device (a vocoder
-// worker behind a bounded queue); with an unbounded preference a single-slot generate queued meanwhile would leave
-// that worker, and the callback, waiting forever.  After kReaderYield the reader is admitted beside the waiting writer.
-class WPLock {
-public:
-    void lock() {
-        std::unique_lock<std::mutex> g(m_);
-        ++waiting_w_;
-        cv_.wait(g, [&] { return !writer_ && readers_ == 0; });
-        --waiting_w_;
-        writer_ = true;
-    }
-    void unlock() {
-        { std::lock_guard<std::mutex> g(m_); writer_ = false; }
-        cv_.notify_all();
-    }
-    void lock_shared() {
-        std::unique_lock<std::mutex> g(m_);
-        if (!cv_.wait_for(g, kReaderYield, [&] { return !writer_ && waiting_w_ == 0; }))
-            cv_.wait(g, [&] { return !writer_; });
-        ++readers_;
-    }
-    void unlock_shared() {
-        bool wake;
-        { std::lock_guard<std::mutex> g(m_); wake = --readers_ == 0; }
-        if (wake) cv_.notify_all();
-    }
-
-private:
-    static constexpr std::chrono::milliseconds kReaderYield{20};
-    std::mutex m_;
-    std::condition_variable cv_;
-    int readers_ = 0, waiting_w_ = 0;
-    bool writer_ = false;
-};
 WPLock g_device_rw[64];
 thread_local int t_device_depth[64];
 }  // namespace
