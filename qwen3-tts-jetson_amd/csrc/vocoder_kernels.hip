@@ -948,22 +948,32 @@ __global__ void __launch_bounds__(512) k_attn_prefill(const float *qkv, uint16_t
     float m = -INFINITY, l = 0.0f, acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const float scale = 0.125f;   // 1 / sqrt(64)
     const int kend = min(F, q0 + QT);
-    for (int k0 = 0; k0 < kend; k0 += KT) {
-        __syncthreads();
-        // chunk: 64 keys x 64 dims of K and V, 2 float4 per thread per tensor
+    // chunk: 64 keys x 64 dims of K and V, 2 float4 per thread per tensor, loaded into registers one chunk ahead (the
+    // chunk loop is serial per workgroup and the longest query block runs 8 chunks: the load latency was exposed once
+    // per chunk).  Unconditional loads (rows clamped, zeroed past F at the LDS store) keep one chunk in flight at the
+    // compiler's waits.
+    float4 kr4[2], vr4[2];
+    auto kv_load = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int e = (u * 512 + tid) * 4, kk = e / D, d = e % D, pos = k0 + kk;
-            float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-            if (pos < F) {
-                const float *row = qkv + (size_t)pos * LD;
-                kv = *reinterpret_cast<const float4 *>(row + nH * D + h * D + d);
-                vv = *reinterpret_cast<const float4 *>(row + 2 * nH * D + h * D + d);
-            }
-            *reinterpret_cast<float4 *>(ks + kk * KP + d) = kv;
-            *reinterpret_cast<float4 *>(vs + kk * KP + d) = vv;
+            const int e = (u * 512 + tid) * 4, kk = e / D, d = e % D, pos = min(k0 + kk, F - 1);
+            const float *row = qkv + (size_t)pos * LD;
+            kr4[u] = *reinterpret_cast<const float4 *>(row + nH * D + h * D + d);
+            vr4[u] = *reinterpret_cast<const float4 *>(row + 2 * nH * D + h * D + d);
+        }
+    };
+    kv_load(0);
+    for (int k0 = 0; k0 < kend; k0 += KT) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = (u * 512 + tid) * 4, kk = e / D, d = e % D;
+            const bool in = k0 + kk < F;
+            *reinterpret_cast<float4 *>(ks + kk * KP + d) = in ? kr4[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4 *>(vs + kk * KP + d) = in ? vr4[u] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
+        kv_load(min(k0 + KT, kend - 1));   // the next chunk (past the last: the last rows again, never stored)
         float sc[4], mt = -INFINITY;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

@@ -11,5 +11,5 @@ for V in head new; do
   if [ $V = head ]; then export Q3T_DEV_LIB=head; else unset Q3T_DEV_LIB; fi
   timeout -k 10 120 python3 tools/dev/voc_only.py 512 0 16 | tail -4 || exit 1
   bash tools/dev/gpu.sh trace voc_$V "python3 $R/tools/dev/voc_only.py 512" --by-grid > /dev/null || exit 1
-  grep -E "conv_pd|conv_mt<2, 96, 2, 3|conv_mt<2, 64, 2, 3|total" gpurun_out/prof_voc_${V}_summary.txt
+  grep -E "attn_prefill|total" gpurun_out/prof_voc_${V}_summary.txt
 done
