@@ -50,6 +50,7 @@ struct ConvParams {
     int nb = 1;
     int64_t xbs = 0, ybs = 0;
     int dev_skip = 0;   // development builds only (timing experiments): 1 weight loads, 2 window loads, 4 epilogue
+    int xcd_tiles = 0;  // k_conv_mt 1-tap narrow variant: channel tiles of a row tile on one XCD (set by conv())
 };
 bool conv(const ConvParams &p, hipStream_t s);
 // one 96-channel decoder residual unit as one launch (vocoder_resunit.hip), bit-identical to its two conv launches:

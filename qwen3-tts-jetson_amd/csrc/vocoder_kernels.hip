@@ -156,6 +156,19 @@ constexpr int MT_KC = 32, MT_LDK = MT_KC + 8;   // LDS row: 32 f16 + 16 B pad (c
 // thread, loaded one chunk ahead like the input window.  1-tap variants (RB 1) also load their residual rows before
 // the main loop, so the epilogue's f32 reads are in flight while the GEMM runs (these convs are bound by that traffic).
 // ACT: 0 = no activation code in the epilogue (the decoder's convs), -1 = p.act at run time
+// Tile order of a conv with n > 1 channel tiles (grid y): the channel tiles of one row tile run on one XCD and are
+// dispatched together -- workgroup L (x fastest) runs on XCD L % 8; it takes row tile 8 (L / (8 n)) + L % 8 and channel
+// tile (L / 8) % n -- so the row tile's input rows are fetched once into that XCD's L2 and hit there for the other
+// channel tiles (in grid order every channel tile of a row tile ran on another XCD, at another time).  A bijection
+// on the grid (the last group of < 8 row tiles likewise); the arithmetic of a tile does not depend on it.
+__device__ __forceinline__ void xcd_tile(int &mt, int &ct) {
+    const int gx = gridDim.x, n = gridDim.y;
+    if (n <= 1) return;
+    const int L = blockIdx.y * gx + blockIdx.x, grp = L / (8 * n), rem = min(8, gx - 8 * grp), r = L - grp * 8 * n;
+    mt = 8 * grp + r % rem;
+    ct = r / rem;
+}
+
 template <int RB, int NT, int MINB, int TW, int ACT>
 __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     constexpr int MT = 128 * RB, CB = NT / 32;
@@ -193,7 +206,10 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
         for (int j = 0; j < CONV_MAX_TAPS; ++j)
             if (tid == j) { tapw[j] = p.taps[j].w; tapdj[j] = p.taps[j].dj; }
     }
-    const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
+    // tile of this workgroup (xcd_tile: the channel tiles of a row tile on one XCD)
+    int mt = blockIdx.x, ct = blockIdx.y;
+    if (p.xcd_tiles && !p.ct_st) xcd_tile(mt, ct);
+    const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps == 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     __syncthreads();
     const int win = MT + dmax - dmin;
@@ -448,7 +464,9 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
     const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
     uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
-    const int m0 = blockIdx.x * MT, co0 = blockIdx.y * NT;
+    int mt = blockIdx.x, ct = blockIdx.y;
+    if (p.xcd_tiles && TAPS != 2) xcd_tile(mt, ct);
+    const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps <= 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     const int win = MT + dmax - dmin;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(pxh), 0,
@@ -613,6 +631,10 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
 }
 
 // Q3T_CONV_PD=0 keeps the multi-tap convs on k_conv_mt (A/B and the bit-exactness test; read at every launch)
+static bool conv_xcd_tiles() {   // Q3T_CONV_XCD=0: the 1-tap narrow convs' tiles in plain grid order (A/B)
+    const char *e = std::getenv("Q3T_CONV_XCD");
+    return !e || std::atoi(e) != 0;
+}
 static bool conv_pd_ct() {   // Q3T_CONV_PD_CT=0 keeps the transposed convs on k_conv_mt (A/B)
     const char *e = std::getenv("Q3T_CONV_PD_CT");
     return !e || std::atoi(e) != 0;
@@ -735,7 +757,9 @@ bool conv(const ConvParams &pin, hipStream_t s) {
         // at three workgroups per CU keep more of it in flight
         const long tiles256 = (long)((p.M + 255) / 256) * (p.C_out / NT) * p.nb;
         const bool big = tiles256 >= 512;
-        if (big && p.n_taps == 1 && p.C_in <= 192) return NT == 96 ? launch_mt<1, 96, 3>(p, s) : launch_mt<1, 64, 3>(p, s);
+        ConvParams q = p;
+        q.xcd_tiles = conv_xcd_tiles();
+        if (big && p.n_taps == 1 && p.C_in <= 192) return NT == 96 ? launch_mt<1, 96, 3>(q, s) : launch_mt<1, 64, 3>(q, s);
         if (g_conv_variant && big && p.n_taps > 1) {
             switch (g_conv_variant) {
                 case 1: return NT == 96 ? launch_mt1<1, 96, 2, 7>(p, s) : launch_mt1<1, 64, 2, 7>(p, s);
@@ -749,11 +773,11 @@ bool conv(const ConvParams &pin, hipStream_t s) {
         // 278 -> 207 us, 192 301 -> 256 us with 512-row tiles; 256-row tiles: 135 / 202 us, and no gain at 192)
         const int pm = conv_pd_mode();
         if (big && p.n_taps > 3 && p.C_in >= 192 && pd_ok(p)) {
-            if (pm == 1) return NT == 96 ? launch_pd<2, 96>(p, s) : launch_pd<2, 64>(p, s);
-            if (pm == 2) return NT == 96 ? launch_pd<4, 96>(p, s) : launch_pd<4, 64>(p, s);
+            if (pm == 1) return NT == 96 ? launch_pd<2, 96>(q, s) : launch_pd<2, 64>(q, s);
+            if (pm == 2) return NT == 96 ? launch_pd<4, 96>(q, s) : launch_pd<4, 64>(q, s);
         }
-        if (NT == 96) return big ? launch_mt<2, 96>(p, s) : launch_mt<1, 96>(p, s);
-        return big ? launch_mt<2, 64>(p, s) : launch_mt<1, 64>(p, s);
+        if (NT == 96) return big ? launch_mt<2, 96>(q, s) : launch_mt<1, 96>(q, s);
+        return big ? launch_mt<2, 64>(q, s) : launch_mt<1, 64>(q, s);
     }
     if (!p.y && !p.y16) { set_error("conv: no output"); return false; }
     const dim3 grid((p.M + CT_M - 1) / CT_M, (p.C_out + CT_N - 1) / CT_N, p.nb);
