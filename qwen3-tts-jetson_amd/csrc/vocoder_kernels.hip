@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     }
     // tile of this workgroup (xcd_tile: the channel tiles of a row tile on one XCD)
     int mt = blockIdx.x, ct = blockIdx.y;
-    if (p.xcd_tiles && !p.ct_st) xcd_tile(mt, ct);
+    if (p.xcd_tiles) xcd_tile(mt, ct);
     const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps == 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     __syncthreads();
@@ -465,7 +465,7 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
     uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
     int mt = blockIdx.x, ct = blockIdx.y;
-    if (p.xcd_tiles && TAPS != 2) xcd_tile(mt, ct);
+    if (p.xcd_tiles) xcd_tile(mt, ct);
     const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps <= 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     const int win = MT + dmax - dmin;
@@ -631,7 +631,7 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
 }
 
 // Q3T_CONV_PD=0 keeps the multi-tap convs on k_conv_mt (A/B and the bit-exactness test; read at every launch)
-static bool conv_xcd_tiles() {   // Q3T_CONV_XCD=0: the 1-tap narrow convs' tiles in plain grid order (A/B)
+static bool conv_xcd_tiles() {   // Q3T_CONV_XCD=0: the conv tiles in plain grid order (A/B)
     const char *e = std::getenv("Q3T_CONV_XCD");
     return !e || std::atoi(e) != 0;
 }
@@ -731,6 +731,7 @@ bool conv(const ConvParams &pin, hipStream_t s) {
         if (p.nb <= 0) return true;
         if (p.nb > 1 && (p.xbs < p.T_in || p.ybs < p.T_out)) { set_error("conv: bad utterance strides"); return false; }
         ConvParams q = p;
+        q.xcd_tiles = conv_xcd_tiles();
         q.M = (p.T_out + p.ct_st - 1) / p.ct_st;   // phase 0 has the most rows
         q.n_taps = (p.ct_k + p.ct_st - 1) / p.ct_st;
         q.dmin = 0;
