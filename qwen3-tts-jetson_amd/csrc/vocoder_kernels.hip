@@ -156,17 +156,23 @@ constexpr int MT_KC = 32, MT_LDK = MT_KC + 8;   // LDS row: 32 f16 + 16 B pad (c
 // thread, loaded one chunk ahead like the input window.  1-tap variants (RB 1) also load their residual rows before
 // the main loop, so the epilogue's f32 reads are in flight while the GEMM runs (these convs are bound by that traffic).
 // ACT: 0 = no activation code in the epilogue (the decoder's convs), -1 = p.act at run time
-// Tile order of a conv with n > 1 channel tiles (grid y): the channel tiles of one row tile run on one XCD and are
-// dispatched together -- workgroup L (x fastest) runs on XCD L % 8; it takes row tile 8 (L / (8 n)) + L % 8 and channel
-// tile (L / 8) % n -- so the row tile's input rows are fetched once into that XCD's L2 and hit there for the other
-// channel tiles (in grid order every channel tile of a row tile ran on another XCD, at another time).  A bijection
-// on the grid (the last group of < 8 row tiles likewise); the arithmetic of a tile does not depend on it.
-__device__ __forceinline__ void xcd_tile(int &mt, int &ct) {
-    const int gx = gridDim.x, n = gridDim.y;
-    if (n <= 1) return;
-    const int L = blockIdx.y * gx + blockIdx.x, grp = L / (8 * n), rem = min(8, gx - 8 * grp), r = L - grp * 8 * n;
+// Tile of a workgroup: (row tile, channel tile, output phase of a transposed conv).  With xcd (ConvParams::xcd_tiles)
+// the n = channel tiles x phases that read one row tile's input rows run on one XCD and are dispatched together --
+// workgroup L (x fastest, then y, then z) runs on XCD L % 8; it takes row tile 8 (L / (8 n)) + L % 8 and
+// (channel tile, phase) number (L / 8) % n -- so those rows are fetched once into that XCD's L2 and hit there for the
+// others (in grid order they ran on other XCDs, at other times).  A bijection on each utterance's tiles (the last
+// group of < 8 row tiles likewise); the arithmetic of a tile does not depend on it.
+__device__ __forceinline__ void conv_tile(bool xcd, int nz, int &mt, int &ct, int &phi) {
+    mt = blockIdx.x;
+    ct = blockIdx.y;
+    phi = blockIdx.z % nz;
+    const int gx = gridDim.x, gy = gridDim.y, n = gy * nz;
+    if (!xcd || n <= 1) return;
+    const int L = (phi * gy + ct) * gx + mt, grp = L / (8 * n), rem = min(8, gx - 8 * grp), r = L - grp * 8 * n;
     mt = 8 * grp + r % rem;
-    ct = r / rem;
+    const int cz = r / rem;
+    ct = cz % gy;
+    phi = cz / gy;
 }
 
 template <int RB, int NT, int MINB, int TW, int ACT>
@@ -188,8 +194,10 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
     float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
     const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
     uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
+    int mt, ct, phi;
+    conv_tile(p.xcd_tiles != 0, nz, mt, ct, phi);
     if (p.ct_st) {
-        const int phi = blockIdx.z - ubi * nz, st = p.ct_st, k0 = (phi + p.ct_trim) % st;
+        const int st = p.ct_st, k0 = (phi + p.ct_trim) % st;
         n_taps = 0;
         for (int k = k0; k < p.ct_k && n_taps < CONV_MAX_TAPS; k += st) {
             const int dj = (phi + p.ct_trim - k) / st;
@@ -206,9 +214,6 @@ __global__ void __launch_bounds__(256, MINB) k_conv_mt(const ConvParams p) {
         for (int j = 0; j < CONV_MAX_TAPS; ++j)
             if (tid == j) { tapw[j] = p.taps[j].w; tapdj[j] = p.taps[j].dj; }
     }
-    // tile of this workgroup (xcd_tile: the channel tiles of a row tile on one XCD)
-    int mt = blockIdx.x, ct = blockIdx.y;
-    if (p.xcd_tiles) xcd_tile(mt, ct);
     const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps == 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     __syncthreads();
@@ -443,8 +448,10 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     size_t wbytes = (size_t)n_taps * p.C_out * p.C_in * 2;
     const int nz = TAPS == 2 ? p.ct_st : 1;
     const size_t ub = blockIdx.z / nz;
+    int mt, ct, phi;
+    conv_tile(p.xcd_tiles != 0, nz, mt, ct, phi);
     if constexpr (TAPS == 2) {
-        const int phi = blockIdx.z - (int)ub * nz, st = p.ct_st, k0 = (phi + p.ct_trim) % st, d0 = (phi + p.ct_trim - k0) / st;
+        const int st = p.ct_st, k0 = (phi + p.ct_trim) % st, d0 = (phi + p.ct_trim - k0) / st;
         n_taps = min(TAPS, (p.ct_k - k0 + st - 1) / st);
 #pragma unroll
         for (int j = 0; j < TAPS; ++j) { dj[j] = d0 - j; wofs[j] = (size_t)(k0 + j * st) * p.C_out * p.C_in; }
@@ -464,8 +471,6 @@ __global__ void __launch_bounds__(256, 1) k_conv_pd(const ConvParams p) {
     float *py = p.y ? p.y + ub * p.ybs * ldy : nullptr;
     const float *pres = p.resid ? p.resid + ub * p.ybs * ldy : nullptr;
     uint16_t *py16 = p.y16 ? p.y16 + ub * p.ybs * p.C_out : nullptr;
-    int mt = blockIdx.x, ct = blockIdx.y;
-    if (p.xcd_tiles) xcd_tile(mt, ct);
     const int m0 = mt * MT, co0 = ct * NT;
     if (m0 >= M || n_taps <= 0) return;   // (uniform per workgroup: shorter phases of a transposed conv)
     const int win = MT + dmax - dmin;
