@@ -591,7 +591,7 @@ bool Vocoder::decode_rows(const int32_t *codes_dev, int F, float *pcm_dev, int64
         }
     }
     // 7) SnakeBeta -> conv k7 (pad 6) -> tanh   (:775-790): ha holds f16(snake(dec5)) of the stream
-    if (dec6_.oc == 1 && dec6_.ic % 8 == 0 && dec6_.ic <= 112 && dec6_.k <= 8) {
+    if (dec6_.oc == 1 && dec6_.ic % 8 == 0 && dec6_.ic <= 104 && dec6_.k <= 8) {
         if (!conv_out1(ha, dec6_.w, dec6_.b, pcm_dev, (int)T, dec6_.ic, dec6_.k, s, nb_)) return false;
         *n_out = T;
         return true;

@@ -866,22 +866,24 @@ bool norm_f16(const float *x, const float *w, const float *b, float eps, int mod
 
 // ======================================================================================= single-channel output conv
 // one workgroup per 256 outputs: the input rows [t0 - (K-1), t0 + 256) staged once in LDS, one output per thread
-constexpr int CO1_T = 256, CO1_MAXC = 112, CO1_MAXK = 8;
+constexpr int CO1_T = 256, CO1_MAXC = 104, CO1_MAXK = 8;
 __global__ void __launch_bounds__(256) k_conv_out1(const uint16_t *xh, const uint16_t *w, const float *bias, float *y,
                                                    int T, int C, int K) {
     // f16 x f16 products (exact in f32) as v_dot2_f32_f16 pairs into four independent f32 accumulators: the
     // single-accumulator f32 chain (h2f per element, 1,344 dependent FMAs per sample) ran at 1.3 TB/s
     typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-    __shared__ __attribute__((aligned(16))) uint16_t xs[(CO1_T + CO1_MAXK) * CO1_MAXC];
+    // input rows at a stride of C + 8 halves: lane l reads row l + j, so at a stride of C = 96 halves (192 B) 16 lanes'
+    // 16-byte reads fell on 4 bank groups (4-way conflicts); C + 8 (208 B) puts them on 16 distinct ones
+    __shared__ __attribute__((aligned(16))) uint16_t xs[(CO1_T + CO1_MAXK) * (CO1_MAXC + 8)];
     __shared__ __attribute__((aligned(16))) uint16_t ws[CO1_MAXK * CO1_MAXC];
     const int t0 = blockIdx.x * CO1_T, tid = threadIdx.x;
     xh += (size_t)blockIdx.y * T * C;   // utterance
     y += (size_t)blockIdx.y * T;
-    const int rows = CO1_T + K - 1, c8n = C / 8;
+    const int rows = CO1_T + K - 1, c8n = C / 8, XLD = C + 8;
     for (int e = tid; e < rows * c8n; e += 256) {
         const int r = e / c8n, c8 = (e % c8n) * 8, i = t0 - (K - 1) + r;
         const uint4 u = (i >= 0 && i < T) ? ldg16(xh + (size_t)i * C + c8) : make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4 *>(xs + r * C + c8) = u;
+        *reinterpret_cast<uint4 *>(xs + r * XLD + c8) = u;
     }
     for (int e = tid; e < K * C; e += 256) ws[e] = w[e];
     __syncthreads();
@@ -889,7 +891,7 @@ __global__ void __launch_bounds__(256) k_conv_out1(const uint16_t *xh, const uin
     if (t >= T) return;
     float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int j = 0; j < K; ++j) {
-        const uint16_t *xr = xs + (tid + j) * C;
+        const uint16_t *xr = xs + (tid + j) * XLD;
         const uint16_t *wr = ws + j * C;
         for (int c = 0; c < C; c += 8) {
             const uint4 u = *reinterpret_cast<const uint4 *>(xr + c);
