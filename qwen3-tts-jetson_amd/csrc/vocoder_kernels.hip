@@ -644,6 +644,10 @@ static bool conv_pd_ct() {   // Q3T_CONV_PD_CT=0 keeps the transposed convs on k
     const char *e = std::getenv("Q3T_CONV_PD_CT");
     return !e || std::atoi(e) != 0;
 }
+static int conv_pd_minc() {   // Q3T_CONV_PD_MINC: smallest C_in of a 7-tap conv on k_conv_pd (A/B; default 192)
+    const char *e = std::getenv("Q3T_CONV_PD_MINC");
+    return e ? std::atoi(e) : 192;
+}
 static int conv_pd_mode() {   // 0 off, 1 256-row tiles, 2 512-row tiles
     const char *e = std::getenv("Q3T_CONV_PD");
     return e ? std::atoi(e) : 2;
@@ -778,7 +782,7 @@ bool conv(const ConvParams &pin, hipStream_t s) {
         // the pipelined kernel for the wide blocks' 7-tap convs (512 frames, per launch: C_in 768 191 -> 125 us, 384
         // 278 -> 207 us, 192 301 -> 256 us with 512-row tiles; 256-row tiles: 135 / 202 us, and no gain at 192)
         const int pm = conv_pd_mode();
-        if (big && p.n_taps > 3 && p.C_in >= 192 && pd_ok(p)) {
+        if (big && p.n_taps > 3 && p.C_in >= conv_pd_minc() && pd_ok(p)) {
             if (pm == 1) return NT == 96 ? launch_pd<2, 96>(q, s) : launch_pd<2, 64>(q, s);
             if (pm == 2) return NT == 96 ? launch_pd<4, 96>(q, s) : launch_pd<4, 64>(q, s);
         }
