@@ -9,5 +9,5 @@ python3 tools/dev/voc_dump.py --cmp gpurun_out/voc_head.npz gpurun_out/voc_new.n
 for V in head new; do
   if [ $V = head ]; then export Q3T_DEV_LIB=head; else unset Q3T_DEV_LIB; fi
   bash tools/dev/gpu.sh trace voc_$V "python3 $R/tools/dev/voc_only.py 512" --by-grid > /dev/null || exit 1
-  grep -E "conv_out1|total" gpurun_out/prof_voc_${V}_summary.txt
+  grep -E "attn_prefill|total" gpurun_out/prof_voc_${V}_summary.txt
 done
