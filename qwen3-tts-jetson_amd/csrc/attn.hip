@@ -319,6 +319,9 @@ __global__ void __launch_bounds__(256) k_attn(const AttnParams p) {
 #ifndef Q3T_ATTN_SEQ_MINB
 #define Q3T_ATTN_SEQ_MINB 2
 #endif
+#ifndef Q3T_ATTN_SEQ_NB
+#define Q3T_ATTN_SEQ_NB 2   // K/V ring depth (attn_seq.h)
+#endif
 template <int D, int R>
 __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnParams p) {
     static_assert(D == 128 && R == 2, "talker heads: D 128, 2 q heads per kv head (attn_seq.h)");
@@ -327,7 +330,7 @@ __global__ void __launch_bounds__(256, Q3T_ATTN_SEQ_MINB) k_attn_seq(const AttnP
     const int pos = p.pos[slot];
     const size_t head_off = ((size_t)slot * p.nKV + g) * p.n_ctx * D;
     const float *qkv = p.qkv + (size_t)slot * (p.nH + 2 * p.nKV) * D;
-    attn_seq_wg<false, 2>(
+    attn_seq_wg<false, Q3T_ATTN_SEQ_NB>(
         pos, p.kc + head_off, p.vc + head_off, p.rope + (size_t)pos * D, p.qn, p.kn, p.eps,
         [&](int v, float (&x)[2]) {
             const float *src = v == R + 1 ? qkv + (size_t)(p.nH + p.nKV + g) * D
